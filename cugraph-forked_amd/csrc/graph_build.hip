@@ -1,0 +1,612 @@
+// Graph construction on the GPU: edge list -> (renumbered) compressed adjacency.
+//
+// Behaviour follows the reference SG path
+//   cpp/src/c_api/graph_sg.cpp:231-330 -> create_graph_from_edgelist_impl.cuh:557-776
+//   renumber_edgelist_impl.cuh:95-452 (vertex set = sorted unique endpoints, ordered by
+//   DESCENDING major degree, stable so ties keep ascending external id)
+//   structure/detail/structure_utils.cuh:162-232 (compress + sorted adjacency lists)
+// but is implemented as two rocPRIM radix sorts over 64-bit (major << b | minor)
+// keys instead of Thrust sort/reduce_by_key chains.
+#include "capi.hpp"
+#include "prims.hpp"
+#include "schedule.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace cgx {
+
+namespace {
+
+// ---------------------------------------------------------------- kernels
+template <typename V>
+__global__ void k_dense_by_table(V* ids, size_t n, int64_t const* table, int64_t lo)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    ids[i] = static_cast<V>(table[(int64_t)ids[i] - lo]);
+}
+
+template <typename V>
+__global__ void k_table_fill(int64_t* table, V const* verts, size_t nv, int64_t lo)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
+    table[(int64_t)verts[i] - lo] = (int64_t)i;
+}
+
+// lower_bound of each id in a sorted array; writes the position (or -1 when absent)
+template <typename V>
+__global__ void k_dense_by_search(V* ids, size_t n, V const* sorted, size_t nv, int* missing)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    V x       = ids[i];
+    size_t lo = 0, hi = nv;
+    while (lo < hi) {
+      size_t mid = (lo + hi) >> 1;
+      if (sorted[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < nv && sorted[lo] == x) ids[i] = static_cast<V>(lo);
+    else {
+      ids[i] = static_cast<V>(-1);
+      if (missing) atomicAdd(missing, 1);
+    }
+  }
+}
+
+template <typename V>
+__global__ void k_count32(V const* major, size_t n, int* deg)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    atomicAdd(deg + major[i], 1);
+}
+template <typename V>
+__global__ void k_count64(V const* major, size_t n, unsigned long long* deg)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    atomicAdd(deg + major[i], 1ull);
+}
+
+template <typename V>
+__global__ void k_make_key(V const* major, V const* minor, size_t n, int b, uint64_t* key)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    key[i] = ((uint64_t)major[i] << b) | (uint64_t)minor[i];
+}
+
+template <typename V>
+__global__ void k_split_key(uint64_t const* key, size_t n, int b, V* major, V* minor)
+{
+  uint64_t mask = (b >= 64) ? ~0ull : ((1ull << b) - 1);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t k = key[i];
+    if (major) major[i] = static_cast<V>(k >> b);
+    minor[i] = static_cast<V>(k & mask);
+  }
+}
+
+template <typename V>
+__global__ void k_relabel(V* ids, size_t n, V const* new_of)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    ids[i] = new_of[ids[i]];
+}
+
+template <typename V>
+__global__ void k_inverse_perm(V const* order, size_t n, V* inv)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    inv[order[i]] = static_cast<V>(i);
+}
+
+// expand offsets into the major id of every edge
+template <typename V, typename E>
+__global__ void k_expand_majors(E const* offsets, int64_t nv, V* majors)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    for (E e = offsets[v]; e < offsets[v + 1]; ++e) majors[e] = static_cast<V>(v);
+  }
+}
+
+template <typename E, typename D>
+__global__ void k_degrees(E const* offsets, int64_t nv, D* deg)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x)
+    deg[v] = static_cast<D>(offsets[v + 1] - offsets[v]);
+}
+
+// is deg non-increasing?  flag set to 1 on any violation
+template <typename E>
+__global__ void k_check_sorted_desc(E const* offsets, int64_t nv, int* bad)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v + 1 < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    E d0 = offsets[v + 1] - offsets[v];
+    E d1 = offsets[v + 2] - offsets[v + 1];
+    if (d1 > d0) *bad = 1;
+  }
+}
+
+// bin starts: for each threshold t, first position whose degree < t (degrees non-increasing in order)
+template <typename V, typename E>
+__global__ void k_bin_starts(E const* offsets, V const* order, int64_t nv, int64_t* out)
+{
+  int b = threadIdx.x;
+  if (b >= kSchedBins) return;
+  int64_t t  = kBinLo[b];
+  int64_t lo = 0, hi = nv;
+  while (lo < hi) {  // first position with degree < t
+    int64_t mid = (lo + hi) >> 1;
+    int64_t v   = order ? (int64_t)order[mid] : mid;
+    int64_t d   = (int64_t)(offsets[v + 1] - offsets[v]);
+    if (d >= t) lo = mid + 1;
+    else hi = mid;
+  }
+  out[b] = lo;  // end of bin b (exclusive) == start of bin b+1
+}
+
+template <typename V, typename E, typename W>
+__global__ void k_row_weight_sums(E const* offsets, W const* w, int64_t nv, W* out)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0;
+    for (E e = offsets[v]; e < offsets[v + 1]; ++e) s += (double)w[e];
+    out[v] = static_cast<W>(s);
+  }
+}
+
+template <typename V, typename W>
+__global__ void k_atomic_weight_sums(V const* idx, W const* w, size_t ne, double* acc)
+{
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < ne; e += (size_t)gridDim.x * blockDim.x)
+    atomicAdd(acc + idx[e], (double)w[e]);
+}
+template <typename V>
+__global__ void k_atomic_counts(V const* idx, size_t ne, unsigned long long* acc)
+{
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < ne; e += (size_t)gridDim.x * blockDim.x)
+    atomicAdd(acc + idx[e], 1ull);
+}
+
+template <typename V>
+__global__ void k_ext_to_int(V* ids, size_t n, V const* sorted_ext, V const* internal, size_t nv, int* bad)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    V x       = ids[i];
+    size_t lo = 0, hi = nv;
+    while (lo < hi) {
+      size_t mid = (lo + hi) >> 1;
+      if (sorted_ext[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < nv && sorted_ext[lo] == x) ids[i] = internal[lo];
+    else {
+      ids[i] = static_cast<V>(-1);
+      atomicAdd(bad, 1);
+    }
+  }
+}
+template <typename V>
+__global__ void k_check_range(V const* ids, size_t n, int64_t nv, int* bad)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if (ids[i] < 0 || (int64_t)ids[i] >= nv) atomicAdd(bad, 1);
+}
+template <typename V>
+__global__ void k_int_to_ext(V* ids, size_t n, V const* nmap, int64_t nv)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    V x = ids[i];
+    if (x >= 0 && (int64_t)x < nv) ids[i] = nmap[x];
+  }
+}
+
+// ---------------------------------------------------------------- helpers
+template <typename V, typename E>
+void degrees_of(V const* majors, size_t n, int64_t nv, E* deg, hipStream_t s)
+{
+  if constexpr (sizeof(E) == 4) {
+    fill<int>(reinterpret_cast<int*>(deg), nv, 0, s);
+    if (n) {
+      hipLaunchKernelGGL(k_count32<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, majors, n,
+                         reinterpret_cast<int*>(deg));
+      CGX_LAUNCH_CHECK();
+    }
+  } else {
+    fill<unsigned long long>(reinterpret_cast<unsigned long long*>(deg), nv, 0ull, s);
+    if (n) {
+      hipLaunchKernelGGL(k_count64<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, majors, n,
+                         reinterpret_cast<unsigned long long*>(deg));
+      CGX_LAUNCH_CHECK();
+    }
+  }
+}
+
+// sort (major, minor[, w]) by (major, minor) and compress into adj
+template <typename V, typename E, typename W>
+void compress(hipStream_t s, int64_t nv, V const* majors, V const* minors, W const* w, size_t n, adjacency_t& adj)
+{
+  CGX_EXPECTS(nv <= (int64_t(1) << 32), CUGRAPH_NOT_IMPLEMENTED, "graphs with more than 2^32 vertices are not supported");
+  int b = bits_for(nv > 0 ? (unsigned long long)(nv - 1) : 0ull);
+  dbuf<uint64_t> key(n, s), key_sorted(n, s);
+  if (n) {
+    hipLaunchKernelGGL(k_make_key<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, majors, minors, n, b,
+                       key.data());
+    CGX_LAUNCH_CHECK();
+  }
+  adj.weights.set_stream(s);
+  if (w) {
+    adj.weights.resize(n * sizeof(W));
+    radix_sort_pairs<uint64_t, W>(key.data(), key_sorted.data(), w, adj.weights.data<W>(), n, 0, 2 * b, s);
+  } else {
+    adj.weights.release();
+    radix_sort_keys<uint64_t>(key.data(), key_sorted.data(), n, 0, 2 * b, s);
+  }
+  key.b.release();
+  dbuf<V> smaj(n, s);
+  adj.indices.set_stream(s);
+  adj.indices.resize(n * sizeof(V));
+  if (n) {
+    hipLaunchKernelGGL(k_split_key<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, key_sorted.data(), n, b,
+                       smaj.data(), adj.indices.data<V>());
+    CGX_LAUNCH_CHECK();
+  }
+  key_sorted.b.release();
+  dbuf<E> deg(nv + 1, s);
+  degrees_of<V, E>(smaj.data(), n, nv + 1, deg.data(), s);
+  adj.offsets.set_stream(s);
+  adj.offsets.resize((nv + 1) * sizeof(E));
+  exclusive_scan<E, E>(deg.data(), adj.offsets.data<E>(), nv + 1, s);
+  adj.sched_valid = false;
+}
+
+template <typename V, typename E, typename W>
+void build_impl(handle_t& h, graph_t& g, array_view_t const& src, array_view_t const& dst, array_view_t const* wv,
+                bool renumber)
+{
+  hipStream_t s = h.stream;
+  size_t n      = src.size;
+  dbuf<V> es(n, s), ed(n, s);
+  if (n) {
+    HIP_CHECK(hipMemcpyAsync(es.data(), src.data, n * sizeof(V), hipMemcpyDefault, s));
+    HIP_CHECK(hipMemcpyAsync(ed.data(), dst.data, n * sizeof(V), hipMemcpyDefault, s));
+  }
+  dbuf<W> ew;
+  if (wv) {
+    ew.resize(n, s);
+    if (n) HIP_CHECK(hipMemcpyAsync(ew.data(), wv->data, n * sizeof(W), hipMemcpyDefault, s));
+  }
+  auto [mn, mx] = minmax<V>(es.data(), n, s);
+  auto [mn2, mx2] = minmax<V>(ed.data(), n, s);
+  mn = std::min(mn, mn2);
+  mx = std::max(mx, mx2);
+  CGX_INPUT(n == 0 || mn >= 0, "Invalid input arguments: negative vertex id.");
+
+  V* majors = g.store_transposed ? ed.data() : es.data();
+  V* minors = g.store_transposed ? es.data() : ed.data();
+  int64_t nv = 0;
+  g.number_map.set_stream(s);
+  if (renumber) {
+    // 1. sorted unique vertex set
+    dbuf<V> all(2 * n, s), all_sorted(2 * n, s);
+    if (n) {
+      HIP_CHECK(hipMemcpyAsync(all.data(), es.data(), n * sizeof(V), hipMemcpyDeviceToDevice, s));
+      HIP_CHECK(hipMemcpyAsync(all.data() + n, ed.data(), n * sizeof(V), hipMemcpyDeviceToDevice, s));
+    }
+    int vb = bits_for((unsigned long long)std::max<long long>(mx, 0));
+    radix_sort_keys<V>(all.data(), all_sorted.data(), 2 * n, 0, vb, s);
+    dbuf<V> verts(2 * n, s);
+    dbuf<size_t> cnt(1, s);
+    if (n) {
+      size_t tmp = 0;
+      HIP_CHECK(rocprim::unique(nullptr, tmp, all_sorted.data(), verts.data(), cnt.data(), 2 * n,
+                                rocprim::equal_to<V>(), s));
+      buffer t(tmp, s);
+      HIP_CHECK(rocprim::unique(t.data(), tmp, all_sorted.data(), verts.data(), cnt.data(), 2 * n,
+                                rocprim::equal_to<V>(), s));
+      nv = (int64_t)to_host_scalar(cnt.data(), s);
+    }
+    all.b.release();
+    all_sorted.b.release();
+    // 2. dense ids (position in the sorted vertex set)
+    int64_t range = n ? (mx - mn + 1) : 0;
+    if (n && range <= std::max<int64_t>(4 * nv, 1 << 22) && range < (int64_t(1) << 31)) {
+      dbuf<int64_t> table(range, s);
+      hipLaunchKernelGGL(k_table_fill<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, table.data(),
+                         verts.data(), (size_t)nv, (int64_t)mn);
+      CGX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_dense_by_table<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, es.data(), n,
+                         table.data(), (int64_t)mn);
+      hipLaunchKernelGGL(k_dense_by_table<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, ed.data(), n,
+                         table.data(), (int64_t)mn);
+      CGX_LAUNCH_CHECK();
+    } else if (n) {
+      hipLaunchKernelGGL(k_dense_by_search<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, es.data(), n,
+                         verts.data(), (size_t)nv, nullptr);
+      hipLaunchKernelGGL(k_dense_by_search<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, ed.data(), n,
+                         verts.data(), (size_t)nv, nullptr);
+      CGX_LAUNCH_CHECK();
+    }
+    // 3. major degrees, 4. stable descending sort by degree
+    dbuf<E> deg(nv, s), deg_sorted(nv, s);
+    degrees_of<V, E>(majors, n, nv, deg.data(), s);
+    dbuf<V> ids(nv, s), order(nv, s);
+    iota<V>(ids.data(), nv, V(0), s);
+    radix_sort_pairs<E, V>(deg.data(), deg_sorted.data(), ids.data(), order.data(), nv, 0,
+                           bits_for((unsigned long long)std::max<int64_t>((int64_t)n, 1)), s, /*descending=*/true);
+    // 5. number map and relabel
+    g.number_map.resize(nv * sizeof(V));
+    gather<V, V>(g.number_map.data<V>(), verts.data(), order.data(), nv, s);
+    hipLaunchKernelGGL(k_inverse_perm<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, order.data(),
+                       (size_t)nv, ids.data());
+    CGX_LAUNCH_CHECK();
+    if (n) {
+      hipLaunchKernelGGL(k_relabel<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, es.data(), n,
+                         ids.data());
+      hipLaunchKernelGGL(k_relabel<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, ed.data(), n,
+                         ids.data());
+      CGX_LAUNCH_CHECK();
+    }
+  } else {
+    nv = n ? (int64_t)mx + 1 : 0;
+    g.number_map.resize(nv * sizeof(V));
+    iota<V>(g.number_map.data<V>(), nv, V(0), s);
+  }
+  g.num_vertices = nv;
+  g.num_edges    = (int64_t)n;
+  g.renumbered   = renumber;
+  auto adj       = std::make_shared<adjacency_t>();
+  compress<V, E, W>(s, nv, majors, minors, wv ? ew.data() : nullptr, n, *adj);
+  adj->degree_sorted = renumber;
+  if (g.store_transposed) g.in = adj;
+  else g.out = adj;
+  if (g.symmetric) {
+    g.in  = adj;
+    g.out = adj;
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+template <typename V, typename E, typename W>
+void transpose_impl(handle_t& h, graph_t& g, bool to_transposed)
+{
+  hipStream_t s          = h.stream;
+  adjacency_t& from      = to_transposed ? *g.out : *g.in;
+  int64_t nv             = g.num_vertices;
+  size_t n               = (size_t)g.num_edges;
+  dbuf<V> majors(n, s);
+  if (nv) {
+    hipLaunchKernelGGL((k_expand_majors<V, E>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s,
+                       from.offsets.data<E>(), nv, majors.data());
+    CGX_LAUNCH_CHECK();
+  }
+  auto adj = std::make_shared<adjacency_t>();
+  // new majors = old minors
+  compress<V, E, W>(s, nv, from.indices.data<V>(), majors.data(), g.weighted ? from.weights.data<W>() : nullptr, n,
+                    *adj);
+  adj->degree_sorted = false;
+  if (to_transposed) g.in = adj;
+  else g.out = adj;
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+template <typename V, typename E, typename W>
+void schedule_impl(handle_t& h, graph_t& g, adjacency_t& adj)
+{
+  hipStream_t s = h.stream;
+  int64_t nv    = g.num_vertices;
+  E const* off  = adj.offsets.data<E>();
+  bool sorted   = adj.degree_sorted;
+  if (!sorted && nv > 1) {
+    dbuf<int> bad(1, s);
+    fill<int>(bad.data(), 1, 0, s);
+    hipLaunchKernelGGL(k_check_sorted_desc<E>, dim3(grid_for(nv, kBlock, 4096)), dim3(kBlock), 0, s, off, nv,
+                       bad.data());
+    CGX_LAUNCH_CHECK();
+    sorted = to_host_scalar(bad.data(), s) == 0;
+  } else if (nv <= 1) {
+    sorted = true;
+  }
+  adj.degree_sorted = sorted;
+  adj.order.set_stream(s);
+  if (!sorted) {
+    dbuf<E> deg(nv, s), deg_sorted(nv, s);
+    hipLaunchKernelGGL((k_degrees<E, E>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off, nv, deg.data());
+    CGX_LAUNCH_CHECK();
+    dbuf<V> ids(nv, s);
+    iota<V>(ids.data(), nv, V(0), s);
+    adj.order.resize(nv * sizeof(V));
+    radix_sort_pairs<E, V>(deg.data(), deg_sorted.data(), ids.data(), adj.order.data<V>(), nv, 0,
+                           bits_for((unsigned long long)std::max<int64_t>(g.num_edges, 1)), s, true);
+  } else {
+    adj.order.release();
+  }
+  dbuf<int64_t> ends(kSchedBins, s);
+  hipLaunchKernelGGL((k_bin_starts<V, E>), dim3(1), dim3(64), 0, s, off, sorted ? nullptr : adj.order.data<V>(), nv,
+                     ends.data());
+  CGX_LAUNCH_CHECK();
+  auto hend = to_host(ends.data(), kSchedBins, s);
+  hend[kSchedBins - 1] = nv;  // degree >= 0: everything
+  adj.bin_begin.assign(kSchedBins + 1, 0);
+  for (int b = 0; b < kSchedBins; ++b) adj.bin_begin[b + 1] = hend[b];
+  // host-built work items, ~8K edges each
+  std::vector<work_item> items;
+  constexpr int64_t kTargetEdges = 8192;
+  for (int b = 0; b < kSchedBins; ++b) {
+    int64_t p0 = adj.bin_begin[b], p1 = adj.bin_begin[b + 1];
+    if (p1 <= p0) continue;
+    int w = kBinWidth[b];
+    if (w == 256) {
+      for (int64_t p = p0; p < p1; ++p) items.push_back(work_item{256, b, p, p + 1});
+      continue;
+    }
+    int64_t groups = 256 / w;
+    int64_t d_est  = std::max<int64_t>(1, kBinLo[b] + kBinLo[b] / 2);
+    int64_t rounds = std::clamp<int64_t>(kTargetEdges / (groups * d_est), 1, 64);
+    if (b == kSchedBins - 1) rounds = 16;  // zero-degree tail: pure vector epilogue
+    int64_t per = groups * rounds;
+    for (int64_t p = p0; p < p1; p += per) items.push_back(work_item{w, b, p, std::min(p1, p + per)});
+  }
+  adj.num_items = (int64_t)items.size();
+  adj.items.set_stream(s);
+  adj.items.resize(std::max<size_t>(items.size(), 1) * sizeof(work_item));
+  to_device(adj.items.data<work_item>(), items.data(), items.size(), s);
+  HIP_CHECK(hipStreamSynchronize(s));
+  adj.sched_valid = true;
+}
+
+template <typename V>
+void ext_lookup_impl(handle_t& h, graph_t& g)
+{
+  hipStream_t s = h.stream;
+  int64_t nv    = g.num_vertices;
+  g.ext_sorted.set_stream(s);
+  g.ext_internal.set_stream(s);
+  g.ext_sorted.resize(nv * sizeof(V));
+  g.ext_internal.resize(nv * sizeof(V));
+  dbuf<V> ids(nv, s);
+  iota<V>(ids.data(), nv, V(0), s);
+  auto [mn, mx] = minmax<V>(g.number_map.data<V>(), nv, s);
+  (void)mn;
+  radix_sort_pairs<V, V>(g.number_map.data<V>(), g.ext_sorted.data<V>(), ids.data(), g.ext_internal.data<V>(), nv,
+                         0, bits_for((unsigned long long)std::max<long long>(mx, 0)), s);
+  HIP_CHECK(hipStreamSynchronize(s));
+  g.ext_lookup_valid = true;
+}
+
+template <typename V, typename E, typename W>
+void outw_impl(handle_t& h, graph_t& g)
+{
+  hipStream_t s = h.stream;
+  int64_t nv    = g.num_vertices;
+  g.outw.set_stream(s);
+  g.outw.resize(std::max<int64_t>(nv, 1) * sizeof(W));
+  W* out = g.outw.data<W>();
+  if (nv == 0) return;
+  if (g.out) {
+    E const* off = g.out->offsets.data<E>();
+    if (g.weighted) {
+      hipLaunchKernelGGL((k_row_weight_sums<V, E, W>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off,
+                         g.out->weights.data<W>(), nv, out);
+    } else {
+      hipLaunchKernelGGL((k_degrees<E, W>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off, nv, out);
+    }
+    CGX_LAUNCH_CHECK();
+  } else {
+    // only in-edges stored: accumulate by source (integer counts are exact; fp64 sums
+    // round once to weight_t)
+    size_t ne    = (size_t)g.num_edges;
+    V const* idx = g.in->indices.data<V>();
+    if (g.weighted) {
+      dbuf<double> acc(nv, s);
+      fill<double>(acc.data(), nv, 0.0, s);
+      if (ne) {
+        hipLaunchKernelGGL((k_atomic_weight_sums<V, W>), dim3(grid_for(ne, kBlock, 8192)), dim3(kBlock), 0, s, idx,
+                           g.in->weights.data<W>(), ne, acc.data());
+        CGX_LAUNCH_CHECK();
+      }
+      convert<W, double>(out, acc.data(), nv, s);
+    } else {
+      dbuf<unsigned long long> acc(nv, s);
+      fill<unsigned long long>(acc.data(), nv, 0ull, s);
+      if (ne) {
+        hipLaunchKernelGGL(k_atomic_counts<V>, dim3(grid_for(ne, kBlock, 8192)), dim3(kBlock), 0, s, idx, ne,
+                           acc.data());
+        CGX_LAUNCH_CHECK();
+      }
+      convert<W, unsigned long long>(out, acc.data(), nv, s);
+    }
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  g.outw_valid = true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- public (internal API)
+void build_sg_graph(handle_t& h, graph_t& g, array_view_t const& src, array_view_t const& dst,
+                    array_view_t const* weights, bool renumber)
+{
+  dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
+    using T = decltype(t);
+    build_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, src, dst, weights, renumber);
+  });
+}
+
+adjacency_t& ensure_adjacency(handle_t& h, graph_t& g, bool transposed)
+{
+  auto& slot = transposed ? g.in : g.out;
+  if (slot) return *slot;
+  dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
+    using T = decltype(t);
+    transpose_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, transposed);
+  });
+  return *slot;
+}
+
+void ensure_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
+{
+  if (adj.sched_valid) return;
+  dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
+    using T = decltype(t);
+    schedule_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, adj);
+  });
+}
+
+void renumber_ext_to_int(handle_t& h, graph_t& g, void* ids, size_t n, bool /*check*/)
+{
+  if (!n) return;
+  hipStream_t s = h.stream;
+  dbuf<int> bad(1, s);
+  fill<int>(bad.data(), 1, 0, s);
+  auto run = [&](auto vtag) {
+    using V = decltype(vtag);
+    V* p    = static_cast<V*>(ids);
+    if (g.renumbered) {
+      if (!g.ext_lookup_valid) ext_lookup_impl<V>(h, g);
+      hipLaunchKernelGGL(k_ext_to_int<V>, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, p, n,
+                         g.ext_sorted.data<V>(), g.ext_internal.data<V>(), (size_t)g.num_vertices, bad.data());
+    } else {
+      hipLaunchKernelGGL(k_check_range<V>, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, p, n,
+                         g.num_vertices, bad.data());
+    }
+    CGX_LAUNCH_CHECK();
+  };
+  if (g.vertex_type == INT32) run(int32_t{});
+  else run(int64_t{});
+  CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: vertex id not in the graph.");
+}
+
+void unrenumber_int_to_ext(handle_t& h, graph_t& g, void* ids, size_t n)
+{
+  if (!n || !g.renumbered) return;
+  hipStream_t s = h.stream;
+  auto run      = [&](auto vtag) {
+    using V = decltype(vtag);
+    hipLaunchKernelGGL(k_int_to_ext<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, static_cast<V*>(ids), n,
+                       g.number_map.data<V>(), g.num_vertices);
+    CGX_LAUNCH_CHECK();
+  };
+  if (g.vertex_type == INT32) run(int32_t{});
+  else run(int64_t{});
+}
+
+std::unique_ptr<device_array_t> number_map_copy(handle_t& h, graph_t& g)
+{
+  auto a = std::make_unique<device_array_t>((size_t)g.num_vertices, g.vertex_type, h.stream);
+  if (g.num_vertices)
+    HIP_CHECK(hipMemcpyAsync(a->buf.data(), g.number_map.data(), g.num_vertices * dtype_size(g.vertex_type),
+                             hipMemcpyDeviceToDevice, h.stream));
+  return a;
+}
+
+void const* out_weight_sums(handle_t& h, graph_t& g)
+{
+  if (!g.outw_valid) {
+    dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
+      using T = decltype(t);
+      outw_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g);
+    });
+  }
+  return g.outw.data();
+}
+
+}  // namespace cgx

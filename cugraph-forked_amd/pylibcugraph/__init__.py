@@ -1,0 +1,257 @@
+"""pylibcugraph-compatible Python surface over the MI355X libcugraph_c.
+
+Mirrors the reference's Cython shim (``python/pylibcugraph/pylibcugraph``) for the
+hot path: ``ResourceHandle`` (resource_handle.pyx:25-46), ``GraphProperties``
+(graph_properties.pyx:17-35), ``SGGraph``/``MGGraph`` (graphs.pyx:60-330),
+``pagerank`` (pagerank.pyx:57-224), ``personalized_pagerank``
+(personalized_pagerank.pyx), ``bfs`` (bfs.pyx:59-200), ``sssp`` (sssp.pyx:52-178),
+``louvain`` (louvain.pyx:58-149) -- same argument names, order, return tuples and
+exception types.  Arrays come back as GPU torch tensors (the reference returns
+cupy arrays).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from ._arrays import DeviceArray, DeviceView, copy_view_to_tensor, optional_view, to_device_tensor, vptr
+
+from . import generators  # noqa: E402,F401  (MI355X build extensions)
+
+__all__ = ["ResourceHandle", "GraphProperties", "SGGraph", "MGGraph", "pagerank",
+           "personalized_pagerank", "bfs", "sssp", "louvain", "version"]
+
+
+def version():
+    return _lib.lib.cugraph_amd_version().decode()
+
+
+class ResourceHandle:
+    """resource_handle.pyx:25-46.  ``handle`` may be a communicator pointer
+    (``cugraph.dask.comms``) for multi-GPU use, else None."""
+
+    def __init__(self, handle=None):
+        p = None if handle is None else ctypes.c_void_p(int(handle))
+        self.c_resource_handle_ptr = _lib.lib.cugraph_create_resource_handle(p)
+        if not self.c_resource_handle_ptr:
+            raise RuntimeError("cugraph_create_resource_handle failed")
+
+    @property
+    def ptr(self):
+        return self.c_resource_handle_ptr
+
+    def get_rank(self):
+        return _lib.lib.cugraph_resource_handle_get_rank(self.c_resource_handle_ptr)
+
+    # measurement hooks (include/cugraph_amd/ext.h)
+    def set_profiling(self, enable=True):
+        _lib.lib.cugraph_amd_set_profiling(self.c_resource_handle_ptr, 1 if enable else 0)
+
+    def last_iterations(self):
+        return _lib.lib.cugraph_amd_last_iterations(self.c_resource_handle_ptr)
+
+    def last_hot_kernel_ms(self):
+        return _lib.lib.cugraph_amd_last_hot_kernel_ms(self.c_resource_handle_ptr)
+
+    def last_hot_kernel_launches(self):
+        return _lib.lib.cugraph_amd_last_hot_kernel_launches(self.c_resource_handle_ptr)
+
+    def last_bfs_levels(self):
+        return _lib.lib.cugraph_amd_last_bfs_levels(self.c_resource_handle_ptr)
+
+    def last_bfs_bottom_up_steps(self):
+        return _lib.lib.cugraph_amd_last_bfs_bottom_up_steps(self.c_resource_handle_ptr)
+
+    def last_louvain_levels(self):
+        return _lib.lib.cugraph_amd_last_louvain_levels(self.c_resource_handle_ptr)
+
+    def __del__(self):
+        p = getattr(self, "c_resource_handle_ptr", None)
+        if p:
+            _lib.lib.cugraph_free_resource_handle(p)
+            self.c_resource_handle_ptr = None
+
+
+class GraphProperties:
+    """graph_properties.pyx:17-35."""
+
+    def __init__(self, is_symmetric=False, is_multigraph=False):
+        self.is_symmetric = bool(is_symmetric)
+        self.is_multigraph = bool(is_multigraph)
+
+    def _c(self):
+        return _lib.GraphPropertiesStruct(int(self.is_symmetric), int(self.is_multigraph))
+
+    def __getnewargs_ex__(self):
+        return ((), {"is_symmetric": self.is_symmetric, "is_multigraph": self.is_multigraph})
+
+
+class _GPUGraph:
+    c_graph_ptr = None
+
+    def number_of_vertices(self):
+        return _lib.lib.cugraph_amd_graph_get_number_of_vertices(self.c_graph_ptr)
+
+    def number_of_edges(self):
+        return _lib.lib.cugraph_amd_graph_get_number_of_edges(self.c_graph_ptr)
+
+    def adjacency(self, resource_handle, transposed=False):
+        """(offsets, indices, weights|None) in internal ids (MI355X build extension)."""
+        o, i, w = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("cugraph_amd_graph_get_adjacency", resource_handle.ptr, self.c_graph_ptr,
+                  1 if transposed else 0, ctypes.byref(o), ctypes.byref(i), ctypes.byref(w))
+        h = resource_handle.ptr
+        out = (DeviceArray(o.value).to_tensor(h), DeviceArray(i.value).to_tensor(h),
+               DeviceArray(w.value).to_tensor(h) if w.value else None)
+        return out
+
+
+def _check_bool(name, v):
+    if not isinstance(v, (int, bool)):
+        raise TypeError(f"expected int or bool for {name}, got {type(v)}")
+
+
+class SGGraph(_GPUGraph):
+    """graphs.pyx:60-240."""
+
+    def __init__(self, resource_handle, graph_properties, src_array, dst_array, weight_array,
+                 store_transposed=False, renumber=False, do_expensive_check=False,
+                 edge_id_array=None, edge_type_array=None):
+        _check_bool("store_transposed", store_transposed)
+        _check_bool("renumber", renumber)
+        _check_bool("do_expensive_check", do_expensive_check)
+        if edge_id_array is not None or edge_type_array is not None:
+            raise NotImplementedError("edge ids / edge types are not supported by this build")
+        src = DeviceView(src_array)
+        dst = DeviceView(dst_array)
+        if dst.c_type != src.c_type:
+            dst = DeviceView(dst.tensor.to(src.tensor.dtype))
+        wgt = optional_view(weight_array)
+        props = graph_properties._c()
+        g = ctypes.c_void_p()
+        _lib.call("cugraph_sg_graph_create", resource_handle.ptr, ctypes.byref(props), src.ptr, dst.ptr,
+                  vptr(wgt), None, None, int(bool(store_transposed)), int(bool(renumber)),
+                  int(bool(do_expensive_check)), ctypes.byref(g))
+        self.c_graph_ptr = g.value
+        self._mg = False
+
+    def __del__(self):
+        if getattr(self, "c_graph_ptr", None):
+            _lib.lib.cugraph_sg_graph_free(self.c_graph_ptr)
+            self.c_graph_ptr = None
+
+
+class MGGraph(_GPUGraph):
+    """graphs.pyx:247-330: collective over the communicator in the handle."""
+
+    def __init__(self, resource_handle, graph_properties, src_array, dst_array, weight_array,
+                 store_transposed=False, num_edges=-1, do_expensive_check=False,
+                 edge_id_array=None, edge_type_array=None):
+        _check_bool("store_transposed", store_transposed)
+        src = DeviceView(src_array)
+        dst = DeviceView(dst_array, src.tensor.dtype)
+        wgt = optional_view(weight_array)
+        if num_edges < 0:
+            raise ValueError("num_edges (global edge count) is required for MGGraph")
+        props = graph_properties._c()
+        g = ctypes.c_void_p()
+        _lib.call("cugraph_mg_graph_create", resource_handle.ptr, ctypes.byref(props), src.ptr, dst.ptr,
+                  vptr(wgt), None, None, int(bool(store_transposed)), int(num_edges),
+                  int(bool(do_expensive_check)), ctypes.byref(g))
+        self.c_graph_ptr = g.value
+        self._mg = True
+
+    def __del__(self):
+        if getattr(self, "c_graph_ptr", None):
+            _lib.lib.cugraph_mg_graph_free(self.c_graph_ptr)
+            self.c_graph_ptr = None
+
+
+def _centrality(api, resource_handle, graph, *views_and_scalars):
+    res = ctypes.c_void_p()
+    _lib.call(api, resource_handle.ptr, graph.c_graph_ptr, *views_and_scalars, ctypes.byref(res))
+    h = resource_handle.ptr
+    try:
+        v = copy_view_to_tensor(h, _lib.lib.cugraph_centrality_result_get_vertices(res))
+        x = copy_view_to_tensor(h, _lib.lib.cugraph_centrality_result_get_values(res))
+    finally:
+        _lib.lib.cugraph_centrality_result_free(res)
+    return v, x
+
+
+def pagerank(resource_handle, graph, precomputed_vertex_out_weight_vertices,
+             precomputed_vertex_out_weight_sums, initial_guess_vertices, initial_guess_values,
+             alpha, epsilon, max_iterations, do_expensive_check):
+    """pagerank.pyx:57-224.  Returns (vertices, pageranks)."""
+    a = optional_view(precomputed_vertex_out_weight_vertices)
+    b = optional_view(precomputed_vertex_out_weight_sums)
+    c = optional_view(initial_guess_vertices)
+    d = optional_view(initial_guess_values)
+    return _centrality("cugraph_pagerank", resource_handle, graph, vptr(a), vptr(b), vptr(c), vptr(d),
+                       float(alpha), float(epsilon), int(max_iterations), int(bool(do_expensive_check)))
+
+
+def personalized_pagerank(resource_handle, graph, precomputed_vertex_out_weight_vertices,
+                          precomputed_vertex_out_weight_sums, initial_guess_vertices,
+                          initial_guess_values, personalization_vertices, personalization_values,
+                          alpha, epsilon, max_iterations, do_expensive_check):
+    """personalized_pagerank.pyx.  Returns (vertices, pageranks)."""
+    a = optional_view(precomputed_vertex_out_weight_vertices)
+    b = optional_view(precomputed_vertex_out_weight_sums)
+    c = optional_view(initial_guess_vertices)
+    d = optional_view(initial_guess_values)
+    e = optional_view(personalization_vertices)
+    f = optional_view(personalization_values)
+    return _centrality("cugraph_personalized_pagerank", resource_handle, graph, vptr(a), vptr(b), vptr(c),
+                       vptr(d), vptr(e), vptr(f), float(alpha), float(epsilon), int(max_iterations),
+                       int(bool(do_expensive_check)))
+
+
+def _paths(resource_handle, res):
+    h = resource_handle.ptr
+    try:
+        v = copy_view_to_tensor(h, _lib.lib.cugraph_paths_result_get_vertices(res))
+        d = copy_view_to_tensor(h, _lib.lib.cugraph_paths_result_get_distances(res))
+        p = copy_view_to_tensor(h, _lib.lib.cugraph_paths_result_get_predecessors(res))
+    finally:
+        _lib.lib.cugraph_paths_result_free(res)
+    return v, d, p
+
+
+def bfs(handle, graph, sources, direction_optimizing, depth_limit, compute_predecessors,
+        do_expensive_check):
+    """bfs.pyx:59-200.  depth_limit <= 0 means unlimited (bfs.pyx:148-149).
+    Returns (distances, predecessors, vertices)."""
+    # the library renumbers sources in place (bfs.cpp:96-114): hand it a private copy
+    src = DeviceView(to_device_tensor(sources).clone())
+    if depth_limit is None or depth_limit <= 0:
+        depth_limit = 2 ** 31 - 2
+    res = ctypes.c_void_p()
+    _lib.call("cugraph_bfs", handle.ptr, graph.c_graph_ptr, src.ptr, int(bool(direction_optimizing)),
+              int(depth_limit), int(bool(compute_predecessors)), int(bool(do_expensive_check)),
+              ctypes.byref(res))
+    v, d, p = _paths(handle, res)
+    return d, p, v
+
+
+def sssp(resource_handle, graph, source, cutoff, compute_predecessors, do_expensive_check):
+    """sssp.pyx:52-178.  Returns (vertices, distances, predecessors)."""
+    res = ctypes.c_void_p()
+    _lib.call("cugraph_sssp", resource_handle.ptr, graph.c_graph_ptr, int(source), float(cutoff),
+              int(bool(compute_predecessors)), int(bool(do_expensive_check)), ctypes.byref(res))
+    return _paths(resource_handle, res)
+
+
+def louvain(resource_handle, graph, max_level, resolution, do_expensive_check):
+    """louvain.pyx:58-149.  Returns (vertices, clusters, modularity)."""
+    res = ctypes.c_void_p()
+    _lib.call("cugraph_louvain", resource_handle.ptr, graph.c_graph_ptr, int(max_level), float(resolution),
+              int(bool(do_expensive_check)), ctypes.byref(res))
+    h = resource_handle.ptr
+    try:
+        v = copy_view_to_tensor(h, _lib.lib.cugraph_heirarchical_clustering_result_get_vertices(res))
+        c = copy_view_to_tensor(h, _lib.lib.cugraph_heirarchical_clustering_result_get_clusters(res))
+        q = _lib.lib.cugraph_heirarchical_clustering_result_get_modularity(res)
+    finally:
+        _lib.lib.cugraph_heirarchical_clustering_result_free(res)
+    return v, c, q

@@ -1,0 +1,130 @@
+"""Device-array plumbing between Python objects and libcugraph_c views.
+
+The reference accepts ``__cuda_array_interface__`` objects (cupy/cudf) and returns
+cupy arrays (``utils.pyx:150-184``).  cupy/cudf do not exist on ROCm here, so
+this build accepts torch tensors (any device), numpy arrays / lists / pandas
+Series (copied to HBM) and ``__cuda_array_interface__`` objects, and returns
+torch tensors resident on the GPU.  torch is plumbing only: every computation
+happens in libcugraph_c.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+_NP_TO_C = {np.dtype(np.int32): _lib.INT32, np.dtype(np.int64): _lib.INT64,
+            np.dtype(np.float32): _lib.FLOAT32, np.dtype(np.float64): _lib.FLOAT64}
+_C_TO_NP = {v: k for k, v in _NP_TO_C.items()}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _torch_dtype(c_type):
+    torch = _torch()
+    return {_lib.INT32: torch.int32, _lib.INT64: torch.int64,
+            _lib.FLOAT32: torch.float32, _lib.FLOAT64: torch.float64}[c_type]
+
+
+def _c_type_of_torch(t):
+    torch = _torch()
+    m = {torch.int32: _lib.INT32, torch.int64: _lib.INT64,
+         torch.float32: _lib.FLOAT32, torch.float64: _lib.FLOAT64}
+    if t.dtype not in m:
+        raise TypeError(f"unsupported dtype {t.dtype}")
+    return m[t.dtype]
+
+
+def to_device_tensor(arr, dtype=None):
+    """Return a contiguous GPU torch tensor for ``arr`` (no copy if already one)."""
+    torch = _torch()
+    if isinstance(arr, torch.Tensor):
+        t = arr
+    elif hasattr(arr, "__cuda_array_interface__") and not isinstance(arr, np.ndarray):
+        t = torch.as_tensor(arr, device="cuda")
+    else:
+        if hasattr(arr, "to_numpy"):
+            arr = arr.to_numpy()
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(arr)))
+    if dtype is not None:
+        t = t.to(dtype)
+    if not t.is_cuda:
+        t = t.to("cuda")
+    return t.contiguous()
+
+
+class DeviceView:
+    """Owns a ``cugraph_type_erased_device_array_view_t*`` plus the tensor it wraps."""
+
+    def __init__(self, arr, dtype=None):
+        self.tensor = to_device_tensor(arr, dtype)
+        self.c_type = _c_type_of_torch(self.tensor)
+        self.ptr = _lib.lib.cugraph_type_erased_device_array_view_create(
+            ctypes.c_void_p(self.tensor.data_ptr()), self.tensor.numel(), self.c_type)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            _lib.lib.cugraph_type_erased_device_array_view_free(self.ptr)
+            self.ptr = None
+
+
+def optional_view(arr, dtype=None):
+    return None if arr is None else DeviceView(arr, dtype)
+
+
+def vptr(v):
+    return None if v is None else v.ptr
+
+
+def copy_view_to_tensor(handle_ptr, view_ptr, free_view=True):
+    """utils.pyx:150-184 copy_to_cupy_array, returning a torch tensor on the GPU."""
+    torch = _torch()
+    c_type = _lib.lib.cugraph_type_erased_device_array_view_type(view_ptr)
+    n = _lib.lib.cugraph_type_erased_device_array_view_size(view_ptr)
+    out = torch.empty(n, dtype=_torch_dtype(c_type), device="cuda")
+    dst = _lib.lib.cugraph_type_erased_device_array_view_create(ctypes.c_void_p(out.data_ptr()), n, c_type)
+    try:
+        _lib.call("cugraph_type_erased_device_array_view_copy", handle_ptr, dst, view_ptr)
+    finally:
+        _lib.lib.cugraph_type_erased_device_array_view_free(dst)
+        if free_view:
+            _lib.lib.cugraph_type_erased_device_array_view_free(view_ptr)
+    return out
+
+
+def copy_view_to_numpy(handle_ptr, view_ptr):
+    c_type = _lib.lib.cugraph_type_erased_device_array_view_type(view_ptr)
+    n = _lib.lib.cugraph_type_erased_device_array_view_size(view_ptr)
+    out = np.empty(n, dtype=_C_TO_NP[c_type])
+    _lib.call("cugraph_type_erased_device_array_view_copy_to_host", handle_ptr,
+              out.ctypes.data_as(ctypes.c_void_p), view_ptr)
+    return out
+
+
+class DeviceArray:
+    """Owning ``cugraph_type_erased_device_array_t*`` returned by the extensions."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def view(self):
+        return _lib.lib.cugraph_type_erased_device_array_view(self.ptr)
+
+    def to_tensor(self, handle_ptr):
+        return copy_view_to_tensor(handle_ptr, self.view())
+
+    def __len__(self):
+        v = self.view()
+        n = _lib.lib.cugraph_type_erased_device_array_view_size(v)
+        _lib.lib.cugraph_type_erased_device_array_view_free(v)
+        return n
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            _lib.lib.cugraph_type_erased_device_array_free(self.ptr)
+            self.ptr = None

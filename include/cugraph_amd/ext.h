@@ -1,0 +1,101 @@
+/*
+ * MI355X build extensions around the libcugraph_c boundary.
+ *
+ * These are the data formats either side of the hot path that the reference
+ * provides through other layers (RAFT's R-MAT generator behind
+ * cugraph.generators.rmat, cudf-based symmetrize/dedup behind
+ * cugraph.Graph.from_cudf_edgelist) plus measurement hooks.  Nothing here is
+ * needed by a caller that only uses the reference ABI.
+ */
+#pragma once
+#include <cugraph_c/algorithms.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * Counter-based Graph500 R-MAT edge generator (definition in oracle/rmat.py;
+ * role of the reference cpp/src/generators/generate_rmat_edgelist.cu:36-103).
+ * Edges [first_edge, first_edge + num_edges) of the stream for `seed`.
+ * vertex_dtype: INT32 or INT64.
+ */
+cugraph_error_code_t cugraph_amd_generate_rmat_edgelist(const cugraph_resource_handle_t* handle,
+                                                        size_t scale,
+                                                        size_t num_edges,
+                                                        double a,
+                                                        double b,
+                                                        double c,
+                                                        uint64_t seed,
+                                                        bool_t clip_and_flip,
+                                                        bool_t scramble_vertex_ids,
+                                                        size_t first_edge,
+                                                        data_type_id_t vertex_dtype,
+                                                        cugraph_type_erased_device_array_t** src,
+                                                        cugraph_type_erased_device_array_t** dst,
+                                                        cugraph_error_t** error);
+
+/* Uniform [0,1) edge weights, 24-bit exact (oracle/rmat.py rmat_weights). */
+cugraph_error_code_t cugraph_amd_generate_edge_weights(const cugraph_resource_handle_t* handle,
+                                                       size_t num_edges,
+                                                       uint64_t seed,
+                                                       size_t first_edge,
+                                                       data_type_id_t weight_dtype,
+                                                       cugraph_type_erased_device_array_t** weights,
+                                                       cugraph_error_t** error);
+
+/*
+ * cugraph.Graph edge-list preprocessing on the device
+ * (python/cugraph/cugraph/structure/symmetrize.py:78-93): optionally append
+ * reversed edges, then drop duplicate (src, dst) pairs keeping the minimum
+ * weight.  Output is sorted by (src, dst).  weights may be NULL.
+ */
+cugraph_error_code_t cugraph_amd_symmetrize_dedup(const cugraph_resource_handle_t* handle,
+                                                  const cugraph_type_erased_device_array_view_t* src,
+                                                  const cugraph_type_erased_device_array_view_t* dst,
+                                                  const cugraph_type_erased_device_array_view_t* weights,
+                                                  bool_t symmetrize,
+                                                  cugraph_type_erased_device_array_t** src_out,
+                                                  cugraph_type_erased_device_array_t** dst_out,
+                                                  cugraph_type_erased_device_array_t** weights_out,
+                                                  cugraph_error_t** error);
+
+/* Graph introspection (vertex count after renumbering, stored edge count). */
+int64_t cugraph_amd_graph_get_number_of_vertices(const cugraph_graph_t* graph);
+int64_t cugraph_amd_graph_get_number_of_edges(const cugraph_graph_t* graph);
+bool_t cugraph_amd_graph_is_symmetric(const cugraph_graph_t* graph);
+
+/*
+ * Copy the graph's compressed adjacency to caller device buffers (for tests):
+ * transposed=FALSE gives CSR (out-edges), TRUE gives CSC (in-edges), in the
+ * graph's internal (renumbered) ids.  Pass NULL to query sizes only.
+ */
+cugraph_error_code_t cugraph_amd_graph_get_adjacency(const cugraph_resource_handle_t* handle,
+                                                     cugraph_graph_t* graph,
+                                                     bool_t transposed,
+                                                     cugraph_type_erased_device_array_t** offsets,
+                                                     cugraph_type_erased_device_array_t** indices,
+                                                     cugraph_type_erased_device_array_t** weights,
+                                                     cugraph_error_t** error);
+
+/*
+ * Measurement hooks.  When profiling is on, algorithms record HIP events
+ * around every launch of their dominant kernel (on the handle's stream) and
+ * keep the total; stats are per handle and reset by each algorithm call.
+ */
+void cugraph_amd_set_profiling(cugraph_resource_handle_t* handle, bool_t enable);
+size_t cugraph_amd_last_iterations(const cugraph_resource_handle_t* handle);
+double cugraph_amd_last_hot_kernel_ms(const cugraph_resource_handle_t* handle);
+size_t cugraph_amd_last_hot_kernel_launches(const cugraph_resource_handle_t* handle);
+/* BFS: edges examined, levels, top-down/bottom-up steps of the last call */
+size_t cugraph_amd_last_bfs_levels(const cugraph_resource_handle_t* handle);
+size_t cugraph_amd_last_bfs_bottom_up_steps(const cugraph_resource_handle_t* handle);
+/* Louvain: levels of the last call */
+size_t cugraph_amd_last_louvain_levels(const cugraph_resource_handle_t* handle);
+
+/* Library build string, e.g. "cugraph-forked_amd gfx950 <date>". */
+const char* cugraph_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif

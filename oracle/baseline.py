@@ -1,0 +1,67 @@
+"""CPU baselines timed by bench.py (TEST INFRASTRUCTURE ONLY -- see oracle/__init__.py).
+
+The reference's CPU path for PageRank is NetworkX (``nx.pagerank`` ->
+``_pagerank_scipy``, networkx 3.4.2): a scipy CSR matrix and the power
+iteration ``x = alpha*(x@A + sum(x[dangling])*p) + (1-alpha)*p`` in float64,
+single-threaded.  ``pagerank_scipy_iterations`` restates exactly that loop body
+on an already-built CSR (graph construction excluded, as the GPU timing
+excludes it), for a fixed number of iterations so the sample is bounded.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+
+def pagerank_scipy_iterations(offsets, indices, num_vertices, iterations=5, alpha=0.85):
+    """Time `iterations` NetworkX-style power iterations on the pull CSR
+    (row v lists in-neighbours u).  Returns (seconds, edges_per_second)."""
+    import scipy.sparse as sp
+
+    V = int(num_vertices)
+    E = int(indices.shape[0])
+    offsets = np.asarray(offsets, dtype=np.int64)
+    indices = np.asarray(indices, dtype=np.int64)
+    outdeg = np.bincount(indices, minlength=V).astype(np.float64)
+    data = np.ones(E, dtype=np.float64)
+    # row-stochastic A[u, v] = 1/outdeg(u) for u -> v, stored as its transpose (rows = v)
+    AT = sp.csr_matrix((data / outdeg[indices], indices, offsets), shape=(V, V))
+    x = np.full(V, 1.0 / V)
+    p = np.full(V, 1.0 / V)
+    dangling = np.nonzero(outdeg == 0)[0]
+    t0 = time.perf_counter()
+    for _ in range(iterations):
+        x = alpha * (AT @ x + x[dangling].sum() * p) + (1 - alpha) * p
+    t = time.perf_counter() - t0
+    return t, E * iterations / t
+
+
+def bfs_numpy(offsets, indices, source, max_levels=1 << 30):
+    """Level-synchronous numpy BFS (oracle/bfs.py without predecessors).
+    Returns (seconds, reached_edges)."""
+    offsets = np.asarray(offsets, dtype=np.int64)
+    indices = np.asarray(indices)
+    V = offsets.shape[0] - 1
+    dist = np.full(V, -1, dtype=np.int32)
+    dist[source] = 0
+    frontier = np.array([source], dtype=np.int64)
+    t0 = time.perf_counter()
+    depth = 0
+    while frontier.size and depth < max_levels:
+        deg = offsets[frontier + 1] - offsets[frontier]
+        tot = int(deg.sum())
+        if tot == 0:
+            break
+        start = np.repeat(offsets[frontier], deg)
+        local = np.arange(tot, dtype=np.int64) - np.repeat(np.cumsum(deg) - deg, deg)
+        nb = indices[start + local]
+        nb = nb[dist[nb] < 0]
+        nb = np.unique(nb)
+        dist[nb] = depth + 1
+        frontier = nb.astype(np.int64)
+        depth += 1
+    t = time.perf_counter() - t0
+    reached = dist >= 0
+    edges = int((offsets[1:] - offsets[:-1])[reached].sum())
+    return t, edges

@@ -1,0 +1,146 @@
+"""PageRank parity: HIP path (through the C ABI) vs the oracle and the reference's
+golden vectors.  Tolerance: 1e-6 relative vs the fp64 oracle (north_star)."""
+import numpy as np
+import pytest
+
+from conftest import dataset_path
+from gpu_util import host, make_graph, plc
+from oracle import graph as og
+from oracle import pagerank as opr
+from oracle import rmat
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-6
+
+
+def by_ext(vertices, values):
+    v, x = host(vertices), host(values)
+    out = np.empty(v.max() + 1 if v.size else 0, dtype=np.float64)
+    out[v] = x
+    return out
+
+
+@pytest.mark.parametrize("case", ["pagerank_c_6v", "pagerank_c_4path"])
+@pytest.mark.parametrize("transposed", [True, False])
+def test_c_golden(golden, case, transposed):
+    g = golden[case]
+    h, G = make_graph(g["src"], g["dst"], g["w"], transposed=transposed, renumber=False)
+    v, pr = plc().pagerank(h, G, None, None, None, None, g["alpha"], g["epsilon"], g["max_iterations"], False)
+    got = by_ext(v, pr)
+    exp = np.asarray(g["expected"])
+    assert np.all(np.abs(got - exp) <= g["tol"] * np.maximum(np.abs(got), np.abs(exp)))
+    ref = opr.pagerank(g["num_vertices"], g["src"], g["dst"], np.asarray(g["w"], np.float32).astype(np.float64),
+                       g["alpha"], g["epsilon"], g["max_iterations"])
+    assert np.max(np.abs(got - ref) / ref) < REL
+
+
+def test_c_golden_personalized(golden):
+    g = golden["pagerank_c_personalized"]
+    h, G = make_graph(g["src"], g["dst"], g["w"], transposed=True, renumber=False)
+    v, pr = plc().personalized_pagerank(h, G, None, None, None, None,
+                                        np.asarray(g["personalization_vertices"], np.int32),
+                                        np.asarray(g["personalization_values"], np.float32),
+                                        g["alpha"], g["epsilon"], g["max_iterations"], False)
+    got = by_ext(v, pr)
+    exp = np.asarray(g["expected"])
+    assert np.all(np.abs(got - exp) <= g["tol"] * np.maximum(np.abs(got), np.abs(exp)))
+
+
+@pytest.mark.parametrize("name", ["karate.csv", "dolphins.csv"])
+def test_pylib_golden(golden, name):
+    p = golden["pagerank_pylib"]
+    s, d, w = og.read_csv(dataset_path(name))
+    h, G = make_graph(s, d, w, transposed=True, renumber=False)
+    v, pr = plc().pagerank(h, G, None, None, None, None, p["alpha"], p["epsilon"], p["max_iterations"], False)
+    got = by_ext(v, pr)
+    assert got == pytest.approx(np.asarray(p[name]), rel=1e-4)
+
+
+def test_not_converged_raises():
+    h, G = make_graph([0, 1, 2], [1, 2, 0], None, transposed=True, renumber=False)
+    with pytest.raises(RuntimeError, match="failed to converge"):
+        plc().pagerank(h, G, None, None, None, None, 0.85, 0.0, 3, False)
+
+
+def test_invalid_alpha():
+    h, G = make_graph([0, 1], [1, 0], None, transposed=True)
+    with pytest.raises(ValueError, match="alpha"):
+        plc().pagerank(h, G, None, None, None, None, 1.5, 1e-6, 100, False)
+
+
+def rmat_graph(scale, weighted, symmetric=True, seed=42):
+    s, d = rmat.rmat(scale, 16 << scale, seed=seed)
+    w = rmat.rmat_weights(s.size, seed=seed + 1).astype(np.float64) if weighted else None
+    if symmetric:
+        s, d, w = og.symmetrize_dedup(s, d, w)
+    return s, d, w
+
+
+@pytest.mark.parametrize("scale,weighted,symmetric,renumber,transposed",
+                         [(10, False, True, True, True), (12, False, True, True, True),
+                          (12, True, True, True, True), (12, False, False, True, True),
+                          (12, True, False, False, False), (13, False, True, False, True)])
+def test_rmat_vs_oracle(scale, weighted, symmetric, renumber, transposed):
+    s, d, w = rmat_graph(scale, weighted, symmetric)
+    h, G = make_graph(s, d, None if w is None else w.astype(np.float32), transposed=transposed,
+                      renumber=renumber, symmetric=symmetric)
+    v, pr = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+    # oracle on the same vertex set
+    og_g = og.create_graph(s, d, None if w is None else w.astype(np.float32), store_transposed=True,
+                           renumber=renumber)
+    ref = opr.pagerank_from_graph(og_g, alpha=0.85, epsilon=1e-6, max_iterations=500)
+    ref_ext = np.zeros(int(og_g.number_map.max()) + 1)
+    ref_ext[og_g.number_map] = ref
+    got = by_ext(v, pr)
+    vv = host(v)
+    assert vv.size == og_g.num_vertices
+    rel = np.abs(got[vv] - ref_ext[vv]) / ref_ext[vv]
+    assert rel.max() < REL, rel.max()
+    assert abs(got[vv].sum() - 1.0) < 1e-5
+
+
+def test_rmat_float64_and_int64():
+    s, d, w = rmat_graph(11, True)
+    h, G = make_graph(s, d, w, transposed=True, renumber=True, symmetric=True, vdtype=np.int64,
+                      wdtype=np.float64)
+    v, pr = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-10, 1000, False)
+    assert pr.dtype.is_floating_point and str(pr.dtype) == "torch.float64"
+    og_g = og.create_graph(s, d, w, store_transposed=True, renumber=True)
+    ref = opr.pagerank_from_graph(og_g, alpha=0.85, epsilon=1e-10, max_iterations=1000)
+    ref_ext = np.zeros(int(og_g.number_map.max()) + 1)
+    ref_ext[og_g.number_map] = ref
+    vv = host(v)
+    got = by_ext(v, pr)
+    assert np.max(np.abs(got[vv] - ref_ext[vv]) / ref_ext[vv]) < 1e-9
+
+
+def test_initial_guess_and_precomputed_outw():
+    s, d, _ = rmat_graph(10, False)
+    h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
+    v0, pr0 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-8, 500, False)
+    it_cold = h.last_iterations()
+    # warm start from the converged answer converges at once
+    v1, pr1 = plc().pagerank(h, G, None, None, v0, pr0, 0.85, 1e-6, 500, False)
+    assert h.last_iterations() <= 2 < it_cold
+    outw = np.bincount(s, minlength=int(max(s.max(), d.max())) + 1).astype(np.float32)
+    verts = np.unique(np.concatenate([s, d])).astype(np.int32)
+    v2, pr2 = plc().pagerank(h, G, verts, outw[verts], None, None, 0.85, 1e-8, 500, False)
+    a, b = by_ext(v0, pr0), by_ext(v2, pr2)
+    assert np.allclose(a, b, rtol=1e-6, atol=0)
+
+
+def test_repeat_is_bitwise_deterministic():
+    s, d, _ = rmat_graph(12, False)
+    h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
+    r1 = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    r2 = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    assert np.array_equal(r1, r2)
+
+
+def test_empty_and_edgeless_graph():
+    h, G = make_graph([0, 3], [0, 3], None, transposed=True, renumber=False)  # self loops only
+    v, pr = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 100, False)
+    got = by_ext(v, pr)
+    ref = opr.pagerank(4, [0, 3], [0, 3], None, 0.85, 1e-6, 100)
+    assert np.allclose(got, ref, rtol=1e-6)
