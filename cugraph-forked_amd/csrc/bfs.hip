@@ -1,0 +1,541 @@
+// Breadth-first search, direction-optimising (single GPU).
+//
+// Reference semantics: cpp/src/traversal/bfs_impl.cuh:94-287 (+ c_api/bfs.cpp:60-145):
+// distances INT_MAX / predecessors -1 for unreached vertices, every source at 0,
+// level-synchronous, stop on an empty frontier or depth >= depth_limit.  The
+// reference only implements top-down ("direction_optimizing ... unimplemented",
+// bfs_impl.cuh:206-207) and lets atomicOr winners pick predecessors; this build:
+//
+//  * top-down step (frontier queues): frontier vertices are kept in three queues
+//    by degree class (<=16: 4 lanes, <=1024: one wave, larger: one block), so the
+//    expansion is load-balanced without a per-level scan; discovered vertices are
+//    claimed with a CAS on the distance and appended to the next queues with a
+//    64-lane __ballot/popcount compaction (one atomic per wave and class).
+//  * bottom-up step (frontier bitmap, symmetric graphs): every unvisited vertex
+//    scans its sorted adjacency in lane groups (degree-binned schedule, as the
+//    PageRank kernel) and stops at the first neighbour in the frontier bitmap
+//    (the bitmap is V/8 bytes: L2/Infinity-Cache resident).
+//  * Beamer switching (alpha = 14, beta = 24) from per-level counters.
+//  * predecessor = the frontier neighbour with the smallest internal id in both
+//    directions (atomicMin top-down, first hit in the sorted list bottom-up), so
+//    results are deterministic and independent of the direction schedule.
+#include "capi.hpp"
+#include "prims.hpp"
+#include "schedule.hpp"
+
+#include <limits>
+
+namespace cgx {
+
+namespace {
+
+constexpr int kSmallDeg = 16;    // 4-lane groups
+constexpr int kMidDeg   = 1024;  // one wave; above: one block
+
+struct bfs_ctr {
+  unsigned long long qlen[3];  // next queues: small / mid / large
+  unsigned long long next_n;   // vertices discovered this level
+  unsigned long long next_m;   // sum of their degrees
+  unsigned long long pad[3];
+};
+
+template <typename V>
+__device__ __forceinline__ bool cas_claim(V* dist, V v, V nd)
+{
+  if constexpr (sizeof(V) == 4) {
+    return atomicCAS(reinterpret_cast<int*>(dist + v), (int)std::numeric_limits<int32_t>::max(), (int)nd) ==
+           std::numeric_limits<int32_t>::max();
+  } else {
+    unsigned long long inf = (unsigned long long)std::numeric_limits<int64_t>::max();
+    return atomicCAS(reinterpret_cast<unsigned long long*>(dist + v), inf, (unsigned long long)nd) == inf;
+  }
+}
+
+template <typename V>
+__device__ __forceinline__ void atomic_min_v(V* p, V x)
+{
+  if constexpr (sizeof(V) == 4) atomicMin(reinterpret_cast<int*>(p), (int)x);
+  else atomicMin(reinterpret_cast<long long*>(p), (long long)x);
+}
+
+// wave-aggregated append: every active lane with `take` gets a distinct slot
+__device__ __forceinline__ long long wave_append(unsigned long long* tail, bool take)
+{
+  unsigned long long mask = __ballot(take);
+  if (mask == 0) return -1;
+  int lane   = threadIdx.x & 63;
+  int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(tail, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  if (!take) return -1;
+  return (long long)(base + __popcll(mask & ((1ull << lane) - 1ull)));
+}
+
+template <typename V, typename E>
+struct bfs_args {
+  E const* off;
+  V const* idx;
+  V* dist;
+  V* pred;  // nullptr when predecessors are not requested
+  uint32_t* vis;
+  uint32_t* fr;   // bottom-up: current frontier bitmap
+  uint32_t* nxt;  // bottom-up: next frontier bitmap
+  V const* qcur[3];
+  unsigned long long ncur[3];
+  V* qnext[3];
+  bfs_ctr* ctr;
+  V depth;  // distance of the current frontier
+  int64_t nv;
+  V const* order;
+  work_item const* items;
+  long long blk_mid_start, blk_small_start;  // top-down grid segmentation
+};
+
+template <typename V, typename E>
+__device__ __forceinline__ void push_next(bfs_args<V, E> const& a, V v, bool take, unsigned long long& my_m)
+{
+  int cls = 0;
+  E deg   = 0;
+  if (take) {
+    deg = a.off[v + 1] - a.off[v];
+    cls = deg <= kSmallDeg ? 0 : (deg <= kMidDeg ? 1 : 2);
+    my_m += (unsigned long long)deg;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    long long slot = wave_append(&a.ctr->qlen[c], take && cls == c);
+    if (slot >= 0) a.qnext[c][slot] = v;
+  }
+}
+
+template <typename V, typename E>
+__device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, V u, V v, bool active, unsigned long long& my_m)
+{
+  bool take = false;
+  if (active) {
+    uint32_t bit = 1u << (uint32_t(v) & 31u);
+    if (!(a.vis[v >> 5] & bit)) {  // not visited before this level
+      if (a.pred) atomic_min_v<V>(a.pred + v, u);
+      take = cas_claim<V>(a.dist, v, (V)(a.depth + 1));
+    }
+  }
+  push_next<V, E>(a, v, take, my_m);
+}
+
+__device__ __forceinline__ void flush_counts(bfs_ctr* ctr, unsigned long long n, unsigned long long m)
+{
+  __shared__ unsigned long long sn[4], sm_[4];
+  unsigned long long wn = 0, wm = 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_xor(n, o, 64);
+    m += __shfl_xor(m, o, 64);
+  }
+  wn = n;
+  wm = m;
+  int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    sn[wid]  = wn;
+    sm_[wid] = wm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tn = sn[0] + sn[1] + sn[2] + sn[3];
+    unsigned long long tm = sm_[0] + sm_[1] + sm_[2] + sm_[3];
+    if (tn) atomicAdd(&ctr->next_n, tn);
+    if (tm) atomicAdd(&ctr->next_m, tm);
+  }
+}
+
+// top-down: blocks [0, mid_start) -> large queue (block per vertex),
+// [mid_start, small_start) -> mid queue (wave per vertex, 4 per block),
+// [small_start, grid) -> small queue (4 lanes per vertex, 64 per block)
+template <typename V, typename E>
+__global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
+{
+  unsigned long long my_m = 0, my_n = 0;
+  long long b = blockIdx.x;
+  int tid     = threadIdx.x;
+  if (b < a.blk_mid_start) {
+    for (long long i = b; i < (long long)a.ncur[2]; i += a.blk_mid_start) {
+      V u    = a.qcur[2][i];
+      E beg  = a.off[u], end = a.off[u + 1];
+      for (E base = beg; base < end; base += 256) {
+        E e = base + tid;
+        bool act = e < end;
+        V v      = act ? a.idx[e] : V(0);
+        unsigned long long m0 = my_m;
+        visit_edge<V, E>(a, u, v, act, my_m);
+        (void)m0;
+      }
+    }
+  } else if (b < a.blk_small_start) {
+    long long nb   = a.blk_small_start - a.blk_mid_start;
+    long long widx = (b - a.blk_mid_start) * 4 + (tid >> 6);
+    int lane       = tid & 63;
+    for (long long i = widx; i < (long long)a.ncur[1]; i += nb * 4) {
+      V u   = a.qcur[1][i];
+      E beg = a.off[u], end = a.off[u + 1];
+      for (E base = beg; base < end; base += 64) {
+        E e      = base + lane;
+        bool act = e < end;
+        V v      = act ? a.idx[e] : V(0);
+        visit_edge<V, E>(a, u, v, act, my_m);
+      }
+    }
+  } else {
+    long long nb  = gridDim.x - a.blk_small_start;
+    long long g   = (b - a.blk_small_start) * 64 + (tid >> 2);
+    int lane      = tid & 3;
+    // all 4 lanes of a group share u; lanes of a wave run the same trip count (<= 4 rounds)
+    for (long long i0 = (b - a.blk_small_start) * 64; i0 < (long long)a.ncur[0]; i0 += nb * 64) {
+      long long i = i0 + (tid >> 2);
+      bool have   = i < (long long)a.ncur[0];
+      V u         = have ? a.qcur[0][i] : V(0);
+      E beg = have ? a.off[u] : E(0), end = have ? a.off[u + 1] : E(0);
+      for (int r = 0; r < kSmallDeg / 4; ++r) {
+        E e      = beg + r * 4 + lane;
+        bool act = e < end;
+        V v      = act ? a.idx[e] : V(0);
+        visit_edge<V, E>(a, u, v, act, my_m);
+      }
+    }
+    (void)g;
+  }
+  (void)my_n;
+  flush_counts(a.ctr, 0, my_m);
+}
+
+// mark the next queues as visited (their distances were set by the claim)
+template <typename V>
+__global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, unsigned long long n1, V const* q2,
+                              unsigned long long n2, uint32_t* vis, uint32_t* fr)
+{
+  unsigned long long tot = n0 + n1 + n2;
+  for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < tot;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    V v = i < n0 ? q0[i] : (i < n0 + n1 ? q1[i - n0] : q2[i - n0 - n1]);
+    uint32_t bit = 1u << (uint32_t(v) & 31u);
+    atomicOr(vis + (v >> 5), bit);
+    if (fr) atomicOr(fr + (v >> 5), bit);
+  }
+}
+
+// bitmap -> class queues (bottom-up to top-down switch)
+template <typename V, typename E>
+__global__ __launch_bounds__(256) void k_bitmap_to_queues(bfs_args<V, E> a, uint32_t const* bm, int64_t nwords)
+{
+  unsigned long long my_m = 0;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += (int64_t)gridDim.x * blockDim.x) {
+    int64_t w     = base + threadIdx.x;
+    uint32_t word = w < nwords ? bm[w] : 0u;
+    // up to 32 rounds: every lane walks its word's set bits
+    for (int r = 0; r < 32; ++r) {
+      bool take = word != 0;
+      V v       = 0;
+      if (take) {
+        int bit = __ffs(word) - 1;
+        word &= word - 1;
+        v = (V)(w * 32 + bit);
+      }
+      if (!__any(take)) break;
+      push_next<V, E>(a, v, take, my_m);
+    }
+  }
+  flush_counts(a.ctr, 0, my_m);
+}
+
+// bottom-up step over all vertices (degree-binned schedule)
+template <typename V, typename E>
+__global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
+{
+  __shared__ int s_hit;
+  work_item const it = a.items[blockIdx.x];
+  unsigned long long my_n = 0, my_m = 0;
+  int tid = threadIdx.x;
+  V const nd = (V)(a.depth + 1);
+  if (it.width == 256) {
+    for (int64_t p = it.begin; p < it.end; ++p) {
+      V v = a.order ? a.order[p] : (V)p;
+      uint32_t bit = 1u << (uint32_t(v) & 31u);
+      if (a.vis[v >> 5] & bit) continue;  // uniform across the block
+      E beg = a.off[v], end = a.off[v + 1];
+      bool done = false;
+      for (E base = beg; base < end && !done; base += 256) {
+        if (tid == 0) s_hit = 0x7fffffff;
+        __syncthreads();
+        E e = base + tid;
+        if (e < end) {
+          V u = a.idx[e];
+          if ((a.fr[u >> 5] >> (uint32_t(u) & 31u)) & 1u) atomicMin(&s_hit, tid);
+        }
+        __syncthreads();
+        int h = s_hit;
+        if (h != 0x7fffffff) {
+          done = true;
+          if (tid == h) {
+            V u     = a.idx[e];
+            a.dist[v] = nd;
+            if (a.pred) a.pred[v] = u;
+            atomicOr(a.nxt + (v >> 5), bit);
+            atomicOr(a.vis + (v >> 5), bit);
+            my_n += 1;
+            my_m += (unsigned long long)(end - beg);
+          }
+        }
+        __syncthreads();
+      }
+    }
+  } else {
+    int const w      = it.width;
+    int const lane   = tid & (w - 1);
+    int const gbase  = (tid & 63) & ~(w - 1);  // first lane of my group within the wave
+    int const groups = 256 / w;
+    unsigned long long const gmask = (w == 64) ? ~0ull : ((1ull << w) - 1ull);
+    for (int64_t p0 = it.begin; p0 < it.end; p0 += groups) {
+      int64_t p  = p0 + tid / w;
+      bool valid = p < it.end;
+      V v        = valid ? (a.order ? a.order[p] : (V)p) : V(0);
+      uint32_t bit = 1u << (uint32_t(v) & 31u);
+      if (valid && (a.vis[v >> 5] & bit)) valid = false;  // same for the whole group
+      E beg = valid ? a.off[v] : E(0), end = valid ? a.off[v + 1] : E(0);
+      for (E base = beg; base < end; base += w) {
+        E e      = base + lane;
+        bool hit = false;
+        V u      = 0;
+        if (e < end) {
+          u   = a.idx[e];
+          hit = (a.fr[u >> 5] >> (uint32_t(u) & 31u)) & 1u;
+        }
+        unsigned long long m  = __ballot(hit);
+        unsigned long long gm = (m >> gbase) & gmask;
+        if (gm) {
+          int first = __ffsll((long long)gm) - 1;
+          if (lane == first) {
+            a.dist[v] = nd;
+            if (a.pred) a.pred[v] = u;
+            atomicOr(a.nxt + (v >> 5), bit);
+            atomicOr(a.vis + (v >> 5), bit);
+            my_n += 1;
+            my_m += (unsigned long long)(end - beg);
+          }
+          break;
+        }
+      }
+    }
+  }
+  flush_counts(a.ctr, my_n, my_m);
+}
+
+template <typename V>
+__global__ void k_bfs_init_sources(V* dist, V const* src, size_t ns, int64_t nv, int* bad)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < ns; i += (size_t)gridDim.x * blockDim.x) {
+    V s = src[i];
+    if (s < 0 || (int64_t)s >= nv) {
+      atomicAdd(bad, 1);
+      continue;
+    }
+    dist[s] = 0;
+  }
+}
+
+template <typename V>
+__global__ void k_finish_pred(V* pred, size_t n, V none)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if (pred[i] == none) pred[i] = (V)-1;
+}
+
+template <typename V>
+__global__ void k_sources_to_bitmap(V const* dist, int64_t nv, uint32_t* vis, uint32_t* fr)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x)
+    if (dist[v] == 0) {
+      atomicOr(vis + (v >> 5), 1u << (uint32_t(v) & 31u));
+      atomicOr(fr + (v >> 5), 1u << (uint32_t(v) & 31u));
+    }
+}
+
+template <typename V, typename E, typename W>
+void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size_t depth_limit, bool want_pred,
+              bool expensive, paths_result_t& res)
+{
+  hipStream_t s = h.stream;
+  int64_t nv    = g.num_vertices;
+  CGX_INPUT(sources->size > 0, "Invalid input argument: input should have at least one source");
+  CGX_INPUT(!dir_opt || g.symmetric,
+            "Invalid input argument: input graph should be symmetric for direction optimizing BFS.");
+  (void)expensive;
+  // sources: external -> internal, in place (c_api/bfs.cpp:96-114)
+  renumber_ext_to_int(h, g, sources->data, sources->size, true);
+  V const INF = std::numeric_limits<V>::max();
+  res.vertices  = number_map_copy(h, g);
+  res.distances = std::make_unique<device_array_t>((size_t)nv, dtype_of<V>(), s);
+  res.predecessors = std::make_unique<device_array_t>(want_pred ? (size_t)nv : 0, dtype_of<V>(), s);
+  V* dist = res.distances->buf.data<V>();
+  V* pred = want_pred ? res.predecessors->buf.data<V>() : nullptr;
+  h.last_bfs_levels    = 0;
+  h.last_bfs_bottom_up = 0;
+  if (nv == 0) return;
+  fill<V>(dist, nv, INF, s);
+  if (pred) fill<V>(pred, nv, INF, s);
+
+  adjacency_t& adj = ensure_adjacency(h, g, false);
+  if (dir_opt) ensure_schedule(h, g, adj);
+
+  int64_t nwords = (nv + 31) / 32;
+  dbuf<uint32_t> vis(nwords, s), fr(nwords, s), nxt(nwords, s);
+  HIP_CHECK(hipMemsetAsync(vis.data(), 0, nwords * 4, s));
+  HIP_CHECK(hipMemsetAsync(fr.data(), 0, nwords * 4, s));
+  HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));
+  dbuf<V> qa[3], qb[3];
+  for (int c = 0; c < 3; ++c) {
+    qa[c].resize(nv, s);
+    qb[c].resize(nv, s);
+  }
+  dbuf<bfs_ctr> ctr(1, s);
+  bfs_ctr* hctr = nullptr;
+  HIP_CHECK(hipHostMalloc((void**)&hctr, sizeof(bfs_ctr), hipHostMallocDefault));
+
+  bfs_args<V, E> a{};
+  a.off   = adj.offsets.data<E>();
+  a.idx   = adj.indices.data<V>();
+  a.dist  = dist;
+  a.pred  = pred;
+  a.vis   = vis.data();
+  a.fr    = fr.data();
+  a.nxt   = nxt.data();
+  a.ctr   = ctr.data();
+  a.nv    = nv;
+  a.order = (dir_opt && !adj.degree_sorted) ? adj.order.data<V>() : nullptr;
+  a.items = dir_opt ? adj.items.data<work_item>() : nullptr;
+
+  auto read_ctr = [&]() {
+    HIP_CHECK(hipMemcpyAsync(hctr, ctr.data(), sizeof(bfs_ctr), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  };
+  auto zero_ctr = [&]() { HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(bfs_ctr), s)); };
+
+  try {
+    // sources -> distance 0, visited, frontier bitmap; then bitmap -> queues
+    dbuf<int> bad(1, s);
+    fill<int>(bad.data(), 1, 0, s);
+    hipLaunchKernelGGL(k_bfs_init_sources<V>, dim3(grid_for(sources->size, kBlock, 1024)), dim3(kBlock), 0, s,
+                       dist, sources->as<V>(), sources->size, nv, bad.data());
+    hipLaunchKernelGGL(k_sources_to_bitmap<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, dist, nv,
+                       vis.data(), fr.data());
+    CGX_LAUNCH_CHECK();
+    CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: sources have invalid vertex IDs.");
+    zero_ctr();
+    for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
+    hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, a,
+                       fr.data(), nwords);
+    CGX_LAUNCH_CHECK();
+    read_ctr();
+    unsigned long long ncur[3] = {hctr->qlen[0], hctr->qlen[1], hctr->qlen[2]};
+    unsigned long long n_f = ncur[0] + ncur[1] + ncur[2];
+    unsigned long long m_f = hctr->next_m;
+    unsigned long long m_u = (unsigned long long)g.num_edges - m_f;
+    bool bottom_up  = false;
+    bool have_queue = true;  // frontier available as queues (qa); else as bitmap fr
+    bool have_bitmap = true; // frontier bitmap fr valid
+    V depth = 0;
+    V limit = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
+                                              (unsigned long long)std::numeric_limits<V>::max());
+    size_t levels = 0, bu_steps = 0;
+    while (n_f > 0 && depth < limit) {
+      if (dir_opt) {
+        if (!bottom_up && (double)m_f > (double)m_u / 14.0) bottom_up = true;
+        else if (bottom_up && (double)n_f < (double)nv / 24.0) bottom_up = false;
+      }
+      a.depth = depth;
+      zero_ctr();
+      if (bottom_up) {
+        if (!have_bitmap) {  // queues -> frontier bitmap
+          HIP_CHECK(hipMemsetAsync(fr.data(), 0, nwords * 4, s));
+          hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
+                             ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), fr.data());
+          CGX_LAUNCH_CHECK();
+          have_bitmap = true;
+        }
+        HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));
+        hipLaunchKernelGGL((k_bottomup<V, E>), dim3(adj.num_items), dim3(kBlock), 0, s, a);
+        CGX_LAUNCH_CHECK();
+        read_ctr();
+        std::swap(a.fr, a.nxt);
+        std::swap(fr, nxt);
+        have_queue = false;
+        n_f = hctr->next_n;
+        m_f = hctr->next_m;
+        ++bu_steps;
+      } else {
+        if (!have_queue) {  // frontier bitmap -> queues
+          for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
+          hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s,
+                             a, fr.data(), nwords);
+          CGX_LAUNCH_CHECK();
+          read_ctr();
+          for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
+          zero_ctr();
+          have_queue = true;
+        }
+        for (int c = 0; c < 3; ++c) {
+          a.qcur[c]  = qa[c].data();
+          a.ncur[c]  = ncur[c];
+          a.qnext[c] = qb[c].data();
+        }
+        long long nb_large = (long long)std::min<unsigned long long>(ncur[2], 1024);
+        long long nb_mid   = (long long)std::min<unsigned long long>((ncur[1] + 3) / 4, 4096);
+        long long nb_small = (long long)std::min<unsigned long long>((ncur[0] + 63) / 64, 8192);
+        a.blk_mid_start    = nb_large;
+        a.blk_small_start  = nb_large + nb_mid;
+        long long grid     = nb_large + nb_mid + nb_small;
+        if (grid > 0) {
+          hipLaunchKernelGGL((k_topdown<V, E>), dim3(grid), dim3(kBlock), 0, s, a);
+          CGX_LAUNCH_CHECK();
+        }
+        read_ctr();
+        for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
+        n_f = ncur[0] + ncur[1] + ncur[2];
+        m_f = hctr->next_m;
+        if (n_f) {
+          hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
+                             ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], vis.data(), nullptr);
+          CGX_LAUNCH_CHECK();
+        }
+        for (int c = 0; c < 3; ++c) std::swap(qa[c], qb[c]);
+        have_bitmap = false;
+      }
+      m_u = m_u > m_f ? m_u - m_f : 0;
+      ++depth;
+      ++levels;
+    }
+    h.last_bfs_levels    = levels;
+    h.last_bfs_bottom_up = bu_steps;
+  } catch (...) {
+    (void)hipHostFree(hctr);
+    throw;
+  }
+  HIP_CHECK(hipHostFree(hctr));
+  if (pred) {
+    hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF);
+    CGX_LAUNCH_CHECK();
+    unrenumber_int_to_ext(h, g, pred, (size_t)nv);
+  }
+}
+
+}  // namespace
+
+void run_bfs(handle_t& h, graph_t& g, array_view_t* sources, bool direction_optimizing, size_t depth_limit,
+             bool compute_predecessors, bool expensive, paths_result_t& res)
+{
+  dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
+    using T = decltype(t);
+    bfs_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(
+      h, g, sources, direction_optimizing, depth_limit, compute_predecessors, expensive, res);
+  });
+}
+
+}  // namespace cgx

@@ -9,15 +9,39 @@
 #include <cugraph_amd/ext.h>
 
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <vector>
 
 using namespace cgx;
 
 namespace {
 
+// Process-wide pool of handle streams.  A stream is never destroyed: memory
+// allocated on it with hipMallocAsync may be freed (stream-ordered) after the
+// handle that owned it is gone.
+std::mutex g_stream_mutex;
+std::vector<std::pair<int, hipStream_t>> g_free_streams;
+
+void release_stream(int device, hipStream_t s)
+{
+  std::lock_guard<std::mutex> lk(g_stream_mutex);
+  g_free_streams.emplace_back(device, s);
+}
+
 hipStream_t make_stream(int& device)
 {
   HIP_CHECK(hipGetDevice(&device));
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mutex);
+    for (size_t i = 0; i < g_free_streams.size(); ++i) {
+      if (g_free_streams[i].first == device) {
+        hipStream_t s = g_free_streams[i].second;
+        g_free_streams.erase(g_free_streams.begin() + i);
+        return s;
+      }
+    }
+  }
   // keep freed blocks cached in the device pool (stream-ordered allocator)
   hipMemPool_t pool;
   if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
@@ -66,7 +90,7 @@ extern "C" void cugraph_free_resource_handle(cugraph_resource_handle_t* handle)
   auto* h = H(handle);
   if (!h) return;
   (void)hipStreamSynchronize(h->stream);
-  (void)hipStreamDestroy(h->stream);
+  release_stream(h->device, h->stream);
   delete h;
 }
 

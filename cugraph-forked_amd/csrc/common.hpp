@@ -100,12 +100,12 @@ class buffer {
     }
   }
   void set_stream(hipStream_t s) { stream_ = s; }
-  // Frees are enqueued on the legacy null stream: it orders after every blocking
-  // stream (all handle streams are blocking), so a buffer may outlive the handle
-  // whose stream allocated it (graphs and results freed after their handle).
+  // Frees are stream-ordered on the allocating stream.  Handle streams come from a
+  // process-wide pool and are never destroyed (capi_core.cpp), so a buffer may
+  // outlive the handle that allocated it (graphs/results freed after their handle).
   void release()
   {
-    if (ptr_) { (void)hipFreeAsync(ptr_, nullptr); }
+    if (ptr_) { (void)hipFreeAsync(ptr_, stream_); }
     ptr_   = nullptr;
     bytes_ = 0;
   }

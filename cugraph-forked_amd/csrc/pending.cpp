@@ -2,14 +2,6 @@
 #include "capi.hpp"
 
 namespace cgx {
-void run_bfs(handle_t&, graph_t&, array_view_t*, bool, size_t, bool, bool, paths_result_t&)
-{
-  fail(CUGRAPH_NOT_IMPLEMENTED, "BFS: not built yet");
-}
-void run_sssp(handle_t&, graph_t&, size_t, double, bool, bool, paths_result_t&)
-{
-  fail(CUGRAPH_NOT_IMPLEMENTED, "SSSP: not built yet");
-}
 void run_louvain(handle_t&, graph_t&, size_t, double, bool, clustering_result_t&)
 {
   fail(CUGRAPH_NOT_IMPLEMENTED, "Louvain: not built yet");

@@ -65,10 +65,10 @@ class ResourceHandle:
     def last_louvain_levels(self):
         return _lib.lib.cugraph_amd_last_louvain_levels(self.c_resource_handle_ptr)
 
-    def __del__(self):
+    def __del__(self, _sd=_lib.SHUTDOWN, _free=_lib.lib.cugraph_free_resource_handle):
         p = getattr(self, "c_resource_handle_ptr", None)
-        if p:
-            _lib.lib.cugraph_free_resource_handle(p)
+        if p and not _sd[0]:
+            _free(p)
             self.c_resource_handle_ptr = None
 
 
@@ -135,9 +135,9 @@ class SGGraph(_GPUGraph):
         self.c_graph_ptr = g.value
         self._mg = False
 
-    def __del__(self):
-        if getattr(self, "c_graph_ptr", None):
-            _lib.lib.cugraph_sg_graph_free(self.c_graph_ptr)
+    def __del__(self, _sd=_lib.SHUTDOWN, _free=_lib.lib.cugraph_sg_graph_free):
+        if getattr(self, "c_graph_ptr", None) and not _sd[0]:
+            _free(self.c_graph_ptr)
             self.c_graph_ptr = None
 
 
@@ -161,9 +161,9 @@ class MGGraph(_GPUGraph):
         self.c_graph_ptr = g.value
         self._mg = True
 
-    def __del__(self):
-        if getattr(self, "c_graph_ptr", None):
-            _lib.lib.cugraph_mg_graph_free(self.c_graph_ptr)
+    def __del__(self, _sd=_lib.SHUTDOWN, _free=_lib.lib.cugraph_mg_graph_free):
+        if getattr(self, "c_graph_ptr", None) and not _sd[0]:
+            _free(self.c_graph_ptr)
             self.c_graph_ptr = None
 
 

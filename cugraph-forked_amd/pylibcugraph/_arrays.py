@@ -67,9 +67,9 @@ class DeviceView:
         self.ptr = _lib.lib.cugraph_type_erased_device_array_view_create(
             ctypes.c_void_p(self.tensor.data_ptr()), self.tensor.numel(), self.c_type)
 
-    def __del__(self):
-        if getattr(self, "ptr", None):
-            _lib.lib.cugraph_type_erased_device_array_view_free(self.ptr)
+    def __del__(self, _sd=_lib.SHUTDOWN, _free=_lib.lib.cugraph_type_erased_device_array_view_free):
+        if getattr(self, "ptr", None) and not _sd[0]:
+            _free(self.ptr)
             self.ptr = None
 
 
@@ -124,7 +124,7 @@ class DeviceArray:
         _lib.lib.cugraph_type_erased_device_array_view_free(v)
         return n
 
-    def __del__(self):
-        if getattr(self, "ptr", None):
-            _lib.lib.cugraph_type_erased_device_array_free(self.ptr)
+    def __del__(self, _sd=_lib.SHUTDOWN, _free=_lib.lib.cugraph_type_erased_device_array_free):
+        if getattr(self, "ptr", None) and not _sd[0]:
+            _free(self.ptr)
             self.ptr = None

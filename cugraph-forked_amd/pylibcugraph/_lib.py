@@ -8,6 +8,7 @@ import fails loudly.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 
@@ -20,7 +21,22 @@ if not os.path.exists(LIB_PATH):
         f"libcugraph_c.so not found at {LIB_PATH}: build it with "
         "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C cugraph-forked_amd`)")
 
+# torch bundles its own HIP runtime (torch/lib/libamdhip64.so, loaded by path).  Load
+# it FIRST so that libcugraph_c's DT_NEEDED libamdhip64.so.7 / libhsa-runtime64.so.1
+# resolve to the same, already-loaded objects: one HIP runtime per process.  (Loading
+# ours first makes torch load a second runtime: two HIP runtimes in one process
+# corrupt the heap at exit.)
+try:
+    import torch  # noqa: F401
+except ImportError:  # pure C-ABI use without torch: the system ROCm runtime is used
+    torch = None
+
 lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+
+# Objects still alive at interpreter exit are not freed (the process is going
+# away; calling into HIP during teardown is not safe).
+SHUTDOWN = [False]
+atexit.register(lambda: SHUTDOWN.__setitem__(0, True))
 
 # enums (include/cugraph_c/resource_handle.h, error.h)
 INT32, INT64, FLOAT32, FLOAT64 = 0, 1, 2, 3

@@ -1,0 +1,114 @@
+"""BFS parity: distances bit-exact vs the oracle; predecessors exact under the
+documented tie rule (smallest internal id), and valid per bfs_test.cpp:210-230."""
+import numpy as np
+import pytest
+
+from conftest import dataset_path
+from gpu_util import host, make_graph, plc
+from oracle import bfs as obfs
+from oracle import graph as og
+from oracle import rmat
+
+pytestmark = pytest.mark.gpu
+INT32_MAX = 2**31 - 1
+
+
+def run(h, G, sources, do, depth=0, pred=True, vdtype=np.int32):
+    d, p, v = plc().bfs(h, G, np.asarray(sources, vdtype), do, depth, pred, False)
+    return host(v), host(d), host(p)
+
+
+def check_vs_oracle(s, d, v, dist, pred, sources_ext, depth_limit=None, inf=INT32_MAX):
+    n_ext = int(max(np.max(s, initial=0), np.max(d, initial=0), np.max(sources_ext))) + 1
+    G = og.create_graph(s, d, None, renumber=False, vertices=np.arange(n_ext))
+    key = np.full(n_ext, np.iinfo(np.int64).max // 2, dtype=np.int64)
+    key[v] = np.arange(v.size)  # internal id = position in the result arrays
+    # make the key a permutation (ids absent from the GPU graph never win)
+    absent = np.setdiff1d(np.arange(n_ext), v)
+    key[absent] = v.size + np.arange(absent.size)
+    rd, rp = obfs.bfs(n_ext, G.offsets, G.indices, sources_ext, depth_limit, tie_key=key, invalid_distance=inf)
+    assert np.array_equal(dist, rd[v])
+    if pred is not None and pred.size:
+        assert np.array_equal(pred, rp[v])
+
+
+def test_c_golden(golden):
+    g = golden["bfs_c"]
+    for transposed in (False, True):
+        h, G = make_graph(g["src"], g["dst"], g["w"], transposed=transposed, renumber=False)
+        v, dist, pred = run(h, G, g["sources"], False, g["depth_limit"])
+        exp_d = np.asarray(g["expected_distances"])
+        exp_p = np.asarray(g["expected_predecessors"])
+        assert np.array_equal(dist, exp_d[v]) and np.array_equal(pred, exp_p[v])
+
+
+@pytest.mark.parametrize("name", ["karate.csv", "dolphins.csv", "netscience.csv"])
+@pytest.mark.parametrize("do", [False, True])
+def test_datasets(name, do):
+    s, d, _ = og.read_csv(dataset_path(name))
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    src = [int(s[0])]
+    v, dist, pred = run(h, G, src, do)
+    check_vs_oracle(s, d, v, dist, pred, src)
+
+
+def rmat_sym(scale, seed=42):
+    s, d = rmat.rmat(scale, 16 << scale, seed=seed)
+    s, d, _ = og.symmetrize_dedup(s, d)
+    return s, d
+
+
+@pytest.mark.parametrize("scale", [10, 14])
+@pytest.mark.parametrize("do", [False, True])
+def test_rmat(scale, do):
+    s, d = rmat_sym(scale)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    deg = np.bincount(s)
+    src = [int(np.argmax(deg))]
+    v, dist, pred = run(h, G, src, do)
+    check_vs_oracle(s, d, v, dist, pred, src)
+    if do and scale == 14:
+        assert h.last_bfs_bottom_up_steps() > 0  # the bottom-up path was exercised
+
+
+def test_rmat_multi_source_and_depth_limit():
+    s, d = rmat_sym(12)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    verts = np.unique(s)
+    srcs = [int(verts[3]), int(verts[100]), int(verts[100]), int(verts[-1])]
+    for do in (False, True):
+        v, dist, pred = run(h, G, srcs, do, depth=2)
+        check_vs_oracle(s, d, v, dist, pred, srcs, depth_limit=2)
+        assert dist[dist != INT32_MAX].max() <= 2
+
+
+def test_directed_top_down_and_do_requires_symmetric():
+    s, d = rmat.rmat(11, 16 << 11)
+    s, d, _ = og.symmetrize_dedup(s, d, symmetrize=False)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=False)
+    src = [int(s[0])]
+    v, dist, pred = run(h, G, src, False)
+    check_vs_oracle(s, d, v, dist, pred, src)
+    with pytest.raises(ValueError, match="symmetric"):
+        run(h, G, src, True)
+
+
+def test_int64_no_predecessors():
+    s, d = rmat_sym(11)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True, vdtype=np.int64)
+    v, dist, pred = run(h, G, [int(s[0])], True, pred=False, vdtype=np.int64)
+    assert pred.size == 0
+    check_vs_oracle(s, d, v, dist, None, [int(s[0])], inf=np.iinfo(np.int64).max)
+
+
+def test_invalid_source():
+    h, G = make_graph([0, 1], [1, 2], None, renumber=True)
+    with pytest.raises(ValueError):
+        run(h, G, [7], False)
+
+
+def test_isolated_source_and_unrenumbered_gaps():
+    # ids 0..9 with vertex 5 isolated (renumber=False keeps it)
+    h, G = make_graph([0, 1, 2, 6], [1, 2, 3, 7], None, renumber=False, symmetric=False)
+    v, dist, pred = run(h, G, [5], False)
+    assert dist[v == 5][0] == 0 and np.all(dist[v != 5] == INT32_MAX)

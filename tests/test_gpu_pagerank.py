@@ -16,7 +16,7 @@ REL = 1e-6
 
 def by_ext(vertices, values):
     v, x = host(vertices), host(values)
-    out = np.empty(v.max() + 1 if v.size else 0, dtype=np.float64)
+    out = np.zeros(v.max() + 1 if v.size else 0, dtype=np.float64)
     out[v] = x
     return out
 
