@@ -76,8 +76,17 @@ struct adjacency_t {
   std::vector<int64_t> bin_begin;       // positions (in processing order) where each bin starts
   buffer items;                         // work items for the SpMV-like kernels
   int64_t num_items = 0;
-  buffer items_bfs;                     // work items for the bottom-up BFS kernel
-  int64_t num_items_bfs = 0;
+  // edge-tiled PageRank schedule (pagerank.hip, identity order only)
+  bool pr_valid = false;
+  int64_t pr_nhub = 0, pr_nmid = 0, pr_ntiles = 0, pr_nzero_tiles = 0, pr_nzero_row = 0;
+  buffer pr_hub_off;    // int64[V+1]: hub CSR offsets (out-neighbours with id < nhub)
+  buffer pr_hub_idx;    // uint32 packed push entries (source offset << 13 | hub id)
+  buffer pr_push_units; // push work units
+  int64_t pr_npush_units = 0;
+  bool pr_push_ok = true;
+  buffer pr_hub_w;      // their weights (weighted graphs)
+  buffer pr_hub_acc;    // u64[nhub] fixed-point accumulators
+  buffer pr_tile_rows;  // tile descriptors of the low-degree rows
 };
 
 struct graph_t {

@@ -26,7 +26,9 @@
 #include "prims.hpp"
 #include "schedule.hpp"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace cgx {
 
@@ -241,6 +243,458 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
 }
 
+// ---------------------------------------------------------------- edge-tiled iteration
+// Identity processing order (renumbered: rows sorted by descending degree).
+//
+// Two kernels per iteration:
+//  * k_pr_push: the nhub highest-degree rows ("hubs", ids [0, nhub)) are not pulled:
+//    their in-neighbours are spread over the whole vertex range, so pulled gathers
+//    would be uniformly random (Infinity-Cache/HBM misses).  Instead every vertex u
+//    pushes x~[u] (x w) to its hub out-neighbours, read from a compact "hub CSR"
+//    (the id < nhub prefix of each sorted out-adjacency row, 16-bit ids) that is
+//    streamed once, into per-block LDS accumulators.  Accumulation is in 64-bit
+//    fixed point (scale 2^62; every hub sum is <= the total rank mass 1), so the
+//    result is exact integer arithmetic: order-independent and bitwise
+//    deterministic.  Blocks flush into a global fixed-point vector with integer
+//    atomics.
+//  * k_pr_stream (persistent): hub rows (fixed point -> fp64), rows of degree >=
+//    kTileHalf one block per row, edge tiles of whole low-degree rows (< kTile edges:
+//    coalesced non-temporal index loads + 8 independent gathers per thread; row data
+//    prefetched into LDS so a tile costs two dependent memory latencies), then the
+//    zero-degree rows; one ticket per block for the iteration state.
+constexpr int kTileHalf   = 1024;           // rows below this degree are tiled
+constexpr int kTile       = 2 * kTileHalf;  // max edges (and rows) per tile = 8 per thread
+constexpr int kZeroRows   = 2048;           // rows per zero-degree unit
+constexpr int kHubMax     = 8192;           // LDS accumulators per push block (64 KB)
+constexpr int kPushThreads = 512;
+constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
+constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
+
+struct tile_desc {
+  int64_t rb, re;  // rows [rb, re)
+  int64_t eb, ee;  // edges [eb, ee) = [off[rb], off[re])
+};
+
+struct push_unit {
+  int64_t k0, k1;  // entries
+  int64_t base;    // source id of (entry >> kHubBits) == 0
+};
+
+template <typename V, typename E, typename R>
+struct pr_stream_args {
+  pr_args<V, E, R> a;
+  tile_desc const* tiles;
+  // push side (hub rows)
+  uint32_t const* push_ent;      // (source offset << kHubBits) | hub id, grouped by source
+  struct push_unit const* push_units;
+  int64_t npush_units;
+  R const* hub_w;                // their weights (weighted graphs)
+  unsigned long long* hub_acc;   // [nhub] fixed-point sums (zeroed; reset by k_pr_stream)
+  int64_t nhub;
+  int64_t nmid;                  // rows [nhub, nmid): degree >= kTileHalf, one block each
+  int64_t ntiles, nzero_units, zero_row;
+  int ablate;  // measurement only (CGX_PR_ABLATE): 1 no gathers, 2 no row phase, 4 no push, 8 no tiles
+};
+
+template <typename T>
+__device__ __forceinline__ T nt_load(T const* p)
+{
+  return __builtin_nontemporal_load(p);
+}
+
+__device__ __forceinline__ unsigned long long to_fixed(double v)
+{
+  return (unsigned long long)__double2ull_rn(v * kFixScale);
+}
+
+// push entries: (source - unit base) << kHubBits | hub id, grouped by source; a unit
+// covers <= kPushUnit entries of sources within 2^(32-kHubBits) of its base
+constexpr int kHubBits  = 13;  // kHubMax = 2^13
+constexpr int kPushUnit = 8 * kPushThreads;
+
+template <typename V, typename E, typename R, bool WEIGHTED>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push(pr_stream_args<V, E, R> sa)
+{
+  __shared__ unsigned long long acc[kHubMax];
+  auto const& a = sa.a;
+  if (a.st->done || (sa.ablate & 4)) return;
+  int const tid  = threadIdx.x;
+  int const nhub = (int)sa.nhub;
+  for (int i = tid; i < nhub; i += kPushThreads) acc[i] = 0ull;
+  __syncthreads();
+  for (int64_t un = blockIdx.x; un < sa.npush_units; un += gridDim.x) {
+    push_unit const pu = sa.push_units[un];
+    uint32_t ent[8];
+    R w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int64_t k = pu.k0 + j * kPushThreads + tid;
+      ent[j]    = k < pu.k1 ? nt_load(sa.push_ent + k) : 0xffffffffu;
+      if constexpr (WEIGHTED) w[j] = k < pu.k1 ? nt_load(sa.hub_w + k) : R(0);
+    }
+    R x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      x[j] = ent[j] != 0xffffffffu ? a.x_in[pu.base + (int64_t)(ent[j] >> kHubBits)] : R(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (ent[j] != 0xffffffffu && x[j] != R(0)) {
+        double v = (double)x[j];
+        if constexpr (WEIGHTED) v *= (double)w[j];
+        atomicAdd(&acc[ent[j] & (kHubMax - 1)], to_fixed(v));
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < nhub; i += kPushThreads)
+    if (acc[i]) atomicAdd(sa.hub_acc + i, acc[i]);
+}
+
+// LDS image of one tile (rows <= kTile, edges < kTile).  Small (16-24 KB) so that 6-8
+// blocks fit a CU: the gathers are latency-bound and need the occupancy.
+template <typename R, bool WEIGHTED>
+struct tile_lds {
+  using val_t = std::conditional_t<WEIGHTED, double, R>;
+  val_t vals[kTile];   // gathered (weighted) values in edge order
+  int off[kTile + 1];  // row offsets relative to eb
+};
+
+template <typename V, typename E, typename R>
+__device__ __forceinline__ void vertex_update_lds(pr_args<V, E, R> const& a, V v, R old, R ow, double s, double base,
+                                                  double pf, double& my_diff, double& my_dang)
+{
+  double n = base + a.alpha * s;
+  if (a.pers) n += pf * (double)a.pers[v];
+  R nr    = (R)n;
+  a.pr[v] = nr;
+  my_diff += fabs((double)nr - (double)old);
+  if (ow == R(0)) {
+    my_dang += (double)nr;
+    a.x_out[v] = R(0);
+  } else {
+    a.x_out[v] = (R)((double)nr / (double)ow);
+  }
+}
+
+// One tile: every global load is issued up front (indices, weights, row offsets into
+// LDS, old pagerank and out-weights into registers), then the gathers, so a tile
+// costs two dependent memory latencies; per-row sums run out of LDS.
+template <typename V, typename E, typename R, bool WEIGHTED>
+__device__ void pr_tile(pr_stream_args<V, E, R> const& sa, tile_desc const& t, double base, double pf,
+                        double& my_diff, double& my_dang, tile_lds<R, WEIGHTED>& L)
+{
+  auto const& a   = sa.a;
+  int const tid   = threadIdx.x;
+  int const lane  = tid & 63, wid = tid >> 6;
+  int const nrows = (int)(t.re - t.rb);
+  E const eb = (E)t.eb, ee = (E)t.ee;
+  bool const wave_rows = (int64_t)(ee - eb) >= 32 * (int64_t)nrows;  // <= 64 rows: one wave per row
+  V u[8];
+  R w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    E e  = eb + j * 256 + tid;
+    u[j] = e < ee ? nt_load(a.idx + e) : V(0);
+    if constexpr (WEIGHTED) w[j] = e < ee ? nt_load(a.wgt + e) : R(0);
+  }
+  for (int i = tid; i <= nrows; i += 256) L.off[i] = (int)(a.off[t.rb + i] - eb);
+  R rpr[8], row_[8];
+  if (wave_rows) {  // lane l holds row wid + 4 l
+    int i = wid + 4 * lane;
+    rpr[0] = i < nrows ? a.pr[t.rb + i] : R(0);
+    row_[0] = i < nrows ? a.outw[t.rb + i] : R(0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int i   = tid + k * 256;
+      rpr[k]  = i < nrows ? a.pr[t.rb + i] : R(0);
+      row_[k] = i < nrows ? a.outw[t.rb + i] : R(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    E e = eb + j * 256 + tid;
+    if (e < ee) {
+      R x = (sa.ablate & 1) ? (R)u[j] : a.x_in[u[j]];
+      if constexpr (WEIGHTED) L.vals[j * 256 + tid] = (double)x * (double)w[j];
+      else L.vals[j * 256 + tid] = x;
+    }
+  }
+  __syncthreads();
+  if (!(sa.ablate & 2)) {
+    if (wave_rows) {
+      for (int i = wid, k = 0; i < nrows; i += 4, ++k) {
+        int lo = L.off[i], hi = L.off[i + 1];
+        double s = 0;
+        for (int q = lo + lane; q < hi; q += 64) s += (double)L.vals[q];
+        s        = wave_sum(s);
+        R old    = __shfl(rpr[0], k, 64);
+        R ow     = __shfl(row_[0], k, 64);
+        if (lane == 0) vertex_update_lds<V, E, R>(a, (V)(t.rb + i), old, ow, s, base, pf, my_diff, my_dang);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        int i = tid + k * 256;
+        if (i < nrows) {
+          int lo = L.off[i], hi = L.off[i + 1];
+          double s = 0;
+          for (int q = lo; q < hi; ++q) s += (double)L.vals[q];
+          vertex_update_lds<V, E, R>(a, (V)(t.rb + i), rpr[k], row_[k], s, base, pf, my_diff, my_dang);
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// one block per row of degree >= kTileHalf (rows [nhub, nmid)), 8 edges per thread per round
+template <typename V, typename E, typename R, bool WEIGHTED>
+__device__ void pr_block_row(pr_args<V, E, R> const& a, int64_t r, double base, double pf, double& my_diff,
+                             double& my_dang, double* sm)
+{
+  int const tid = threadIdx.x;
+  E const e0 = a.off[r], e1 = a.off[r + 1];
+  double s0 = 0, s1 = 0;
+  for (E b = e0; b < e1; b += 8 * 256) {
+    V u[8];
+    R w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      E e  = b + j * 256 + tid;
+      u[j] = e < e1 ? nt_load(a.idx + e) : V(0);
+      if constexpr (WEIGHTED) w[j] = e < e1 ? nt_load(a.wgt + e) : R(0);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      E e = b + j * 256 + tid;
+      if (e < e1) {
+        double t = (double)a.x_in[u[j]];
+        if constexpr (WEIGHTED) t *= (double)w[j];
+        if (j & 1) s1 += t;
+        else s0 += t;
+      }
+    }
+  }
+  double s = block_sum_256(s0 + s1, sm);
+  if (tid == 0) vertex_update<V, E, R>(a, (V)r, s, base, pf, my_diff, my_dang);
+}
+
+template <typename V, typename E, typename R, bool WEIGHTED>
+__global__ __launch_bounds__(256) void k_pr_stream(pr_stream_args<V, E, R> sa)
+{
+  __shared__ tile_lds<R, WEIGHTED> L;
+  __shared__ double sm[4];
+  auto const& a = sa.a;
+  if (a.st->done) return;
+  double const base = a.st->base;
+  double const pf   = a.st->pers_factor;
+  double my_diff = 0, my_dang = 0;
+  int64_t const nhubu = (sa.nhub + 255) / 256;
+  int64_t const nmid  = sa.nmid - sa.nhub;
+  int64_t const total = nhubu + nmid + sa.ntiles + sa.nzero_units;
+  for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {
+    if (u < nhubu) {  // hub rows: fixed-point push sums -> fp64
+      int64_t r = u * 256 + threadIdx.x;
+      if (r < sa.nhub) {
+        unsigned long long f = sa.hub_acc[r];
+        sa.hub_acc[r]        = 0ull;  // ready for the next iteration's push
+        vertex_update<V, E, R>(a, (V)r, (double)f * kFixScaleInv, base, pf, my_diff, my_dang);
+      }
+    } else if (u < nhubu + nmid) {
+      pr_block_row<V, E, R, WEIGHTED>(a, sa.nhub + (u - nhubu), base, pf, my_diff, my_dang, sm);
+    } else if (u < nhubu + nmid + sa.ntiles) {
+      if (sa.ablate & 8) continue;
+      tile_desc t = sa.tiles[u - nhubu - nmid];
+      pr_tile<V, E, R, WEIGHTED>(sa, t, base, pf, my_diff, my_dang, L);
+    } else {
+      int64_t r0 = sa.zero_row + (u - nhubu - nmid - sa.ntiles) * kZeroRows;
+      int64_t r1 = r0 + kZeroRows < a.nv ? r0 + kZeroRows : a.nv;
+      for (int64_t r = r0 + threadIdx.x; r < r1; r += 256)
+        vertex_update<V, E, R>(a, (V)r, 0.0, base, pf, my_diff, my_dang);
+    }
+  }
+  finish_iteration<V, E, R>(a, my_diff, my_dang, true);
+}
+
+// hub_cnt[u] = number of out-neighbours of u with id < nhub (prefix of the sorted row)
+template <typename V, typename E>
+__global__ void k_hub_count(E const* off, V const* idx, int64_t nv, int64_t nhub, int64_t* cnt)
+{
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < nv; u += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = (int64_t)off[u], hi = (int64_t)off[u + 1], b = lo;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)idx[mid] < nhub) lo = mid + 1;
+      else hi = mid;
+    }
+    cnt[u] = lo - b;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[nv] = 0;
+}
+
+// unit_base[i] = source row of entry i * kPushUnit (last row whose offset <= it)
+__global__ void k_push_unit_base(int64_t const* hoff, int64_t nv, int64_t nunits, int64_t* unit_base)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nunits; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k  = i * kPushUnit;
+    int64_t lo = 0, hi = nv;  // last u with hoff[u] <= k
+    while (lo < hi) {
+      int64_t mid = (lo + hi + 1) >> 1;
+      if (hoff[mid] <= k) lo = mid;
+      else hi = mid - 1;
+    }
+    unit_base[i] = lo;
+  }
+}
+
+template <typename V, typename E, typename R>
+__global__ void k_hub_fill(E const* off, V const* idx, R const* w, int64_t nv, int64_t const* hoff,
+                           int64_t const* unit_base, uint32_t* ent, R* hw, int* bad)
+{
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < nv; u += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k0 = hoff[u], k1 = hoff[u + 1];
+    E e = off[u];
+    for (int64_t k = k0; k < k1; ++k, ++e) {
+      int64_t rel = u - unit_base[k / kPushUnit];
+      if (rel >= (int64_t(1) << (32 - kHubBits))) atomicAdd(bad, 1);
+      ent[k] = ((uint32_t)rel << kHubBits) | (uint32_t)idx[e];
+      if (hw) hw[k] = w[e];
+    }
+  }
+}
+
+__global__ void k_push_units(int64_t const* unit_base, int64_t nunits, int64_t nent, push_unit* units)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nunits; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k0 = i * kPushUnit;
+    int64_t k1 = k0 + kPushUnit < nent ? k0 + kPushUnit : nent;
+    units[i]   = push_unit{k0, k1, unit_base[i]};
+  }
+}
+
+template <typename E>
+__global__ void k_tile_desc(E const* off, int64_t const* rows, int64_t ntiles, tile_desc* out)
+{
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ntiles; k += (int64_t)gridDim.x * blockDim.x)
+    out[k] = tile_desc{rows[k], rows[k + 1], (int64_t)off[rows[k]], (int64_t)off[rows[k + 1]]};
+}
+
+template <typename E>
+__global__ void k_tile_rows(E const* off, int64_t r0, int64_t r1, int64_t ntiles, int64_t* out)
+{
+  E base = off[r0];
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k <= ntiles; k += (int64_t)gridDim.x * blockDim.x) {
+    if (k == ntiles) {
+      out[k] = r1;
+      continue;
+    }
+    E t = base + (E)(k * kTileHalf);
+    int64_t lo = r0, hi = r1;  // first row in [r0, r1) with off[row] >= t
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (off[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    out[k] = lo;
+  }
+}
+
+template <typename E>
+__global__ void k_first_below(E const* off, int64_t nv, int64_t t0, int64_t t1, int64_t* out)
+{
+  // first row with degree < t (degrees non-increasing), for t0 and t1
+  if (threadIdx.x >= 2) return;
+  int64_t t  = threadIdx.x == 0 ? t0 : t1;
+  int64_t lo = 0, hi = nv;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)(off[mid + 1] - off[mid]) >= t) lo = mid + 1;
+    else hi = mid;
+  }
+  out[threadIdx.x] = lo;
+}
+
+// Schedule (cached on the pull adjacency): hub count, the hub CSR built from the
+// out-adjacency (same object for symmetric graphs), block rows, tiles.
+template <typename V, typename E, typename R>
+void build_pr_stream_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
+{
+  hipStream_t s  = h.stream;
+  int64_t nv     = g.num_vertices;
+  E const* off   = adj.offsets.data<E>();
+  dbuf<int64_t> fb(2, s);
+  hipLaunchKernelGGL(k_first_below<E>, dim3(1), dim3(64), 0, s, off, nv, (int64_t)kTileHalf, (int64_t)1, fb.data());
+  CGX_LAUNCH_CHECK();
+  auto hb = to_host(fb.data(), 2, s);
+  int64_t nmid = hb[0], nzero = hb[1];
+  int64_t nhub = std::min<int64_t>(nmid, kHubMax);
+  adj.pr_nhub = nhub;
+  adj.pr_nmid = nmid;
+  // hub CSR from the out-adjacency (rows sorted ascending: hubs are each row's prefix)
+  adjacency_t& out = ensure_adjacency(h, g, false);
+  E const* ooff    = out.offsets.data<E>();
+  V const* oidx    = out.indices.data<V>();
+  dbuf<int64_t> cnt(nv + 1, s);
+  hipLaunchKernelGGL((k_hub_count<V, E>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, ooff, oidx, nv, nhub,
+                     cnt.data());
+  CGX_LAUNCH_CHECK();
+  adj.pr_hub_off.set_stream(s);
+  adj.pr_hub_off.resize((nv + 1) * sizeof(int64_t));
+  exclusive_scan<int64_t, int64_t>(cnt.data(), adj.pr_hub_off.data<int64_t>(), nv + 1, s);
+  int64_t nent = to_host(adj.pr_hub_off.data<int64_t>() + nv, 1, s)[0];
+  int64_t nunits = (nent + kPushUnit - 1) / kPushUnit;
+  dbuf<int64_t> ubase(std::max<int64_t>(nunits, 1), s);
+  if (nunits)
+    hipLaunchKernelGGL(k_push_unit_base, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s,
+                       adj.pr_hub_off.data<int64_t>(), nv, nunits, ubase.data());
+  CGX_LAUNCH_CHECK();
+  adj.pr_hub_idx.set_stream(s);
+  adj.pr_hub_idx.resize(std::max<int64_t>(nent, 1) * sizeof(uint32_t));
+  adj.pr_hub_w.set_stream(s);
+  if (g.weighted) adj.pr_hub_w.resize(std::max<int64_t>(nent, 1) * sizeof(R));
+  else adj.pr_hub_w.release();
+  dbuf<int> bad(1, s);
+  fill<int>(bad.data(), 1, 0, s);
+  hipLaunchKernelGGL((k_hub_fill<V, E, R>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, ooff, oidx,
+                     g.weighted ? out.weights.data<R>() : nullptr, nv, adj.pr_hub_off.data<int64_t>(), ubase.data(),
+                     adj.pr_hub_idx.data<uint32_t>(), g.weighted ? adj.pr_hub_w.data<R>() : nullptr, bad.data());
+  CGX_LAUNCH_CHECK();
+  adj.pr_push_units.set_stream(s);
+  adj.pr_push_units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
+  if (nunits)
+    hipLaunchKernelGGL(k_push_units, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, ubase.data(), nunits,
+                       nent, adj.pr_push_units.data<push_unit>());
+  CGX_LAUNCH_CHECK();
+  adj.pr_npush_units = nunits;
+  adj.pr_push_ok     = to_host_scalar(bad.data(), s) == 0;
+  adj.pr_hub_off.release();  // only needed to build the entries
+  adj.pr_hub_acc.set_stream(s);
+  adj.pr_hub_acc.resize(std::max<int64_t>(nhub, 1) * sizeof(unsigned long long));
+  HIP_CHECK(hipMemsetAsync(adj.pr_hub_acc.data(), 0, std::max<int64_t>(nhub, 1) * sizeof(unsigned long long), s));
+  // edge tiles over the remaining non-empty rows [nmid, nzero)
+  E o_mid  = to_host(off + nmid, 1, s)[0];
+  E o_zero = to_host(off + nzero, 1, s)[0];
+  int64_t ntiles = ((int64_t)(o_zero - o_mid) + kTileHalf - 1) / kTileHalf;
+  adj.pr_ntiles      = ntiles;
+  adj.pr_nzero_row   = nzero;
+  adj.pr_nzero_tiles = (nv - nzero + kZeroRows - 1) / kZeroRows;
+  adj.pr_tile_rows.set_stream(s);
+  {
+    dbuf<int64_t> rows(ntiles + 1, s);
+    hipLaunchKernelGGL(k_tile_rows<E>, dim3(grid_for(ntiles + 1, kBlock, 4096)), dim3(kBlock), 0, s, off, nmid, nzero,
+                       ntiles, rows.data());
+    CGX_LAUNCH_CHECK();
+    adj.pr_tile_rows.resize(std::max<int64_t>(ntiles, 1) * sizeof(tile_desc));
+    if (ntiles)
+      hipLaunchKernelGGL(k_tile_desc<E>, dim3(grid_for(ntiles, kBlock, 4096)), dim3(kBlock), 0, s, off, rows.data(),
+                         ntiles, adj.pr_tile_rows.data<tile_desc>());
+    CGX_LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  adj.pr_valid = true;
+}
+
 template <typename V, typename R>
 __global__ void k_scatter_values(R* dst, V const* ids, R const* vals, size_t n, double scale)
 {
@@ -364,7 +818,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   // iteration state
   int const nblk_iter = (int)adj.num_items;
   int const nblk_init = (int)grid_for(nv, kBlock, 1024);
-  dbuf<double> partials(2 * std::max(nblk_iter, nblk_init), s);
+  dbuf<double> partials(2 * std::max({nblk_iter, nblk_init, 2048}), s);
   dbuf<pr_state> st(1, s);
   HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(pr_state), s));
   dbuf<R> xa(nv, s), xb(nv, s);
@@ -391,13 +845,44 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
 
   if (max_iter == 0) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
 
+  // identity order (degree-sorted majors) with our own out-weight sums: hub push + edge tiles
+  // (user-precomputed out-weights could break the fixed-point bound: generic kernel then)
+  bool stream = adj.degree_sorted && pow_v == nullptr;
+  pr_stream_args<V, E, R> sa{};
+  int nblk_stream = 0, nblk_push = 0;
+  auto pkernel = g.weighted ? k_pr_push<V, E, R, true> : k_pr_push<V, E, R, false>;
+  auto skernel = g.weighted ? k_pr_stream<V, E, R, true> : k_pr_stream<V, E, R, false>;
+  if (stream) {
+    if (!adj.pr_valid) build_pr_stream_schedule<V, E, R>(h, g, adj);
+  }
+  if (stream && !adj.pr_push_ok) stream = false;  // source span too wide for the packed entries
+  if (stream) {
+    sa.tiles       = adj.pr_tile_rows.data<tile_desc>();
+    sa.push_ent    = adj.pr_hub_idx.data<uint32_t>();
+    sa.push_units  = adj.pr_push_units.data<push_unit>();
+    sa.npush_units = adj.pr_npush_units;
+    sa.hub_w       = g.weighted ? adj.pr_hub_w.data<R>() : nullptr;
+    sa.hub_acc     = adj.pr_hub_acc.data<unsigned long long>();
+    sa.nhub        = adj.pr_nhub;
+    sa.nmid        = adj.pr_nmid;
+    sa.ntiles      = adj.pr_ntiles;
+    sa.nzero_units = adj.pr_nzero_tiles;
+    sa.zero_row    = adj.pr_nzero_row;
+    if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
+    int64_t units = (sa.nhub + 255) / 256 + (sa.nmid - sa.nhub) + sa.ntiles + sa.nzero_units;
+    // persistent grids: as many blocks as the LDS footprint lets every CU hold
+    size_t lds  = g.weighted ? sizeof(tile_lds<R, true>) : sizeof(tile_lds<R, false>);
+    int per_cu  = (int)std::clamp<size_t>((160 * 1024) / (lds + 512), 1, 8);
+    nblk_stream = (int)std::max<int64_t>(1, std::min<int64_t>(units, 256 * per_cu));
+    nblk_push   = sa.nhub > 0 ? 512 : 0;
+  }
   // chunked enqueue; profiling records HIP events around every iteration launch
   int const chunk = 8;
   std::vector<hipEvent_t> ev;
   pr_state hst{};
   R* bufs[2]    = {xa.data(), xb.data()};
   size_t launched = 0;
-  auto kernel = g.weighted ? k_pr_iter<V, E, R, true> : k_pr_iter<V, E, R, false>;
+  auto kernel  = g.weighted ? k_pr_iter<V, E, R, true> : k_pr_iter<V, E, R, false>;
   pr_state* hpin = nullptr;
   HIP_CHECK(hipHostMalloc((void**)&hpin, sizeof(pr_state), hipHostMallocDefault));
   try {
@@ -413,7 +898,13 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
           ev.push_back(e1);
           HIP_CHECK(hipEventRecord(e0, s));
         }
-        hipLaunchKernelGGL(kernel, dim3(nblk_iter), dim3(kBlock), 0, s, a);
+        if (stream) {
+          sa.a = a;
+          if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
+          hipLaunchKernelGGL(skernel, dim3(nblk_stream), dim3(kBlock), 0, s, sa);
+        } else {
+          hipLaunchKernelGGL(kernel, dim3(nblk_iter), dim3(kBlock), 0, s, a);
+        }
         CGX_LAUNCH_CHECK();
         if (h.profiling) HIP_CHECK(hipEventRecord(ev.back(), s));
         ++launched;
