@@ -77,16 +77,13 @@ struct adjacency_t {
   buffer items;                         // work items for the SpMV-like kernels
   int64_t num_items = 0;
   // edge-tiled PageRank schedule (pagerank.hip, identity order only)
-  bool pr_valid = false;
-  int64_t pr_nhub = 0, pr_nmid = 0, pr_ntiles = 0, pr_nzero_tiles = 0, pr_nzero_row = 0;
-  buffer pr_hub_off;    // int64[V+1]: hub CSR offsets (out-neighbours with id < nhub)
-  buffer pr_hub_idx;    // uint32 packed push entries (source offset << 13 | hub id)
-  buffer pr_push_units; // push work units
-  int64_t pr_npush_units = 0;
-  bool pr_push_ok = true;
-  buffer pr_hub_w;      // their weights (weighted graphs)
-  buffer pr_hub_acc;    // u64[nhub] fixed-point accumulators
-  buffer pr_tile_rows;  // tile descriptors of the low-degree rows
+  bool pr_valid = false;    // PageRank push schedule built (pagerank.hip)
+  bool pr_push_ok = false;  // ids and edge positions fit the 32-bit packing
+  buffer pr_ent;            // uint32[E] push entries (source offset << 13 | window offset)
+  buffer pr_ew;             // their weights (weighted graphs)
+  buffer pr_units;          // push work units
+  int64_t pr_nunits = 0;
+  buffer pr_acc;            // u64[windows * 8192] fixed-point accumulators
 };
 
 struct graph_t {

@@ -8,7 +8,7 @@ OUT="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="${@:---no-bfs --no-cpu-baseline --steps 3 --warmup 1}"
+ARGS="${@:---no-bfs --no-cpu-baseline --no-traffic --steps 3 --warmup 1}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- python3 "$ROOT/bench.py" $ARGS > "$OUT/kt.log" 2>&1 || { echo "kt failed"; tail -20 "$OUT/kt.log"; exit 1; }
 echo "kernel trace done"
 if [ -n "${PMC_SETS:-}" ]; then

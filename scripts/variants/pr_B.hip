@@ -1,31 +1,27 @@
-// PageRank power iteration -- the hot path.
+// PageRank power iteration on the pull (CSC) adjacency -- the hot path.
 //
 // Algorithm: cpp/src/link_analysis/pagerank_impl.cuh:48-293 (init :168-183, loop
 // :209-292, stop rule :287-290).  The reference runs, per iteration, a copy, a
 // dangling transform_reduce (host sync), a divide pass, the 4 segment SpMV
 // kernels of prims/per_v_transform_reduce_incoming_outgoing_e.cuh and an L1
-// transform_reduce (host sync).  Per iteration here:
+// transform_reduce (host sync).  Here ONE kernel per iteration does all of it:
 //
-//   s[v]   = sum_{u in in(v)} x~[u] * w(u,v)
-//   pr'[v] = base + alpha*s (+ pers[v]*(alpha*dangling + 1 - alpha))
-//   x~'[v] = pr'[v] / outw[v]   (0 for dangling)     -> the next iteration's source
-//   diff  += |pr'[v] - pr[v]|,  dangling' += pr'[v] if outw[v] == 0
-//
-// Main path (windowed push, below): k_pr_push computes s in 64-bit fixed point from
-// a source-ordered copy of the edges, k_pr_apply does the per-vertex update.  The
-// generic path (k_pr_iter: user-supplied out-weight sums, or ids beyond 32 bits)
-// pulls over the degree-binned CSC schedule in one kernel with fp64 sums.
-// Both end an iteration with per-block (diff, dangling) partials that the last
-// block to arrive (ticket) reduces in block order -- deterministic -- writing the
-// next iteration's base, the convergence flag and the iteration count.
+//   for every vertex v (degree-binned lane groups, schedule.hpp):
+//     s      = sum_{u in in(v)} x~[u] * w(u,v)        fp64 accumulation of fp32 gathers
+//     pr'[v] = base + alpha*s (+ pers[v]*(alpha*dangling + 1 - alpha))
+//     x~'[v] = pr'[v] / outw[v]   (0 for dangling)     -> the next iteration's gather source
+//     diff  += |pr'[v] - pr[v]|,  dangling' += pr'[v] if outw[v] == 0
+//   per-block (diff, dangling) partials; the last block to arrive (agent-scope
+//   release/acquire ticket) reduces them in block order -- deterministic -- and
+//   writes the next iteration's base, the convergence flag and the iteration count.
 //
 // The host enqueues iterations in chunks and reads the flag once per chunk; a
 // kernel launched after convergence returns immediately, so no per-iteration
 // host round trip remains (the reference has two).
 //
-// Roofline: HBM.  Algorithmic bytes per iteration (the reference's pull
-// formulation) = 4E (indices) + 4V (offsets, int32) + 4V (x~ read)
-// + 4V (pr' write) + 4V (outw) [+4E weights] = 4E + 16V.
+// Roofline: HBM.  Algorithmic bytes per iteration = 4E (indices) + 4V (offsets,
+// int32) + 4V (x~ read, compulsory) + 4V (pr' write) + 4V (outw) [+4E weights]
+// = 4E + 16V.
 #include "capi.hpp"
 #include "prims.hpp"
 #include "schedule.hpp"
@@ -79,19 +75,23 @@ __device__ void finish_iteration(pr_args<V, E, R> const& a, double my_diff, doub
   double bd = block_sum_256(my_diff, sm);
   double bg = block_sum_256(my_dang, sm);
   if (threadIdx.x == 0) {
-    // write-through (sc1) partials: no agent release (an L2 write-back per block) needed
-    __hip_atomic_store(&a.partials[2 * blockIdx.x], bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.partials[2 * blockIdx.x + 1], bg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.partials[2 * blockIdx.x]     = bd;
+    a.partials[2 * blockIdx.x + 1] = bg;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned t = __hip_atomic_fetch_add(&a.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last     = (t == gridDim.x - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   if (!s_last) return;
   double d = 0, g = 0;
-  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {  // sc1 loads: L1 bypassed
-    d += __hip_atomic_load(&a.partials[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g += __hip_atomic_load(&a.partials[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+    d += a.partials[2 * b];
+    g += a.partials[2 * b + 1];
   }
   d = block_sum_256(d, sm);
   g = block_sum_256(g, sm);
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 constexpr int kWinBits     = 13;
 constexpr int kWin         = 1 << kWinBits;
 constexpr int kSrcBits     = 32 - kWinBits;  // 19
-constexpr int kPushThreads = 1024;
+constexpr int kPushThreads = 512;
 constexpr int kPushUnit    = 8 * kPushThreads;
 constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
 constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
@@ -316,6 +316,68 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
   __syncthreads();
 }
 
+// 16-byte vectors for the streamed arrays (4 B-per-lane loads cap near 3.8 TB/s)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <typename R>
+__device__ __forceinline__ void load4(R const* p, R* out, bool nt)
+{
+  if constexpr (sizeof(R) == 4) {
+    f32x4 v = nt ? __builtin_nontemporal_load(reinterpret_cast<f32x4 const*>(p)) : *reinterpret_cast<f32x4 const*>(p);
+    out[0] = v.x, out[1] = v.y, out[2] = v.z, out[3] = v.w;
+  } else {
+    f64x2 a = nt ? __builtin_nontemporal_load(reinterpret_cast<f64x2 const*>(p)) : *reinterpret_cast<f64x2 const*>(p);
+    f64x2 b = nt ? __builtin_nontemporal_load(reinterpret_cast<f64x2 const*>(p) + 1)
+                 : *(reinterpret_cast<f64x2 const*>(p) + 1);
+    out[0] = a.x, out[1] = a.y, out[2] = b.x, out[3] = b.y;
+  }
+}
+
+template <typename R>
+__device__ __forceinline__ void store4(R* p, R const* v)
+{
+  if constexpr (sizeof(R) == 4) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  } else {
+    reinterpret_cast<f64x2*>(p)[0] = f64x2{v[0], v[1]};
+    reinterpret_cast<f64x2*>(p)[1] = f64x2{v[2], v[3]};
+  }
+}
+
+// A unit lies inside one kPushUnit-aligned block of entries.  Inside a block the
+// entries are stored permuted (k_push_pack: phys = (j / 4) * kPushUnit/2 + 4t + j % 4
+// for logical entry j * kPushThreads + t) so that thread t loads its 8 entries as two
+// 16-byte quads while every gather instruction still covers kPushThreads consecutive
+// logical entries (same-source entries coalesce into few cache lines).
+template <typename R, bool WEIGHTED>
+struct unit_regs {
+  push_unit pu;
+  u32x4 e[2];
+  R w[8];
+};
+
+template <typename V, typename E, typename R, bool WEIGHTED>
+__device__ __forceinline__ void load_unit(push_args<V, E, R> const& sa, int64_t un, unit_regs<R, WEIGHTED>& r)
+{
+  r.pu = sa.units[un];
+  int64_t const blk = r.pu.k0 & ~(int64_t)(kPushUnit - 1);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // quad h of thread t holds logical entries blk + (4h + i) * kPushThreads + t, i < 4
+    int64_t kq = blk + h * (kPushUnit / 2) + 4 * threadIdx.x;
+    int64_t l0 = blk + 4 * h * kPushThreads + threadIdx.x;
+    bool live  = l0 + 3 * kPushThreads >= r.pu.k0 && l0 < r.pu.k1;
+    r.e[h]     = live ? __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(sa.ent + kq)) : u32x4{0, 0, 0, 0};
+    if constexpr (WEIGHTED) {
+      if (live) load4<R>(sa.ew + kq, r.w + 4 * h, true);
+      else r.w[4 * h] = r.w[4 * h + 1] = r.w[4 * h + 2] = r.w[4 * h + 3] = R(0);
+    }
+  }
+}
+
 template <typename V, typename E, typename R, bool WEIGHTED>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
 {
@@ -328,49 +390,38 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
   int64_t const u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
   int64_t cur      = u0 < u1 ? sa.units[u0].win : -1;
   __syncthreads();
-  uint32_t ent[8];
-  R w[8];
-  push_unit pu{};
-  auto load_unit = [&](int64_t un, push_unit& p, uint32_t* e, R* ww) {
-    p = sa.units[un];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int64_t k = p.k0 + j * kPushThreads + tid;
-      e[j]      = k < p.k1 ? nt_load(sa.ent + k) : 0u;
-      if constexpr (WEIGHTED) ww[j] = k < p.k1 ? nt_load(sa.ew + k) : R(0);
-    }
-  };
-  if (u0 < u1) load_unit(u0, pu, ent, w);
+  // software pipeline: the next unit's entries are in flight while this unit's
+  // gathers and LDS atomics run
+  unit_regs<R, WEIGHTED> r;
+  if (u0 < u1) load_unit<V, E, R, WEIGHTED>(sa, u0, r);
   for (int64_t un = u0; un < u1; ++un) {
-    uint32_t ent_n[8];
-    R w_n[8];
-    push_unit pu_n{};
-    if (un + 1 < u1) load_unit(un + 1, pu_n, ent_n, w_n);
-    if (pu.win != cur) {
+    unit_regs<R, WEIGHTED> n;
+    if (un + 1 < u1) load_unit<V, E, R, WEIGHTED>(sa, un + 1, n);
+    if (r.pu.win != cur) {
       flush_window<V, E, R>(sa, acc, cur);
-      cur = pu.win;
+      cur = r.pu.win;
     }
+    int64_t const blk = r.pu.k0 & ~(int64_t)(kPushUnit - 1);
+    uint32_t ent[8];
     R x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bool const ok = pu.k0 + j * kPushThreads + tid < pu.k1;
+      int h     = j >> 2;
+      ent[j]    = r.e[h][j & 3];
+      int64_t k = blk + j * kPushThreads + tid;  // logical entry
+      bool ok   = k >= r.pu.k0 && k < r.pu.k1;
       if (sa.ablate & 1) x[j] = ok ? R(1e-9) : R(0);
-      else x[j] = ok ? a.x_in[pu.base + (int64_t)(ent[j] >> kWinBits)] : R(0);
+      else x[j] = ok ? a.x_in[r.pu.base + (int64_t)(ent[j] >> kWinBits)] : R(0);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (x[j] != R(0) && !(sa.ablate & 2)) {
         double v = (double)x[j];
-        if constexpr (WEIGHTED) v *= (double)w[j];
+        if constexpr (WEIGHTED) v *= (double)r.w[j];
         atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
       }
     }
-    pu = pu_n;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ent[j] = ent_n[j];
-      if constexpr (WEIGHTED) w[j] = w_n[j];
-    }
+    r = n;
   }
   if (cur >= 0) flush_window<V, E, R>(sa, acc, cur);
 }
@@ -433,8 +484,11 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
     uint64_t key = keys[k];
     uint32_t e   = vals[k];
     uint32_t src = (uint32_t)key;
-    ent[k]       = ((src & ((1u << kSrcBits) - 1)) << kWinBits) | (rows[e] & (kWin - 1));
-    if (w) ew[k] = w[e];
+    int64_t l    = k & (kPushUnit - 1);
+    int64_t j    = l / kPushThreads, t = l % kPushThreads;
+    int64_t ph   = (k - l) + (j >> 2) * (kPushUnit / 2) + 4 * t + (j & 3);
+    ent[ph]      = ((src & ((1u << kSrcBits) - 1)) << kWinBits) | (rows[e] & (kWin - 1));
+    if (w) ew[ph] = w[e];
     if (flag[k]) units[uid[k]] = push_unit{k, 0, (int64_t)(src >> kSrcBits) << kSrcBits, (int64_t)(key >> 32)};
   }
 }
@@ -484,9 +538,10 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
   int64_t nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
   adj.pr_ent.set_stream(s);
-  adj.pr_ent.resize(ne * sizeof(uint32_t));
+  int64_t const ne_pad = (ne + kPushUnit - 1) / kPushUnit * kPushUnit;  // whole aligned quads
+  adj.pr_ent.resize(ne_pad * sizeof(uint32_t));
   adj.pr_ew.set_stream(s);
-  if (g.weighted) adj.pr_ew.resize(ne * sizeof(R));
+  if (g.weighted) adj.pr_ew.resize(ne_pad * sizeof(R));
   else adj.pr_ew.release();
   adj.pr_units.set_stream(s);
   adj.pr_units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));

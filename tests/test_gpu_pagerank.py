@@ -144,3 +144,31 @@ def test_empty_and_edgeless_graph():
     got = by_ext(v, pr)
     ref = opr.pagerank(4, [0, 3], [0, 3], None, 0.85, 1e-6, 100)
     assert np.allclose(got, ref, rtol=1e-6)
+
+
+@pytest.mark.parametrize("weighted,symmetric,renumber", [(False, True, True), (True, False, False)])
+def test_rmat_multi_window_push(weighted, symmetric, renumber):
+    """Scale 20: > 2^19 sources (several source segments per window) and ~128
+    destination windows of the push path (pagerank.hip), against the oracle and
+    against the generic pull kernel (precomputed out-weights take that path)."""
+    s, d, w = rmat_graph(20, weighted, symmetric)
+    w32 = None if w is None else w.astype(np.float32)
+    h, G = make_graph(s, d, w32, transposed=True, renumber=renumber, symmetric=symmetric)
+    v, pr = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+    og_g = og.create_graph(s, d, w32, store_transposed=True, renumber=renumber)
+    assert og_g.num_vertices > (1 << 19)
+    ref = opr.pagerank_from_graph(og_g, alpha=0.85, epsilon=1e-6, max_iterations=500)
+    ref_ext = np.zeros(int(og_g.number_map.max()) + 1)
+    ref_ext[og_g.number_map] = ref
+    got = by_ext(v, pr)
+    vv = host(v)
+    rel = np.abs(got[vv] - ref_ext[vv]) / ref_ext[vv]
+    assert rel.max() < REL, rel.max()
+    # generic pull path on the same graph
+    n = int(ref_ext.size)
+    wsum = np.zeros(n)
+    np.add.at(wsum, s, 1.0 if w32 is None else w32.astype(np.float64))
+    verts = vv.astype(np.int32)
+    v2, pr2 = plc().pagerank(h, G, verts, wsum[verts].astype(np.float32), None, None, 0.85, 1e-6, 500, False)
+    got2 = by_ext(v2, pr2)
+    assert np.max(np.abs(got2[vv] - got[vv]) / got[vv]) < REL
