@@ -671,7 +671,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.acc    = adj.pr_acc.data<unsigned long long>();
     if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
     nblk_push  = (int)std::min<int64_t>(sa.nunits, 256 * 2);  // 64 KB LDS: two blocks per CU
-    nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
+    nblk_apply = (int)grid_for(nv, kBlock, 256);
   }
   // chunked enqueue; profiling records HIP events around every iteration launch
   int const chunk = 8;

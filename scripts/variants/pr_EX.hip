@@ -1,31 +1,27 @@
-// PageRank power iteration -- the hot path.
+// PageRank power iteration on the pull (CSC) adjacency -- the hot path.
 //
 // Algorithm: cpp/src/link_analysis/pagerank_impl.cuh:48-293 (init :168-183, loop
 // :209-292, stop rule :287-290).  The reference runs, per iteration, a copy, a
 // dangling transform_reduce (host sync), a divide pass, the 4 segment SpMV
 // kernels of prims/per_v_transform_reduce_incoming_outgoing_e.cuh and an L1
-// transform_reduce (host sync).  Per iteration here:
+// transform_reduce (host sync).  Here ONE kernel per iteration does all of it:
 //
-//   s[v]   = sum_{u in in(v)} x~[u] * w(u,v)
-//   pr'[v] = base + alpha*s (+ pers[v]*(alpha*dangling + 1 - alpha))
-//   x~'[v] = pr'[v] / outw[v]   (0 for dangling)     -> the next iteration's source
-//   diff  += |pr'[v] - pr[v]|,  dangling' += pr'[v] if outw[v] == 0
-//
-// Main path (windowed push, below): k_pr_push computes s in 64-bit fixed point from
-// a source-ordered copy of the edges, k_pr_apply does the per-vertex update.  The
-// generic path (k_pr_iter: user-supplied out-weight sums, or ids beyond 32 bits)
-// pulls over the degree-binned CSC schedule in one kernel with fp64 sums.
-// Both end an iteration with per-block (diff, dangling) partials that the last
-// block to arrive (ticket) reduces in block order -- deterministic -- writing the
-// next iteration's base, the convergence flag and the iteration count.
+//   for every vertex v (degree-binned lane groups, schedule.hpp):
+//     s      = sum_{u in in(v)} x~[u] * w(u,v)        fp64 accumulation of fp32 gathers
+//     pr'[v] = base + alpha*s (+ pers[v]*(alpha*dangling + 1 - alpha))
+//     x~'[v] = pr'[v] / outw[v]   (0 for dangling)     -> the next iteration's gather source
+//     diff  += |pr'[v] - pr[v]|,  dangling' += pr'[v] if outw[v] == 0
+//   per-block (diff, dangling) partials; the last block to arrive (agent-scope
+//   release/acquire ticket) reduces them in block order -- deterministic -- and
+//   writes the next iteration's base, the convergence flag and the iteration count.
 //
 // The host enqueues iterations in chunks and reads the flag once per chunk; a
 // kernel launched after convergence returns immediately, so no per-iteration
 // host round trip remains (the reference has two).
 //
-// Roofline: HBM.  Algorithmic bytes per iteration (the reference's pull
-// formulation) = 4E (indices) + 4V (offsets, int32) + 4V (x~ read)
-// + 4V (pr' write) + 4V (outw) [+4E weights] = 4E + 16V.
+// Roofline: HBM.  Algorithmic bytes per iteration = 4E (indices) + 4V (offsets,
+// int32) + 4V (x~ read, compulsory) + 4V (pr' write) + 4V (outw) [+4E weights]
+// = 4E + 16V.
 #include "capi.hpp"
 #include "prims.hpp"
 #include "schedule.hpp"
@@ -316,6 +312,42 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
   __syncthreads();
 }
 
+// 16-byte vectors for the streamed arrays (4 B-per-lane loads cap near 3.8 TB/s)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <typename R>
+__device__ __forceinline__ void load4(R const* p, R* out, bool nt)
+{
+  if constexpr (sizeof(R) == 4) {
+    f32x4 v = nt ? __builtin_nontemporal_load(reinterpret_cast<f32x4 const*>(p)) : *reinterpret_cast<f32x4 const*>(p);
+    out[0] = v.x, out[1] = v.y, out[2] = v.z, out[3] = v.w;
+  } else {
+    f64x2 a = nt ? __builtin_nontemporal_load(reinterpret_cast<f64x2 const*>(p)) : *reinterpret_cast<f64x2 const*>(p);
+    f64x2 b = nt ? __builtin_nontemporal_load(reinterpret_cast<f64x2 const*>(p) + 1)
+                 : *(reinterpret_cast<f64x2 const*>(p) + 1);
+    out[0] = a.x, out[1] = a.y, out[2] = b.x, out[3] = b.y;
+  }
+}
+
+template <typename R>
+__device__ __forceinline__ void store4(R* p, R const* v)
+{
+  if constexpr (sizeof(R) == 4) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  } else {
+    reinterpret_cast<f64x2*>(p)[0] = f64x2{v[0], v[1]};
+    reinterpret_cast<f64x2*>(p)[1] = f64x2{v[2], v[3]};
+  }
+}
+
+// A unit lies inside one kPushUnit-aligned block of entries.  Inside a block the
+// entries are stored permuted (k_push_pack: phys = (j / 4) * kPushUnit/2 + 4t + j % 4
+// for logical entry j * kPushThreads + t) so that thread t loads its 8 entries as two
+// 16-byte quads while every gather instruction still covers kPushThreads consecutive
+// logical entries (same-source entries coalesce into few cache lines).
 template <typename V, typename E, typename R, bool WEIGHTED>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
 {
@@ -324,10 +356,10 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
   if (a.st->done || (sa.ablate & 4)) return;
   int const tid = threadIdx.x;
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
-  // contiguous runs of units (window-major order; measured faster than an
-  // XCD-blocked or segment-major schedule, which multiply the window flushes)
-  int64_t const u0 = blockIdx.x * sa.nunits / gridDim.x;
-  int64_t const u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
+  int64_t const nb = gridDim.x;
+  int64_t const lb = nb % 8 == 0 ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+  int64_t const u0 = lb * sa.nunits / nb;
+  int64_t const u1 = (lb + 1) * sa.nunits / nb;
   int64_t cur      = u0 < u1 ? sa.units[u0].win : -1;
   __syncthreads();
   uint32_t ent[8];
@@ -417,8 +449,7 @@ __global__ void k_push_keys(V const* idx, uint32_t const* rows, int64_t ne, uint
   }
 }
 
-// key = (window, source); unit starts: a new segment (window, 2^kSrcBits source
-// block) or every kPushUnit-th entry
+// unit starts: a new segment (window, source block) or every kPushUnit-th entry
 __global__ void k_unit_flags(uint64_t const* keys, int64_t ne, uint32_t* flag)
 {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
@@ -436,8 +467,9 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
     uint64_t key = keys[k];
     uint32_t e   = vals[k];
     uint32_t src = (uint32_t)key;
-    ent[k]       = ((src & ((1u << kSrcBits) - 1)) << kWinBits) | (rows[e] & (kWin - 1));
-    if (w) ew[k] = w[e];
+    int64_t ph   = k;
+    ent[ph]      = ((src & ((1u << kSrcBits) - 1)) << kWinBits) | (rows[e] & (kWin - 1));
+    if (w) ew[ph] = w[e];
     if (flag[k]) units[uid[k]] = push_unit{k, 0, (int64_t)(src >> kSrcBits) << kSrcBits, (int64_t)(key >> 32)};
   }
 }
@@ -487,9 +519,10 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
   int64_t nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
   adj.pr_ent.set_stream(s);
-  adj.pr_ent.resize(ne * sizeof(uint32_t));
+  int64_t const ne_pad = (ne + kPushUnit - 1) / kPushUnit * kPushUnit;  // whole aligned quads
+  adj.pr_ent.resize(ne_pad * sizeof(uint32_t));
   adj.pr_ew.set_stream(s);
-  if (g.weighted) adj.pr_ew.resize(ne * sizeof(R));
+  if (g.weighted) adj.pr_ew.resize(ne_pad * sizeof(R));
   else adj.pr_ew.release();
   adj.pr_units.set_stream(s);
   adj.pr_units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
@@ -671,7 +704,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.acc    = adj.pr_acc.data<unsigned long long>();
     if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
     nblk_push  = (int)std::min<int64_t>(sa.nunits, 256 * 2);  // 64 KB LDS: two blocks per CU
-    nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
+    nblk_apply = (int)grid_for(nv, kBlock, 2048);
   }
   // chunked enqueue; profiling records HIP events around every iteration launch
   int const chunk = 8;
