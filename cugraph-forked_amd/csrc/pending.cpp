@@ -2,10 +2,6 @@
 #include "capi.hpp"
 
 namespace cgx {
-void run_louvain(handle_t&, graph_t&, size_t, double, bool, clustering_result_t&)
-{
-  fail(CUGRAPH_NOT_IMPLEMENTED, "Louvain: not built yet");
-}
 void mg_run_pagerank(handle_t&, graph_t&, array_view_t const*, array_view_t const*, array_view_t const*,
                      array_view_t const*, array_view_t const*, array_view_t const*, double, double, size_t, bool,
                      centrality_result_t&)

@@ -1,0 +1,128 @@
+"""Louvain parity (csrc/louvain.hip through cugraph_louvain) against the oracle
+(oracle/louvain.py) and the reference's golden vectors.
+
+Integer weights make every sum exact in any order, so there the clustering must be
+identical to the oracle's; with fractional weights the modularity must agree
+within 1e-6 relative and equal the modularity of the returned partition."""
+import numpy as np
+import pytest
+
+from conftest import dataset_path
+from gpu_util import host, make_graph, plc
+from oracle import graph as og
+from oracle import louvain as olv
+from oracle import rmat
+
+pytestmark = pytest.mark.gpu
+
+
+def run(h, G, max_level=100, resolution=1.0):
+    v, c, q = plc().louvain(h, G, max_level, resolution, False)
+    return host(v), host(c), q
+
+
+def oracle_run(src, dst, w, renumber, max_level=100, resolution=1.0):
+    G = og.create_graph(src, dst, w, renumber=renumber)
+    s, d, ww = G.coo()
+    c, q, levels = olv.louvain(G.num_vertices, s, d, ww, max_level, resolution)
+    return G, c, q, levels
+
+
+def test_c_golden(golden):
+    g = golden["louvain_c"]
+    h, G = make_graph(g["src"], g["dst"], g["w"], renumber=False)
+    v, c, q = run(h, G, g["max_level"], g["resolution"])
+    assert v.tolist() == list(range(g["num_vertices"]))
+    assert c.tolist() == g["expected_clusters"]
+    assert abs(q - g["expected_modularity"]) <= g["tol"] * abs(g["expected_modularity"])
+
+
+def test_pylib_golden(golden):
+    g = golden["louvain_pylib"]
+    h, G = make_graph(g["src"], g["dst"], g["w"], renumber=True, symmetric=True)
+    v, c, q = run(h, G, g["max_level"], g["resolution"])
+    assert v.tolist() == g["expected_vertices"]
+    assert c.tolist() == g["expected_clusters"]
+    assert q == pytest.approx(g["expected_modularity"], abs=1e-12)
+
+
+def test_karate_gtest(golden):
+    g = golden["louvain_karate_gtest"]
+    s, d, w = og.read_csv(dataset_path(g["dataset"]))
+    h, G = make_graph(s, d, w, renumber=False, symmetric=True)
+    v, c, q = run(h, G, g["max_level"], g["resolution"])
+    assert h.last_louvain_levels() == g["expected_level"]
+    a, b = np.float32(q), np.float32(g["expected_modularity"])
+    assert abs(int(a.view(np.int32)) - int(b.view(np.int32))) <= 4  # ASSERT_FLOAT_EQ
+    _, oc, oq, _ = oracle_run(s, d, w, renumber=False)
+    assert np.array_equal(c, oc) and q == oq
+
+
+@pytest.mark.parametrize("name", ["dolphins.csv", "netscience.csv", "polbooks.csv"])
+def test_datasets_vs_oracle(name):
+    s, d, w = og.read_csv(dataset_path(name))
+    h, G = make_graph(s, d, w, renumber=True, symmetric=True)
+    v, c, q = run(h, G)
+    OG, oc, oq, olevels = oracle_run(s, d, w, renumber=True)
+    assert np.array_equal(v, OG.number_map)
+    assert h.last_louvain_levels() == olevels
+    assert abs(q - oq) <= 1e-6 * abs(oq)
+    ss, dd, ww = OG.coo()
+    assert abs(olv.modularity(ss, dd, ww, c) - q) <= 1e-6 * abs(q)
+
+
+@pytest.mark.parametrize("scale,integer", [(10, True), (12, True), (12, False)])
+def test_rmat_vs_oracle(scale, integer):
+    s, d = rmat.rmat(scale, 16 << scale, seed=7)
+    w = rmat.rmat_weights(s.size, seed=8).astype(np.float64)
+    if integer:
+        w = np.floor(w * 8.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    h, G = make_graph(s, d, w.astype(np.float32), renumber=True, symmetric=True)
+    v, c, q = run(h, G)
+    OG, oc, oq, olevels = oracle_run(s, d, w.astype(np.float32).astype(np.float64), renumber=True)
+    assert np.array_equal(v, OG.number_map)
+    ss, dd, ww = OG.coo()
+    if integer:
+        assert np.array_equal(c, oc)
+        assert q == oq
+        assert h.last_louvain_levels() == olevels
+    else:
+        assert abs(q - oq) <= 1e-6 * abs(oq)
+    assert abs(olv.modularity(ss, dd, ww, c) - q) <= 1e-6 * abs(q)
+
+
+def test_resolution_and_max_level():
+    s, d, w = og.read_csv(dataset_path("karate.csv"))
+    for res, ml in ((0.5, 100), (1.0, 1), (2.0, 2)):
+        h, G = make_graph(s, d, w, renumber=False, symmetric=True)
+        v, c, q = run(h, G, ml, res)
+        _, oc, oq, olevels = oracle_run(s, d, w, renumber=False, max_level=ml, resolution=res)
+        assert np.array_equal(c, oc) and q == pytest.approx(oq, rel=1e-12)
+        assert h.last_louvain_levels() == olevels <= ml
+
+
+def test_int64_and_double():
+    s, d, w = og.read_csv(dataset_path("karate.csv"))
+    h, G = make_graph(s, d, w, renumber=True, symmetric=True, vdtype=np.int64, wdtype=np.float64)
+    v, c, q = run(h, G)
+    assert c.dtype == np.int64
+    OG, oc, oq, _ = oracle_run(s, d, w, renumber=True)
+    assert np.array_equal(c, oc) and q == oq
+
+
+def test_unweighted_graph_fails():
+    s, d, _ = og.read_csv(dataset_path("karate.csv"))
+    h, G = make_graph(s, d, None, renumber=False, symmetric=True)
+    with pytest.raises(RuntimeError, match="weighted"):
+        run(h, G)
+
+
+def test_repeat_is_deterministic():
+    s, d = rmat.rmat(12, 16 << 12, seed=3)
+    w = rmat.rmat_weights(s.size, seed=4)
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    h, G = make_graph(s, d, w.astype(np.float32), renumber=True, symmetric=True)
+    a = run(h, G)
+    b = run(h, G)
+    assert np.array_equal(a[1], b[1]) and a[2] == b[2]
