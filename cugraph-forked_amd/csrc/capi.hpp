@@ -18,12 +18,13 @@
 
 namespace cgx {
 
-struct comm_t;  // comm.hpp (multi-GPU); nullptr for single GPU
+struct mg_graph_t;  // mg_graph.hpp
+struct mg_context;  // comm.hpp (multi-GPU); nullptr for single GPU
 
 struct handle_t {
   int device         = 0;
   hipStream_t stream = nullptr;
-  comm_t* comm       = nullptr;
+  mg_context* mg     = nullptr;
   bool profiling     = false;
   // statistics of the last algorithm call (see include/cugraph_amd/ext.h)
   size_t last_iterations     = 0;
@@ -64,6 +65,19 @@ struct err_t {
   std::string message;
 };
 
+// PageRank windowed-push schedule of one edge set (pagerank.hip): packed entries
+// sorted by (destination window, source), work units and fixed-point accumulators
+struct pr_push_t {
+  bool built = false;
+  bool ok    = false;  // ids and edge positions fit the 32-bit packing
+  buffer ent;          // uint32[E]: (source - segment base) << 13 | (destination - window base)
+  buffer ew;           // weight_t[E] for weighted graphs
+  buffer units;        // push_unit[nunits]
+  int64_t nunits = 0;
+  buffer acc;          // u64[nacc] fixed-point sums, zero between iterations
+  int64_t nacc = 0;
+};
+
 // One orientation of the adjacency: majors (rows) -> minors (indices).
 struct adjacency_t {
   buffer offsets;  // edge_t[V+1]
@@ -76,14 +90,7 @@ struct adjacency_t {
   std::vector<int64_t> bin_begin;       // positions (in processing order) where each bin starts
   buffer items;                         // work items for the SpMV-like kernels
   int64_t num_items = 0;
-  // edge-tiled PageRank schedule (pagerank.hip, identity order only)
-  bool pr_valid = false;    // PageRank push schedule built (pagerank.hip)
-  bool pr_push_ok = false;  // ids and edge positions fit the 32-bit packing
-  buffer pr_ent;            // uint32[E] push entries (source offset << 13 | window offset)
-  buffer pr_ew;             // their weights (weighted graphs)
-  buffer pr_units;          // push work units
-  int64_t pr_nunits = 0;
-  buffer pr_acc;            // u64[windows * 8192] fixed-point accumulators
+  pr_push_t pr;  // PageRank windowed-push schedule (pagerank.hip), built on first use
 };
 
 struct graph_t {
@@ -108,7 +115,7 @@ struct graph_t {
   // cached per-vertex out-weight sums (weight_t[V]) and their dangling mask source
   bool outw_valid = false;
   buffer outw;
-  void* mg = nullptr;  // multi-GPU partition state (mg_graph.hpp)
+  std::shared_ptr<mg_graph_t> mg;  // multi-GPU partition state (mg_graph.hpp); null for SG
 };
 
 struct centrality_result_t {

@@ -5,6 +5,7 @@
 //   cpp/src/c_api/resource_handle.cpp, error.cpp, array.cpp, graph_sg.cpp:231-330
 // (argument checks, error codes, ownership); the storage behind them is our own.
 #include "capi.hpp"
+#include "comm.hpp"
 
 #include <cugraph_amd/ext.h>
 
@@ -61,10 +62,6 @@ void set_err(cugraph_error_t** error, char const* msg)
 
 }  // namespace
 
-namespace cgx {
-void* comm_from_raft_handle(void* p);  // comm.cpp
-int comm_rank(comm_t* c);
-}  // namespace cgx
 
 // ============================================================== resource handle
 extern "C" cugraph_resource_handle_t* cugraph_create_resource_handle(void* raft_handle)
@@ -72,7 +69,7 @@ extern "C" cugraph_resource_handle_t* cugraph_create_resource_handle(void* raft_
   try {
     auto* h   = new handle_t{};
     h->stream = make_stream(h->device);
-    h->comm   = static_cast<comm_t*>(raft_handle ? comm_from_raft_handle(raft_handle) : nullptr);
+    h->mg     = static_cast<mg_context*>(raft_handle);  // cugraph_amd_mg_context_t (comm.h) or NULL
     return reinterpret_cast<cugraph_resource_handle_t*>(h);
   } catch (...) {
     return nullptr;
@@ -82,7 +79,7 @@ extern "C" cugraph_resource_handle_t* cugraph_create_resource_handle(void* raft_
 extern "C" int cugraph_resource_handle_get_rank(const cugraph_resource_handle_t* handle)
 {
   auto* h = H(handle);
-  return (h && h->comm) ? comm_rank(h->comm) : 0;
+  return (h && h->mg) ? h->mg->rank() : 0;
 }
 
 extern "C" void cugraph_free_resource_handle(cugraph_resource_handle_t* handle)

@@ -27,8 +27,12 @@
 // formulation) = 4E (indices) + 4V (offsets, int32) + 4V (x~ read)
 // + 4V (pr' write) + 4V (outw) [+4E weights] = 4E + 16V.
 #include "capi.hpp"
+#include "comm.hpp"
+#include "mg_graph.hpp"
 #include "prims.hpp"
 #include "schedule.hpp"
+
+#include <rocprim/device/device_reduce_by_key.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -62,12 +66,36 @@ struct pr_args {
   double alpha;
   double eps;
   int max_iter;
-  int64_t nv;
+  int64_t nv;         // vertices this process updates
+  int64_t nv_global;  // |V| of the graph (teleport base)
   double* partials;
   pr_state* st;
+  double* mg_sums;  // multi-GPU: (diff, dangling) of this rank, allreduced before k_mg_finish
 };
 
 namespace {
+
+// next iteration's base, convergence flag and iteration count from the global
+// L1 difference d and dangling mass g (pagerank_impl.cuh:209-292)
+template <typename V, typename E, typename R>
+__device__ void update_state(pr_args<V, E, R> const& a, double d, double g, bool count_iter)
+{
+  pr_state* st    = a.st;
+  int it          = st->iter + (count_iter ? 1 : 0);
+  st->iter        = it;
+  st->diff        = d;
+  st->dangling    = g;
+  double pf       = g * a.alpha + (1.0 - a.alpha);
+  st->pers_factor = pf;
+  st->base        = a.pers ? 0.0 : pf / (double)a.nv_global;
+  int done        = 0;
+  if (count_iter) {
+    if (d < a.eps) done = 1;
+    else if (it >= a.max_iter) done = 2;
+  }
+  st->ticket = 0;
+  st->done   = done;
+}
 
 // the last-arriving block reduces the per-block (diff, dangling) partials and
 // updates the iteration state (cdna_hip_programming.md §6 Guideline 16 ticket form)
@@ -96,22 +124,21 @@ __device__ void finish_iteration(pr_args<V, E, R> const& a, double my_diff, doub
   d = block_sum_256(d, sm);
   g = block_sum_256(g, sm);
   if (threadIdx.x == 0) {
-    pr_state* st    = a.st;
-    int it          = st->iter + (count_iter ? 1 : 0);
-    st->iter        = it;
-    st->diff        = d;
-    st->dangling    = g;
-    double pf       = g * a.alpha + (1.0 - a.alpha);
-    st->pers_factor = pf;
-    st->base        = a.pers ? 0.0 : pf / (double)a.nv;
-    int done        = 0;
-    if (count_iter) {
-      if (d < a.eps) done = 1;
-      else if (it >= a.max_iter) done = 2;
+    if (a.mg_sums) {
+      a.mg_sums[0] = d;
+      a.mg_sums[1] = g;
+      a.st->ticket = 0;
+    } else {
+      update_state<V, E, R>(a, d, g, count_iter);
     }
-    st->ticket = 0;
-    st->done   = done;
   }
+}
+
+// multi-GPU: the state update from the allreduced (diff, dangling)
+template <typename V, typename E, typename R>
+__global__ void k_mg_finish(pr_args<V, E, R> a, bool count_iter)
+{
+  if (threadIdx.x == 0 && blockIdx.x == 0) update_state<V, E, R>(a, a.mg_sums[0], a.mg_sums[1], count_iter);
 }
 
 // init: x~ = pr / outw, dangling mass of the initial vector
@@ -448,32 +475,29 @@ __global__ void k_unit_ends(push_unit* units, int64_t nunits, int64_t ne)
     units[i].k1 = i + 1 < nunits ? units[i + 1].k0 : ne;
 }
 
-template <typename V, typename E, typename R>
-void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
+// Push schedule of an edge list given as (row = destination, col = source) with
+// destinations in [0, n_rows) and sources in [0, n_cols) -- the SG pull adjacency
+// or one MG 2D block.
+template <typename C, typename R>
+void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
+                         int64_t n_cols, pr_push_t& pp)
 {
-  hipStream_t s = h.stream;
-  int64_t nv    = g.num_vertices;
-  int64_t ne    = g.num_edges;
-  adj.pr_valid  = true;
-  adj.pr_push_ok = (uint64_t)nv < (1ull << 32) && (uint64_t)ne < (1ull << 32);
-  if (!adj.pr_push_ok) return;
-  int64_t nwin = (nv + kWin - 1) / kWin;
-  adj.pr_acc.set_stream(s);
-  adj.pr_acc.resize(std::max<int64_t>(nwin * kWin, 1) * sizeof(unsigned long long));
-  HIP_CHECK(hipMemsetAsync(adj.pr_acc.data(), 0, std::max<int64_t>(nwin * kWin, 1) * sizeof(unsigned long long), s));
-  adj.pr_nunits = 0;
+  pp.built = true;
+  pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
+  if (!pp.ok) return;
+  int64_t nwin = (n_rows + kWin - 1) / kWin;
+  pp.nacc      = std::max<int64_t>(nwin * kWin, 1);
+  pp.acc.set_stream(s);
+  pp.acc.resize(pp.nacc * sizeof(unsigned long long));
+  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
+  pp.nunits = 0;
   if (ne == 0) return;
-  E const* off = adj.offsets.data<E>();
-  V const* idx = adj.indices.data<V>();
-  dbuf<uint32_t> rows(ne, s);
-  hipLaunchKernelGGL(k_edge_rows<E>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, off, nv, ne, rows.data());
-  CGX_LAUNCH_CHECK();
   dbuf<uint64_t> keys_out(ne, s);
   dbuf<uint32_t> vals_out(ne, s);
   {
     dbuf<uint64_t> keys(ne, s);
     dbuf<uint32_t> vals(ne, s);
-    hipLaunchKernelGGL(k_push_keys<V>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, idx, rows.data(), ne,
+    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne,
                        keys.data(), vals.data());
     CGX_LAUNCH_CHECK();
     radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
@@ -486,23 +510,42 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
   fill<uint32_t>(flag.data() + ne, 1, 0u, s);
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
   int64_t nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
-  adj.pr_ent.set_stream(s);
-  adj.pr_ent.resize(ne * sizeof(uint32_t));
-  adj.pr_ew.set_stream(s);
-  if (g.weighted) adj.pr_ew.resize(ne * sizeof(R));
-  else adj.pr_ew.release();
-  adj.pr_units.set_stream(s);
-  adj.pr_units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
+  pp.ent.set_stream(s);
+  pp.ent.resize(ne * sizeof(uint32_t));
+  pp.ew.set_stream(s);
+  if (w) pp.ew.resize(ne * sizeof(R));
+  else pp.ew.release();
+  pp.units.set_stream(s);
+  pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
   hipLaunchKernelGGL(k_push_pack<R>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                     vals_out.data(), rows.data(), g.weighted ? adj.weights.data<R>() : nullptr, flag.data(),
-                     uid.data(), ne, adj.pr_ent.data<uint32_t>(), g.weighted ? adj.pr_ew.data<R>() : nullptr,
-                     adj.pr_units.data<push_unit>());
+                     vals_out.data(), rows, w, flag.data(), uid.data(), ne, pp.ent.data<uint32_t>(),
+                     w ? pp.ew.data<R>() : nullptr, pp.units.data<push_unit>());
   CGX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s,
-                     adj.pr_units.data<push_unit>(), nunits, ne);
+                     pp.units.data<push_unit>(), nunits, ne);
   CGX_LAUNCH_CHECK();
-  adj.pr_nunits = nunits;
+  pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
+}
+
+template <typename V, typename E, typename R>
+void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
+{
+  hipStream_t s = h.stream;
+  int64_t nv    = g.num_vertices;
+  int64_t ne    = g.num_edges;
+  if ((uint64_t)ne >= (1ull << 32) || (uint64_t)nv >= (1ull << 32)) {
+    adj.pr.built = true;
+    adj.pr.ok    = false;
+    return;
+  }
+  dbuf<uint32_t> rows(std::max<int64_t>(ne, 1), s);
+  if (ne)
+    hipLaunchKernelGGL(k_edge_rows<E>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, adj.offsets.data<E>(),
+                       nv, ne, rows.data());
+  CGX_LAUNCH_CHECK();
+  build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), g.weighted ? adj.weights.data<R>() : nullptr, ne,
+                            nv, nv, adj.pr);
 }
 
 template <typename V, typename R>
@@ -646,6 +689,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   a.eps      = eps;
   a.max_iter = (int)std::min<size_t>(max_iter, (size_t)INT32_MAX);
   a.nv       = nv;
+  a.nv_global = nv;
   a.partials = partials.data();
   a.st       = st.data();
   a.x_in     = nullptr;
@@ -658,17 +702,17 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   // windowed push (our own out-weight sums keep every fixed-point sum <= 1; user
   // precomputed out-weights may not: generic pull kernel then)
   bool push = pow_v == nullptr;
-  if (push && !adj.pr_valid) build_pr_push_schedule<V, E, R>(h, g, adj);
-  push = push && adj.pr_push_ok;
+  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj);
+  push = push && adj.pr.ok;
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
   auto pkernel = g.weighted ? k_pr_push<V, E, R, true> : k_pr_push<V, E, R, false>;
   if (push) {
-    sa.ent    = adj.pr_ent.data<uint32_t>();
-    sa.ew     = g.weighted ? adj.pr_ew.data<R>() : nullptr;
-    sa.units  = adj.pr_units.data<push_unit>();
-    sa.nunits = adj.pr_nunits;
-    sa.acc    = adj.pr_acc.data<unsigned long long>();
+    sa.ent    = adj.pr.ent.data<uint32_t>();
+    sa.ew     = g.weighted ? adj.pr.ew.data<R>() : nullptr;
+    sa.units  = adj.pr.units.data<push_unit>();
+    sa.nunits = adj.pr.nunits;
+    sa.acc    = adj.pr.acc.data<unsigned long long>();
     if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
     nblk_push  = (int)std::min<int64_t>(sa.nunits, 256 * 2);  // 64 KB LDS: two blocks per CU
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
@@ -733,6 +777,241 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   if (hst.done == 2) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
 }
 
+// ---------------------------------------------------------------- multi-GPU (2D partition)
+// Rank (r, c) holds the edges whose source is owned by row r and destination by
+// column c (mg_graph.hpp).  Per iteration (pagerank_impl.cuh:241-257 MG path):
+//   row allgather of x~ (each rank's owned slice, padded to the row's largest) ->
+//   windowed push over the local block into fixed-point sums for the column's
+//   destinations -> column reduce-scatter (u64 sums: exact) -> apply on the owned
+//   vertices -> world allreduce of (diff, dangling) -> state update.
+// Everything is stream-ordered; the host reads the convergence flag once per chunk.
+struct mg_pr_block {
+  int64_t nmax_row = 0, nmax_col = 0;
+  pr_push_t pp;
+  buffer outw;  // weight_t[n_own]
+};
+
+template <typename V>
+__global__ void k_mg_block_coo(V const* src, V const* dst, int64_t ne, int64_t const* voff, int P, int C,
+                               int64_t nmax_row, int64_t nmax_col, uint32_t* rows, uint32_t* cols)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    int ou  = mg_owner_of_global((int64_t)src[e], voff, P);
+    int ov  = mg_owner_of_global((int64_t)dst[e], voff, P);
+    cols[e] = (uint32_t)((ou % C) * nmax_row + ((int64_t)src[e] - voff[ou]));
+    rows[e] = (uint32_t)((ov / C) * nmax_col + ((int64_t)dst[e] - voff[ov]));
+  }
+}
+
+template <typename R>
+__global__ void k_weight_or_one(R const* w, int64_t n, double* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = w ? (double)w[i] : 1.0;
+}
+
+__global__ void k_scatter_sums(uint32_t const* keys, double const* vals, int64_t n, double* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[keys[i]] = vals[i];
+}
+
+template <typename R>
+__global__ void k_to_weight(double const* in, int64_t n, R* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (R)in[i];
+}
+
+template <typename V, typename E, typename R>
+__global__ void k_mg_finish_guarded(pr_args<V, E, R> a, bool count_iter)
+{
+  // after convergence the (stale) sums are allreduced again: never touch a finished state
+  if (threadIdx.x == 0 && blockIdx.x == 0 && !a.st->done) update_state<V, E, R>(a, a.mg_sums[0], a.mg_sums[1], count_iter);
+}
+
+template <typename V, typename E, typename R>
+mg_pr_block& mg_block(handle_t& h, graph_t& g)
+{
+  mg_graph_t& mg = *g.mg;
+  if (mg.pr_block) return *static_cast<mg_pr_block*>(mg.pr_block.get());
+  hipStream_t s = h.stream;
+  mg_context& ctx = *h.mg;
+  auto blk      = std::make_shared<mg_pr_block>();
+  int const P = mg.P, C = mg.C, R_ = mg.R, r = mg.p / C, c = mg.p % C;
+  for (int q = 0; q < C; ++q) blk->nmax_row = std::max(blk->nmax_row, mg.voff[r * C + q + 1] - mg.voff[r * C + q]);
+  for (int q = 0; q < R_; ++q) blk->nmax_col = std::max(blk->nmax_col, mg.voff[q * C + c + 1] - mg.voff[q * C + c]);
+  int64_t const ne = mg.ne, n_cols = C * blk->nmax_row, n_rows = R_ * blk->nmax_col;
+  dbuf<int64_t> voff_d(P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  dbuf<uint32_t> rows(std::max<int64_t>(ne, 1), s), cols(std::max<int64_t>(ne, 1), s);
+  if (ne)
+    hipLaunchKernelGGL(k_mg_block_coo<V>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, mg.src.data<V>(),
+                       mg.dst.data<V>(), ne, voff_d.data(), P, C, blk->nmax_row, blk->nmax_col, rows.data(),
+                       cols.data());
+  CGX_LAUNCH_CHECK();
+  build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), g.weighted ? mg.w.data<R>() : nullptr, ne, n_rows,
+                                   n_cols, blk->pp);
+  int64_t bad = ctx.world->host_allreduce<int64_t>(blk->pp.ok ? 0 : 1, CGX_COMM_SUM, s);
+  CGX_EXPECTS(bad == 0, CUGRAPH_NOT_IMPLEMENTED, "MG PageRank: a 2D block exceeds the 32-bit push packing");
+  // out-weight sums: per-block partials (sorted, deterministic) -> row reduce-scatter
+  dbuf<double> part(std::max<int64_t>(n_cols, 1), s), own(std::max<int64_t>(blk->nmax_row, 1), s);
+  fill<double>(part.data(), std::max<int64_t>(n_cols, 1), 0.0, s);
+  if (ne) {
+    dbuf<double> wv(ne, s), wv2(ne, s), sums(ne, s);
+    dbuf<uint32_t> k2(ne, s), uk(ne, s);
+    hipLaunchKernelGGL(k_weight_or_one<R>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s,
+                       g.weighted ? mg.w.data<R>() : nullptr, ne, wv.data());
+    CGX_LAUNCH_CHECK();
+    radix_sort_pairs<uint32_t, double>(cols.data(), k2.data(), wv.data(), wv2.data(), ne, 0,
+                                       bits_for((unsigned long long)std::max<int64_t>(n_cols - 1, 1)), s);
+    dbuf<unsigned long long> nu(1, s);
+    size_t tmp = 0;
+    HIP_CHECK(rocprim::reduce_by_key(nullptr, tmp, k2.data(), wv2.data(), (size_t)ne, uk.data(), sums.data(),
+                                     nu.data(), rocprim::plus<double>(), rocprim::equal_to<uint32_t>(), s));
+    buffer t(tmp, s);
+    HIP_CHECK(rocprim::reduce_by_key(t.data(), tmp, k2.data(), wv2.data(), (size_t)ne, uk.data(), sums.data(),
+                                     nu.data(), rocprim::plus<double>(), rocprim::equal_to<uint32_t>(), s));
+    int64_t n_u = (int64_t)to_host_scalar(nu.data(), s);
+    hipLaunchKernelGGL(k_scatter_sums, dim3(grid_for(n_u, kBlock, 16384)), dim3(kBlock), 0, s, uk.data(), sums.data(),
+                       n_u, part.data());
+    CGX_LAUNCH_CHECK();
+  }
+  ctx.row->reduce_scatter<double>(part.data(), own.data(), (size_t)blk->nmax_row, CGX_COMM_SUM, s);
+  int64_t n_own = mg.n_own();
+  blk->outw.set_stream(s);
+  blk->outw.resize(std::max<int64_t>(n_own, 1) * sizeof(R));
+  if (n_own)
+    hipLaunchKernelGGL(k_to_weight<R>, dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s, own.data(), n_own,
+                       blk->outw.data<R>());
+  CGX_LAUNCH_CHECK();
+  HIP_CHECK(hipStreamSynchronize(s));
+  mg.pr_block = blk;
+  return *blk;
+}
+
+template <typename V, typename E, typename R>
+void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t max_iter, centrality_result_t& res)
+{
+  hipStream_t s   = h.stream;
+  mg_context& ctx = *h.mg;
+  mg_graph_t& mg  = *g.mg;
+  CGX_INPUT(alpha >= 0.0 && alpha <= 1.0, "Invalid input argument: alpha should be in [0.0, 1.0].");
+  CGX_INPUT(eps >= 0.0, "Invalid input argument: epsilon should be non-negative.");
+  int64_t const n_own = mg.n_own();
+  res.vertices        = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
+  if (n_own)
+    HIP_CHECK(hipMemcpyAsync(res.vertices->buf.data(), g.number_map.data(), n_own * sizeof(V), hipMemcpyDeviceToDevice,
+                             s));
+  res.values = std::make_unique<device_array_t>((size_t)n_own, dtype_of<R>(), s);
+  h.last_iterations   = 0;
+  h.last_hot_ms       = 0;
+  h.last_hot_launches = 0;
+  if (g.num_vertices == 0) return;
+  mg_pr_block& blk = mg_block<V, E, R>(h, g);
+  int const C = mg.C, R_ = mg.R;
+
+  R* pr = res.values->buf.data<R>();
+  fill<R>(pr, std::max<int64_t>(n_own, 0), (R)(R(1.0) / (R)g.num_vertices), s);
+  dbuf<R> x_send(std::max<int64_t>(blk.nmax_row, 1), s), x_row(std::max<int64_t>(C * blk.nmax_row, 1), s);
+  fill<R>(x_send.data(), std::max<int64_t>(blk.nmax_row, 1), R(0), s);
+  dbuf<unsigned long long> acc_own(std::max<int64_t>(blk.nmax_col, 1), s);
+  fill<unsigned long long>(acc_own.data(), std::max<int64_t>(blk.nmax_col, 1), 0ull, s);
+  dbuf<double> partials(2 * 4096, s), sums(2, s);
+  dbuf<pr_state> st(1, s);
+  HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(pr_state), s));
+
+  pr_args<V, E, R> a{};
+  a.pr        = pr;
+  a.outw      = blk.outw.data<R>();
+  a.alpha     = alpha;
+  a.eps       = eps;
+  a.max_iter  = (int)std::min<size_t>(max_iter, (size_t)INT32_MAX);
+  a.nv        = n_own;
+  a.nv_global = g.num_vertices;
+  a.partials  = partials.data();
+  a.st        = st.data();
+  a.mg_sums   = sums.data();
+  a.x_in      = x_row.data();
+  a.x_out     = x_send.data();
+  int const nblk_init = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 1024);
+  hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
+  CGX_LAUNCH_CHECK();
+  ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
+  hipLaunchKernelGGL((k_mg_finish<V, E, R>), dim3(1), dim3(64), 0, s, a, false);
+  CGX_LAUNCH_CHECK();
+  if (max_iter == 0) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
+
+  push_args<V, E, R> sp{}, sap{};
+  sp.a      = a;
+  sp.ent    = blk.pp.ent.data<uint32_t>();
+  sp.ew     = g.weighted ? blk.pp.ew.data<R>() : nullptr;
+  sp.units  = blk.pp.units.data<push_unit>();
+  sp.nunits = blk.pp.nunits;
+  sp.acc    = blk.pp.acc.data<unsigned long long>();
+  sap       = sp;
+  sap.acc   = acc_own.data();
+  int const nblk_push  = (int)std::min<int64_t>(sp.nunits, 256 * 2);
+  int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
+  size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
+
+  int const chunk = 8;
+  std::vector<hipEvent_t> ev;
+  pr_state hst{};
+  pr_state* hpin = nullptr;
+  HIP_CHECK(hipHostMalloc((void**)&hpin, sizeof(pr_state), hipHostMallocDefault));
+  try {
+    while (true) {
+      for (int i = 0; i < chunk; ++i) {
+        if (h.profiling) {
+          hipEvent_t e0, e1;
+          HIP_CHECK(hipEventCreate(&e0));
+          HIP_CHECK(hipEventCreate(&e1));
+          ev.push_back(e0);
+          ev.push_back(e1);
+          HIP_CHECK(hipEventRecord(e0, s));
+        }
+        ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
+        if (nblk_push)
+          hipLaunchKernelGGL((g.weighted ? k_pr_push<V, E, R, true> : k_pr_push<V, E, R, false>), dim3(nblk_push),
+                             dim3(kPushThreads), 0, s, sp);
+        CGX_LAUNCH_CHECK();
+        ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
+        if (block_acc_bytes) HIP_CHECK(hipMemsetAsync(sp.acc, 0, block_acc_bytes, s));
+        hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
+        CGX_LAUNCH_CHECK();
+        ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
+        hipLaunchKernelGGL((k_mg_finish_guarded<V, E, R>), dim3(1), dim3(64), 0, s, a, true);
+        CGX_LAUNCH_CHECK();
+        if (h.profiling) HIP_CHECK(hipEventRecord(ev.back(), s));
+      }
+      HIP_CHECK(hipMemcpyAsync(hpin, st.data(), sizeof(pr_state), hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      hst = *hpin;
+      if (hst.done) break;
+    }
+  } catch (...) {
+    (void)hipHostFree(hpin);
+    for (auto e : ev) (void)hipEventDestroy(e);
+    throw;
+  }
+  HIP_CHECK(hipHostFree(hpin));
+  h.last_iterations = (size_t)hst.iter;
+  if (h.profiling) {
+    double tot = 0;
+    size_t k   = std::min<size_t>((size_t)hst.iter, ev.size() / 2);
+    for (size_t i = 0; i < k; ++i) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+      tot += ms;
+    }
+    for (auto e : ev) HIP_CHECK(hipEventDestroy(e));
+    h.last_hot_ms       = tot;
+    h.last_hot_launches = k;
+  }
+  if (hst.done == 2) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
+}
+
 }  // namespace
 
 void run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view_t const* pow_s,
@@ -747,4 +1026,22 @@ void run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view
   });
 }
 
+}  // namespace cgx
+
+namespace cgx {
+void mg_run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view_t const* pow_s,
+                     array_view_t const* guess_v, array_view_t const* guess_s, array_view_t const* pers_v,
+                     array_view_t const* pers_s, double alpha, double eps, size_t max_iter, bool /*expensive*/,
+                     centrality_result_t& res)
+{
+  CGX_EXPECTS(h.mg != nullptr, CUGRAPH_INVALID_HANDLE, "multi-GPU graph used with a single-GPU resource handle");
+  CGX_EXPECTS(pow_v == nullptr && pow_s == nullptr && guess_v == nullptr && guess_s == nullptr &&
+                pers_v == nullptr && pers_s == nullptr,
+              CUGRAPH_NOT_IMPLEMENTED,
+              "multi-GPU PageRank: precomputed out-weights, initial guess and personalization are not supported yet");
+  dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
+    using T = decltype(t);
+    mg_pagerank_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, alpha, eps, max_iter, res);
+  });
+}
 }  // namespace cgx

@@ -17,6 +17,7 @@ from . import _lib
 from ._arrays import DeviceArray, DeviceView, copy_view_to_tensor, optional_view, to_device_tensor, vptr
 
 from . import generators  # noqa: E402,F401  (MI355X build extensions)
+from . import comms  # noqa: E402,F401  (multi-GPU communicator contexts)
 
 __all__ = ["ResourceHandle", "GraphProperties", "SGGraph", "MGGraph", "pagerank",
            "personalized_pagerank", "bfs", "sssp", "louvain", "version"]

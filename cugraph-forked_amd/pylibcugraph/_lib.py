@@ -124,6 +124,12 @@ _proto("cugraph_amd_last_bfs_levels", c_size_t, P)
 _proto("cugraph_amd_last_bfs_bottom_up_steps", c_size_t, P)
 _proto("cugraph_amd_last_louvain_levels", c_size_t, P)
 _proto("cugraph_amd_version", ctypes.c_char_p)
+# multi-GPU communicator contexts (include/cugraph_amd/comm.h)
+_proto("cugraph_amd_comm_unique_id_size", c_size_t)
+_proto("cugraph_amd_comm_get_unique_id", c_int, P, PP)
+_proto("cugraph_amd_mg_context_create_rccl", c_int, P, c_int, c_int, c_int, PP, PP)
+_proto("cugraph_amd_mg_context_create_ops", c_int, P, P, P, c_int, PP, PP)
+_proto("cugraph_amd_mg_context_free", None, P)
 
 
 def assert_success(code, err, api_name):
