@@ -1,0 +1,485 @@
+// Multi-GPU BFS (one process per GPU).
+//
+// Reference: cpp/src/traversal/bfs_impl.cuh:94-287 (MG path: frontier broadcast
+// over the column communicator, all-to-all of (destination, parent) over the row
+// communicator, termination allreduce).  Here every rank owns the
+// out-adjacency of its own vertices (a 1D partition by source owner, built once
+// from the 2D blocks and cached), and a level is either
+//
+//  * top-down: own frontier vertices emit (v, u) candidates; they are sorted by
+//    (v, u), reduced to the smallest parent per v, and sent to v's owner in one
+//    all-to-all (global ids are contiguous per owner, so the sort also groups by
+//    destination rank); owners claim unvisited v with parent = smallest u;
+//  * bottom-up (symmetric graphs, direction_optimizing): the frontier bitmap of
+//    every rank is allgathered (V/8 bytes), each rank scans its unvisited
+//    vertices' sorted adjacency and stops at the first frontier neighbour.
+//
+// Both pick the frontier neighbour with the smallest global id, so distances and
+// predecessors do not depend on the direction schedule (Beamer alpha 14 / beta 24
+// on global counts).  Predecessors are returned as external ids.
+#include "capi.hpp"
+#include "comm.hpp"
+#include "mg_graph.hpp"
+#include "prims.hpp"
+
+#include <rocprim/device/device_select.hpp>
+
+#include <limits>
+
+namespace cgx {
+
+namespace {
+
+inline unsigned blocks(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 16384); }
+
+struct bfs_rows_t {
+  int64_t n_own = 0, ne = 0;
+  buffer off;  // int64[n_own + 1]
+  buffer idx;  // uint32 global ids, ascending per row
+  int64_t words = 0;  // 32-bit words of each rank's bitmap segment (max over ranks)
+};
+
+template <typename V>
+__global__ void k_owner_src(V const* src, int64_t n, int64_t const* voff, int P, int* dest)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dest[i] = mg_owner_of_global((int64_t)src[i], voff, P);
+}
+
+template <typename V>
+__global__ void k_row_keys(V const* src, V const* dst, int64_t n, int64_t base, unsigned long long* keys)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    keys[i] = ((unsigned long long)((int64_t)src[i] - base) << 32) | (unsigned long long)(uint32_t)dst[i];
+}
+
+__global__ void k_split_row_keys(unsigned long long const* keys, int64_t n, uint32_t* row, uint32_t* col)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    row[i] = (uint32_t)(keys[i] >> 32);
+    col[i] = (uint32_t)keys[i];
+  }
+}
+
+__global__ void k_offsets_u32(uint32_t const* row, int64_t ne, int64_t n, int64_t* off)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = ne;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)row[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    off[v] = lo;
+  }
+}
+
+template <typename V>
+bfs_rows_t& mg_rows(handle_t& h, graph_t& g)
+{
+  mg_graph_t& mg = *g.mg;
+  if (mg.bfs_rows) return *static_cast<bfs_rows_t*>(mg.bfs_rows.get());
+  hipStream_t s = h.stream;
+  comm_t& comm  = *h.mg->world;
+  CGX_EXPECTS(g.num_vertices < (int64_t)UINT32_MAX, CUGRAPH_NOT_IMPLEMENTED, "MG BFS: more than 2^32 vertices");
+  auto rows   = std::make_shared<bfs_rows_t>();
+  int const P = mg.P;
+  dbuf<int64_t> voff_d(P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  int64_t ne = mg.ne;
+  // edges of the 2D block -> owner of the source (a 1D partition by rows)
+  dbuf<int> dest(std::max<int64_t>(ne, 1), s);
+  if (ne)
+    hipLaunchKernelGGL(k_owner_src<V>, dim3(blocks(ne)), dim3(kBlock), 0, s, mg.src.data<V>(), ne, voff_d.data(), P,
+                       dest.data());
+  CGX_LAUNCH_CHECK();
+  dbuf<int> d2(std::max<int64_t>(ne, 1), s);
+  dbuf<int64_t> iv(std::max<int64_t>(ne, 1), s), perm(std::max<int64_t>(ne, 1), s);
+  std::vector<size_t> counts(P, 0);
+  if (ne) {
+    iota<int64_t>(iv.data(), ne, 0, s);
+    radix_sort_pairs<int, int64_t>(dest.data(), d2.data(), iv.data(), perm.data(), ne, 0, bits_for(P), s);
+    auto hd = to_host(d2.data(), ne, s);
+    for (auto q : hd) counts[q]++;
+  }
+  dbuf<V> ps(std::max<int64_t>(ne, 1), s), pd(std::max<int64_t>(ne, 1), s);
+  if (ne) {
+    gather<V, int64_t>(ps.data(), mg.src.data<V>(), perm.data(), ne, s);
+    gather<V, int64_t>(pd.data(), mg.dst.data<V>(), perm.data(), ne, s);
+  }
+  std::vector<size_t> rc;
+  auto rs = exchange<V>(comm, ps.data(), counts, rc, s);
+  auto rd = exchange<V>(comm, pd.data(), counts, rc, s);
+  int64_t m = (int64_t)rs.n;
+  rows->n_own = mg.n_own();
+  rows->ne    = m;
+  dbuf<unsigned long long> k1(std::max<int64_t>(m, 1), s), k2(std::max<int64_t>(m, 1), s);
+  dbuf<uint32_t> rr(std::max<int64_t>(m, 1), s);
+  rows->idx.set_stream(s);
+  rows->idx.resize(std::max<int64_t>(m, 1) * sizeof(uint32_t));
+  rows->off.set_stream(s);
+  rows->off.resize((rows->n_own + 1) * sizeof(int64_t));
+  if (m) {
+    hipLaunchKernelGGL(k_row_keys<V>, dim3(blocks(m)), dim3(kBlock), 0, s, rs.data(), rd.data(), m, mg.voff[mg.p],
+                       k1.data());
+    CGX_LAUNCH_CHECK();
+    radix_sort_keys<unsigned long long>(k1.data(), k2.data(), m, 0, 64, s);
+    hipLaunchKernelGGL(k_split_row_keys, dim3(blocks(m)), dim3(kBlock), 0, s, k2.data(), m, rr.data(),
+                       rows->idx.data<uint32_t>());
+    CGX_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_offsets_u32, dim3(blocks(rows->n_own + 1)), dim3(kBlock), 0, s, rr.data(), m, rows->n_own,
+                     rows->off.data<int64_t>());
+  CGX_LAUNCH_CHECK();
+  int64_t maxn = 0;
+  for (int q = 0; q < P; ++q) maxn = std::max(maxn, mg.voff[q + 1] - mg.voff[q]);
+  rows->words = std::max<int64_t>((maxn + 31) / 32, 1);
+  HIP_CHECK(hipStreamSynchronize(s));
+  mg.bfs_rows = rows;
+  return *rows;
+}
+
+// ---------------------------------------------------------------- level kernels
+struct level_ctr {
+  unsigned long long next_n;  // own vertices discovered
+  unsigned long long next_m;  // sum of their degrees
+  unsigned long long ncand;   // candidates written
+  unsigned long long pad;
+};
+
+template <typename V>
+__global__ void k_init_sources(V const* src_global, size_t n, int64_t lo, int64_t hi, V* dist, uint32_t* queue,
+                               unsigned long long* nq, int* flag)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    int64_t v = (int64_t)src_global[i];
+    if (v >= lo && v < hi) {
+      int64_t l = v - lo;
+      if (atomicCAS(flag + l, 0, 1) == 0) {
+        dist[l]                      = 0;
+        queue[atomicAdd(nq, 1ull)]   = (uint32_t)l;
+      }
+    }
+  }
+}
+
+// exclusive prefix of frontier degrees is in `pre`; one thread per candidate edge
+template <typename V>
+__global__ void k_td_candidates(uint32_t const* frontier, int64_t nf, unsigned long long const* pre, int64_t m,
+                                int64_t const* off, uint32_t const* idx, int64_t lo, int64_t hi, V const* dist,
+                                unsigned long long* out)
+{
+  V const INF = std::numeric_limits<V>::max();
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t a = 0, b = nf - 1;  // last frontier slot with pre <= t
+    while (a < b) {
+      int64_t mid = (a + b + 1) >> 1;
+      if ((int64_t)pre[mid] <= t) a = mid;
+      else b = mid - 1;
+    }
+    uint32_t u    = frontier[a];
+    int64_t e     = off[u] + (t - (int64_t)pre[a]);
+    uint32_t v    = idx[e];
+    bool visited  = (int64_t)v >= lo && (int64_t)v < hi && dist[(int64_t)v - lo] != INF;  // own: known locally
+    out[t]        = visited ? ~0ull : (((unsigned long long)v << 32) | (unsigned long long)(uint32_t)(lo + u));
+  }
+}
+
+template <typename V>
+__global__ void k_frontier_degrees(uint32_t const* frontier, int64_t nf, int64_t const* off, unsigned long long* deg)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x)
+    deg[i] = (unsigned long long)(off[frontier[i] + 1] - off[frontier[i]]);
+}
+
+// first position with key >= voff[q] << 32, for q in [0, P]
+__global__ void k_split_points(unsigned long long const* keys, int64_t n, int64_t const* voff, int P, int64_t* pos)
+{
+  int q = threadIdx.x;
+  if (q > P) return;
+  unsigned long long bound = q == P ? ~0ull : ((unsigned long long)voff[q] << 32);
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < bound) lo = mid + 1;
+    else hi = mid;
+  }
+  pos[q] = lo;
+}
+
+struct same_v {
+  __host__ __device__ bool operator()(unsigned long long a, unsigned long long b) const { return (a >> 32) == (b >> 32); }
+};
+
+template <typename V>
+__global__ void k_td_claim(unsigned long long const* cand, int64_t n, int64_t lo, V const* dist, long long* best,
+                           int* flag, uint32_t* next, level_ctr* ctr)
+{
+  V const INF = std::numeric_limits<V>::max();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t v = (int64_t)(cand[i] >> 32) - lo;
+    long long u = (long long)(uint32_t)cand[i];
+    if (dist[v] != INF) continue;
+    atomicMin(best + v, u);
+    if (atomicCAS(flag + v, 0, 1) == 0) next[atomicAdd(&ctr->next_n, 1ull)] = (uint32_t)v;
+  }
+}
+
+template <typename V>
+__global__ void k_td_finalize(uint32_t const* next, int64_t n, V depth1, V* dist, V* pred, long long* best,
+                              int64_t const* off, level_ctr* ctr)
+{
+  unsigned long long m = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t v = next[i];
+    dist[v]    = depth1;
+    if (pred) pred[v] = (V)best[v];
+    best[v] = std::numeric_limits<long long>::max();
+    m += (unsigned long long)(off[v + 1] - off[v]);
+  }
+  atomicAdd(&ctr->next_m, m);
+}
+
+__global__ void k_mark_bits(uint32_t const* q, int64_t n, uint32_t* bits)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicOr(bits + (q[i] >> 5), 1u << (q[i] & 31u));
+}
+
+template <typename V>
+__global__ void k_bottom_up(int64_t n_own, int64_t const* off, uint32_t const* idx, V* dist, V* pred,
+                            uint32_t const* bitmap, int64_t const* voff, int P, int64_t words, V depth1, int* flag,
+                            uint32_t* next, level_ctr* ctr)
+{
+  V const INF = std::numeric_limits<V>::max();
+  unsigned long long m = 0;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_own; v += (int64_t)gridDim.x * blockDim.x) {
+    if (dist[v] != INF) continue;
+    for (int64_t e = off[v]; e < off[v + 1]; ++e) {
+      int64_t u = idx[e];
+      int q     = mg_owner_of_global(u, voff, P);
+      int64_t l = u - voff[q];
+      if ((bitmap[q * words + (l >> 5)] >> (l & 31)) & 1u) {
+        dist[v] = depth1;
+        if (pred) pred[v] = (V)u;
+        flag[v] = 1;
+        next[atomicAdd(&ctr->next_n, 1ull)] = (uint32_t)v;
+        m += (unsigned long long)(off[v + 1] - off[v]);
+        break;
+      }
+    }
+  }
+  atomicAdd(&ctr->next_m, m);
+}
+
+template <typename V>
+__global__ void k_fill_pred_none(V* pred, int64_t n)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (pred[i] == std::numeric_limits<V>::max()) pred[i] = (V)-1;
+}
+
+struct deg_sum_f {
+  int64_t const* off;
+  __device__ double operator()(size_t i) const { return (double)(off[i + 1] - off[i]); }
+};
+
+template <typename V>
+void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size_t depth_limit, bool want_pred,
+                 paths_result_t& res)
+{
+  hipStream_t s   = h.stream;
+  mg_context& ctx = *h.mg;
+  comm_t& comm    = *ctx.world;
+  mg_graph_t& mg  = *g.mg;
+  int const P     = mg.P;
+  CGX_INPUT(!dir_opt || g.symmetric,
+            "Invalid input argument: input graph should be symmetric for direction optimizing BFS.");
+  int64_t nsrc_total = comm.host_allreduce<int64_t>((int64_t)sources->size, CGX_COMM_SUM, s);
+  CGX_INPUT(nsrc_total > 0, "Invalid input argument: input should have at least one source");
+  bfs_rows_t& rows = mg_rows<V>(h, g);
+  int64_t const n_own = mg.n_own(), lo = mg.voff[mg.p], hi = mg.voff[mg.p + 1];
+  V const INF = std::numeric_limits<V>::max();
+
+  res.vertices = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
+  if (n_own)
+    HIP_CHECK(hipMemcpyAsync(res.vertices->buf.data(), g.number_map.data(), n_own * sizeof(V), hipMemcpyDeviceToDevice,
+                             s));
+  res.distances    = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
+  res.predecessors = std::make_unique<device_array_t>(want_pred ? (size_t)n_own : 0, g.vertex_type, s);
+  V* dist = res.distances->buf.data<V>();
+  V* pred = want_pred ? res.predecessors->buf.data<V>() : nullptr;
+  fill<V>(dist, std::max<int64_t>(n_own, 0), INF, s);
+  if (pred) fill<V>(pred, std::max<int64_t>(n_own, 0), INF, s);
+  h.last_bfs_levels    = 0;
+  h.last_bfs_bottom_up = 0;
+
+  // sources: external -> global ids (collective), then claimed by their owners
+  dbuf<V> srcg(std::max<size_t>(sources->size, 1), s);
+  if (sources->size)
+    HIP_CHECK(hipMemcpyAsync(srcg.data(), sources->data, sources->size * sizeof(V), hipMemcpyDeviceToDevice, s));
+  mg_ext_to_global(h, g, srcg.data(), sources->size, true);
+  std::vector<size_t> rc;
+  dbuf<V> all_src;
+  {  // every rank sees every source (small)
+    auto counts  = comm.host_allgather<int64_t>((int64_t)sources->size, s);
+    int64_t tot  = 0, mx = 0;
+    for (auto c : counts) tot += c, mx = std::max(mx, c);
+    dbuf<V> pad(std::max<int64_t>(mx, 1), s), gath(std::max<int64_t>(mx * P, 1), s);
+    fill<V>(pad.data(), std::max<int64_t>(mx, 1), (V)-1, s);
+    if (sources->size)
+      HIP_CHECK(hipMemcpyAsync(pad.data(), srcg.data(), sources->size * sizeof(V), hipMemcpyDeviceToDevice, s));
+    comm.allgather<V>(pad.data(), gath.data(), (size_t)std::max<int64_t>(mx, 1), s);
+    all_src = std::move(gath);
+    all_src.n = (size_t)std::max<int64_t>(mx, 1) * P;
+  }
+  dbuf<uint32_t> qa(std::max<int64_t>(n_own, 1), s), qb(std::max<int64_t>(n_own, 1), s);
+  dbuf<int> flag(std::max<int64_t>(n_own, 1), s);
+  fill<int>(flag.data(), std::max<int64_t>(n_own, 1), 0, s);
+  dbuf<long long> best(std::max<int64_t>(n_own, 1), s);
+  fill<long long>(best.data(), std::max<int64_t>(n_own, 1), std::numeric_limits<long long>::max(), s);
+  dbuf<level_ctr> ctr(1, s);
+  HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
+  hipLaunchKernelGGL(k_init_sources<V>, dim3(blocks(all_src.n)), dim3(kBlock), 0, s, all_src.data(), all_src.n, lo, hi,
+                     dist, qa.data(), &ctr.data()->next_n, flag.data());
+  CGX_LAUNCH_CHECK();
+  auto hc  = to_host(ctr.data(), 1, s)[0];
+  int64_t nf_own = (int64_t)hc.next_n;
+
+  dbuf<int64_t> voff_d(P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  dbuf<uint32_t> seg(rows.words, s), bitmap(rows.words * P, s);
+  dbuf<double> scratch(1024, s), dsum(1, s);
+  // m_u: degrees of unvisited vertices (global)
+  double deg_own = 0;
+  if (n_own) {
+    device_sum(deg_sum_f{rows.off.data<int64_t>()}, (size_t)n_own, dsum.data(), scratch.data(), s);
+    deg_own = to_host_scalar(dsum.data(), s);
+  }
+  double m_u = comm.host_allreduce<double>(deg_own, CGX_COMM_SUM, s);
+  double m_f = 0;
+  {
+    // degrees of the initial frontier
+    dbuf<unsigned long long> dg(std::max<int64_t>(nf_own, 1), s);
+    double mf_own = 0;
+    if (nf_own) {
+      hipLaunchKernelGGL(k_frontier_degrees<V>, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own,
+                         rows.off.data<int64_t>(), dg.data());
+      CGX_LAUNCH_CHECK();
+      for (auto x : to_host(dg.data(), nf_own, s)) mf_own += (double)x;
+    }
+    m_f = comm.host_allreduce<double>(mf_own, CGX_COMM_SUM, s);
+    m_u -= m_f;
+  }
+  int64_t nf = comm.host_allreduce<int64_t>(nf_own, CGX_COMM_SUM, s);
+  V limit    = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
+                                               (unsigned long long)std::numeric_limits<V>::max());
+  V depth    = 0;
+  bool bottom_up = false;
+  size_t levels = 0, bu_steps = 0;
+  while (nf > 0 && depth < limit) {
+    if (dir_opt) {
+      if (!bottom_up && m_f > m_u / 14.0) bottom_up = true;
+      else if (bottom_up && (double)nf < (double)g.num_vertices / 24.0) bottom_up = false;
+    }
+    HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
+    V const depth1 = depth + 1;
+    if (bottom_up) {
+      HIP_CHECK(hipMemsetAsync(seg.data(), 0, rows.words * 4, s));
+      if (nf_own)
+        hipLaunchKernelGGL(k_mark_bits, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own, seg.data());
+      CGX_LAUNCH_CHECK();
+      comm.allgather<uint32_t>(seg.data(), bitmap.data(), (size_t)rows.words, s);
+      if (n_own)
+        hipLaunchKernelGGL(k_bottom_up<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
+                           rows.idx.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), P, rows.words, depth1,
+                           flag.data(), qb.data(), ctr.data());
+      CGX_LAUNCH_CHECK();
+      ++bu_steps;
+    } else {
+      // candidates of the own frontier, smallest parent per destination, to the owners
+      dbuf<unsigned long long> dg(std::max<int64_t>(nf_own, 1), s), pre(std::max<int64_t>(nf_own + 1, 1), s);
+      int64_t mcand = 0;
+      if (nf_own) {
+        hipLaunchKernelGGL(k_frontier_degrees<V>, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own,
+                           rows.off.data<int64_t>(), dg.data());
+        CGX_LAUNCH_CHECK();
+        exclusive_scan<unsigned long long, unsigned long long>(dg.data(), pre.data(), nf_own, s);
+        auto last = to_host(pre.data() + nf_own - 1, 1, s)[0] + to_host(dg.data() + nf_own - 1, 1, s)[0];
+        mcand     = (int64_t)last;
+      }
+      dbuf<unsigned long long> cand(std::max<int64_t>(mcand, 1), s), cs(std::max<int64_t>(mcand, 1), s),
+        cu(std::max<int64_t>(mcand, 1), s);
+      int64_t nu = 0;
+      if (mcand) {
+        hipLaunchKernelGGL(k_td_candidates<V>, dim3(blocks(mcand)), dim3(kBlock), 0, s, qa.data(), nf_own,
+                           pre.data(), mcand, rows.off.data<int64_t>(), rows.idx.data<uint32_t>(), lo, hi, dist,
+                           cand.data());
+        CGX_LAUNCH_CHECK();
+        radix_sort_keys<unsigned long long>(cand.data(), cs.data(), mcand, 0, 64, s);
+        dbuf<size_t> cnt(1, s);
+        size_t tmp = 0;
+        HIP_CHECK(rocprim::unique(nullptr, tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v(), s));
+        buffer t(tmp, s);
+        HIP_CHECK(rocprim::unique(t.data(), tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v(), s));
+        nu = (int64_t)to_host_scalar(cnt.data(), s);
+      }
+      // per-owner split points (the sentinel ~0 run, if any, sorts last and is dropped)
+      std::vector<size_t> counts(P, 0);
+      if (nu) {
+        dbuf<int64_t> pos(P + 1, s);
+        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), nu, voff_d.data(), P, pos.data());
+        CGX_LAUNCH_CHECK();
+        auto hp = to_host(pos.data(), P + 1, s);
+        for (int q = 0; q < P; ++q) counts[q] = (size_t)(hp[q + 1] - hp[q]);
+      }
+      std::vector<size_t> rcnt;
+      auto got = exchange<int64_t>(comm, reinterpret_cast<int64_t const*>(cu.data()), counts, rcnt, s);
+      if (got.n)
+        hipLaunchKernelGGL(k_td_claim<V>, dim3(blocks(got.n)), dim3(kBlock), 0, s,
+                           reinterpret_cast<unsigned long long const*>(got.data()), (int64_t)got.n, lo, dist,
+                           best.data(), flag.data(), qb.data(), ctr.data());
+      CGX_LAUNCH_CHECK();
+      auto hn = to_host(ctr.data(), 1, s)[0];
+      if (hn.next_n)
+        hipLaunchKernelGGL(k_td_finalize<V>, dim3(blocks(hn.next_n)), dim3(kBlock), 0, s, qb.data(),
+                           (int64_t)hn.next_n, depth1, dist, pred, best.data(), rows.off.data<int64_t>(), ctr.data());
+      CGX_LAUNCH_CHECK();
+    }
+    auto hn = to_host(ctr.data(), 1, s)[0];
+    nf_own  = (int64_t)hn.next_n;
+    std::swap(qa, qb);
+    dbuf<double> red(2, s);
+    double loc[2] = {(double)hn.next_n, (double)hn.next_m};
+    HIP_CHECK(hipMemcpyAsync(red.data(), loc, sizeof(loc), hipMemcpyHostToDevice, s));
+    comm.allreduce<double>(red.data(), red.data(), 2, CGX_COMM_SUM, s);
+    auto gr = to_host(red.data(), 2, s);
+    nf      = (int64_t)gr[0];
+    m_f     = gr[1];
+    m_u     = m_u > m_f ? m_u - m_f : 0;
+    ++depth;
+    ++levels;
+  }
+  h.last_bfs_levels    = levels;
+  h.last_bfs_bottom_up = bu_steps;
+  if (pred) {
+    if (n_own) hipLaunchKernelGGL(k_fill_pred_none<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, pred, n_own);
+    CGX_LAUNCH_CHECK();
+    mg_global_to_ext(h, g, pred, (size_t)n_own);
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace
+
+void mg_run_bfs(handle_t& h, graph_t& g, array_view_t* sources, bool direction_optimizing, size_t depth_limit,
+                bool compute_predecessors, bool /*expensive*/, paths_result_t& res)
+{
+  CGX_EXPECTS(h.mg != nullptr, CUGRAPH_INVALID_HANDLE, "multi-GPU graph used with a single-GPU resource handle");
+  if (g.vertex_type == INT32)
+    mg_bfs_impl<int32_t>(h, g, sources, direction_optimizing, depth_limit, compute_predecessors, res);
+  else
+    mg_bfs_impl<int64_t>(h, g, sources, direction_optimizing, depth_limit, compute_predecessors, res);
+}
+
+}  // namespace cgx

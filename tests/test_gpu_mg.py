@@ -63,9 +63,10 @@ def _worker(rank, world, port, C, scale, weighted, algo):
         v, x = plc.pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
         mine = (v.cpu().numpy(), x.cpu().numpy())
     else:
-        src = np.unique(s)[:1] if rank == 0 else np.zeros(0, np.int64)
+        root = int(np.unique(s)[0])
+        src = np.array([root], np.int64) if rank == world - 1 else np.zeros(0, np.int64)
         srct = torch.as_tensor(src.astype(np.int32), device="cuda")
-        v, dist_, pred = plc.bfs(h, G, srct, False, 0, True, False)
+        dist_, pred, v = plc.bfs(h, G, srct, algo == "bfs_do", 0, True, False)
         mine = (v.cpu().numpy(), dist_.cpu().numpy(), pred.cpu().numpy())
     allr = [None] * world
     dist.all_gather_object(allr, mine)
@@ -84,12 +85,18 @@ def _worker(rank, world, port, C, scale, weighted, algo):
         else:
             dists = np.concatenate([a[1] for a in allr])
             preds = np.concatenate([a[2] for a in allr])
-            g = og.create_graph(s, d, None, store_transposed=False, renumber=False)
+            n = int(max(s.max(), d.max())) + 1
+            g = og.create_graph(s, d, None, store_transposed=False, renumber=False, vertices=np.arange(n))
             root = int(np.unique(s)[0])
-            rd, rp = obfs.bfs(g.num_vertices, g.offsets, g.indices, [root])
-            assert np.array_equal(dists, rd[verts])
-            # predecessors: the smallest-id frontier neighbour (same rule as SG)
-            assert np.array_equal(preds, rp[verts])
+            rd, _ = obfs.bfs(g.num_vertices, g.offsets, g.indices, [root])
+            assert np.array_equal(dists, rd[verts])  # bit-exact distances
+            # predecessors valid (cpp/tests/traversal/mg_bfs_test.cpp rule): dist[p] + 1 == dist[v], edge p-v
+            reached = (dists != 2**31 - 1) & (verts != root)
+            pv = preds[reached]
+            assert np.array_equal(rd[pv] + 1, dists[reached])
+            adj = set(zip(s.tolist(), d.tolist()))
+            assert all((int(p_), int(v_)) in adj for p_, v_ in zip(pv, verts[reached]))
+            assert np.all(preds[~reached] == -1)
     dist.barrier()
     h = None
     G = None
@@ -101,3 +108,9 @@ def _worker(rank, world, port, C, scale, weighted, algo):
 def test_mg_pagerank_vs_oracle(world, C, weighted):
     import torch.multiprocessing as tmp
     tmp.spawn(_worker, args=(world, _free_port(), C, 11, weighted, "pagerank"), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,C,algo", [(2, 2, "bfs"), (4, 2, "bfs_do"), (3, 3, "bfs_do")])
+def test_mg_bfs_vs_oracle(world, C, algo):
+    import torch.multiprocessing as tmp
+    tmp.spawn(_worker, args=(world, _free_port(), C, 12, False, algo), nprocs=world, join=True)
