@@ -17,8 +17,14 @@ Extra fields on the same JSON line:
   bfs           -- configs[2]: RMAT scale-24 BFS MTEPS (Graph500 counting), when
                    the BFS path is available.
 
-Multi-GPU (--gpus N, launched by torch.distributed.run): weak scaling, R-MAT
-scale 22 + log2(N) over the 2D partition.
+Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU):
+weak scaling, R-MAT scale 22 + log2(N) for PageRank (the headline value); the
+BFS leg stays on RMAT-24 at every N as BASELINE.json names it.  Every rank generates
+and deduplicates the same edge list, keeps its 1/N slice, and the MG graph is
+built collectively (cugraph_mg_graph_create: hash owners, degree renumbering, 2D
+R x C edge blocks); PageRank and BFS then run over RCCL communicators created
+inside libcugraph_c (pylibcugraph.comms.init_rccl).  torch.distributed (gloo)
+is only used for the RCCL unique id, the timing barrier and the max over ranks.
 """
 from __future__ import annotations
 
@@ -45,7 +51,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want_roots=0):
+def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want_roots=0, mg=None):
+    """Device R-MAT -> symmetrise + dedup (cugraph.Graph preprocessing) -> graph.
+    mg = (rank, world): every rank makes the same edge list and passes its slice to
+    the collective MGGraph build."""
     import numpy as np
     import torch
     n = 16 << scale
@@ -53,23 +62,33 @@ def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want
     w = p.generators.generate_edge_weights(h, n, seed + 1) if weighted else None
     s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
     props = p.GraphProperties(is_symmetric=True, is_multigraph=False)
-    g = p.SGGraph(h, props, s, d, w, store_transposed=transposed, renumber=True)
-    roots = None
+    roots, deg = None, None
     if want_roots:
         # Graph500 root sampling: vertices with degree > 0 (every edge source has one)
         rng = np.random.default_rng(seed)
         pick = torch.as_tensor(rng.integers(0, s.numel(), size=4 * want_roots), device=s.device)
         roots = list(dict.fromkeys(s[pick].cpu().numpy().tolist()))[:want_roots]
+    if mg is None:
+        g = p.SGGraph(h, props, s, d, w, store_transposed=transposed, renumber=True)
+    else:
+        rank, world = mg
+        E = s.numel()
+        if want_roots:
+            deg = torch.bincount(s.to(torch.int64), minlength=1 << scale)  # degree by external id
+        lo, hi = rank * E // world, (rank + 1) * E // world
+        sl = slice(lo, hi)
+        g = p.MGGraph(h, props, s[sl].contiguous(), d[sl].contiguous(), None if w is None else w[sl].contiguous(),
+                      store_transposed=transposed, num_edges=E)
     del s, d, w
     torch.cuda.synchronize()
-    return (g, roots) if want_roots else g
+    return g, roots, deg
 
 
 def pagerank_leg(p, args):
     import torch
-    h = p.ResourceHandle()
+    h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
     t0 = time.perf_counter()
-    g = build_rmat_graph(p, h, args.scale)
+    g, _, _ = build_rmat_graph(p, h, args.scale, mg=args.mg)
     build_s = time.perf_counter() - t0
     V, E = g.number_of_vertices(), g.number_of_edges()
     log(f"[bench] RMAT-{args.scale}: V={V} E={E} (build {build_s:.2f}s)")
@@ -78,6 +97,7 @@ def pagerank_leg(p, args):
     torch.cuda.synchronize()
     times, iters, kms, klaunch = [], [], 0.0, 0
     h.set_profiling(True)
+    barrier(args)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -86,11 +106,13 @@ def pagerank_leg(p, args):
         kms += h.last_hot_kernel_ms()
         klaunch += h.last_hot_kernel_launches()
     torch.cuda.synchronize()
+    barrier(args)
     t = time.perf_counter() - t0
     h.set_profiling(False)
     it_total = sum(iters)
     value = E * it_total / t
-    bytes_per_iter = 4 * E + 16 * V
+    # algorithmic bytes of one rank's share: 4E/N + 16V/N
+    bytes_per_iter = (4 * E + 16 * V) / args.world
     avg_ms = kms / max(klaunch, 1)
     achieved = bytes_per_iter / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     return dict(h=h, g=g, V=V, E=E, t=t, iters=iters, value=value, avg_ms=avg_ms, achieved=achieved,
@@ -142,40 +164,68 @@ def traffic_leg(args):
 
 
 def bfs_leg(p, args):
-    import numpy as np
     import torch
-    h = p.ResourceHandle()
-    g, roots = build_rmat_graph(p, h, args.bfs_scale, transposed=False, want_roots=args.bfs_roots)
+    h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
+    scale = args.bfs_scale
+    g, roots, deg = build_rmat_graph(p, h, scale, transposed=False, want_roots=args.bfs_roots, mg=args.mg)
     V, E = g.number_of_vertices(), g.number_of_edges()
+    if deg is None:  # SG: degrees from the CSR (internal order == result order)
+        off, _, _ = g.adjacency(h, transposed=False)
+        deg_int = (off[1:] - off[:-1]).to(torch.int64)
     rates, levels, bu, times = [], [], [], []
     for r in roots:
-        src = torch.tensor([int(r)], dtype=torch.int32, device="cuda")
-        p.bfs(h, g, src, True, 0, True, False)  # warm
+        mine = [int(r)] if args.rank == 0 else []
+        src = torch.tensor(mine, dtype=torch.int32, device="cuda")
+        p.bfs(h, g, src.clone(), True, 0, True, False)  # warm
         torch.cuda.synchronize()
+        barrier(args)
         t0 = time.perf_counter()
-        dist, pred, verts = p.bfs(h, g, src, True, 0, True, False)
+        dist, pred, verts = p.bfs(h, g, src.clone(), True, 0, True, False)
         torch.cuda.synchronize()
-        t = time.perf_counter() - t0
-        # Graph500 TEPS: undirected edges in the source's component = stored directed edges / 2
+        barrier(args)
+        t = max_over_ranks(args, time.perf_counter() - t0)
         reached = dist < 2**31 - 1
-        off, _, _ = (None, None, None)
-        e_cc = int(reached.sum().item())  # vertices reached (edges computed below)
+        # Graph500 TEPS: undirected edges of the source's component = stored directed edges / 2
+        if deg is None:
+            e_cc = int(deg_int[reached].sum().item())
+        else:
+            e_cc = int(sum_over_ranks(args, float(deg[verts[reached].to(torch.int64)].sum().item())))
         times.append(t)
         levels.append(h.last_bfs_levels())
         bu.append(h.last_bfs_bottom_up_steps())
-        rates.append((t, reached))
-    # edges in the component from the CSR degrees (internal order == verts order)
-    off, _, _ = g.adjacency(h, transposed=False)
-    deg = (off[1:] - off[:-1]).to(torch.int64)
-    mteps = []
-    for (t, reached) in rates:
-        e_cc = int(deg[reached].sum().item())
-        mteps.append((e_cc / 2) / t / 1e6)
-    hm = len(mteps) / sum(1.0 / m for m in mteps)
-    return {"scale": args.bfs_scale, "vertices": V, "edges": E, "roots": len(mteps),
-            "mteps_harmonic_mean": hm, "mteps_min": min(mteps), "mteps_max": max(mteps),
+        rates.append((e_cc / 2) / t / 1e6)
+    hm = len(rates) / sum(1.0 / m for m in rates)
+    return {"scale": scale, "vertices": V, "edges": E, "roots": len(rates),
+            "mteps_harmonic_mean": hm, "mteps_min": min(rates), "mteps_max": max(rates),
             "ms_mean": 1e3 * sum(times) / len(times), "levels": levels, "bottom_up_steps": bu,
-            "direction_optimizing": True, "teps_counting": "Graph500: undirected edges of the source component / time"}
+            "direction_optimizing": True, "n_gpus": args.world,
+            "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)"}
+
+
+def barrier(args):
+    if args.world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(args, t):
+    if args.world == 1:
+        return t
+    import torch
+    import torch.distributed as dist
+    x = torch.tensor([t], dtype=torch.float64)
+    dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    return float(x[0])
+
+
+def sum_over_ranks(args, v):
+    if args.world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    x = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(x)
+    return float(x[0])
 
 
 def main():
@@ -190,7 +240,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bfs", dest="bfs", action="store_true", default=True)
     ap.add_argument("--no-bfs", dest="bfs", action="store_false")
-    ap.add_argument("--bfs-scale", type=int, default=24)
+    ap.add_argument("--bfs-scale", type=int, default=None)
+    ap.add_argument("--row-comm-size", type=int, default=None, help="C of the R x C grid (default: R <= C)")
+    ap.add_argument("--comm", choices=["rccl", "torch"], default="rccl",
+                    help="MG collectives: RCCL inside libcugraph_c (default), or torch.distributed callbacks "
+                         "(code-path rehearsal with several ranks on one GPU; not a performance number)")
     ap.add_argument("--bfs-roots", type=int, default=8)
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
@@ -198,32 +252,40 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    grow = int(round(math.log2(max(world, 1))))
     if args.scale is None:
-        args.scale = 22 + int(round(math.log2(max(world, 1))))
+        args.scale = 22 + grow
+    if args.bfs_scale is None:
+        args.bfs_scale = 24  # BASELINE: BFS on RMAT-24 at 1/2/4/8 GPUs (fixed graph)
+    args.world, args.rank = world, rank
+    args.mg = (rank, world) if world > 1 else None
 
     import torch
     import pylibcugraph as p
 
+    args.ctx = None
     if world > 1:
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("gloo")
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group("gloo")  # bootstrap + timing only; the data path is RCCL
+        if args.comm == "rccl":
+            args.ctx = p.comms.init_rccl(args.row_comm_size)
+        else:
+            args.ctx = p.comms.init_torch(args.row_comm_size)
     torch.cuda.init()
 
     r = pagerank_leg(p, args)
     if args.traffic_child:
         return
+    r["t"] = max_over_ranks(args, r["t"])
+    r["value"] = r["E"] * sum(r["iters"]) / r["t"]
     log(f"[bench] pagerank: {r['value']:.4g} edges/s, iters {r['iters']}, kernel {r['avg_ms']:.4f} ms/iter, "
         f"{r['achieved']:.1f} GB/s algorithmic")
-
+    grid = None
     if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([r["t"]], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        r["t"] = float(tt[0])
-        # interim: independent replicas per rank (weak), until the 2D-partitioned path lands
-        r["value"] = r["E"] * sum(r["iters"]) * world / r["t"]
+        C = args.ctx.row_comm_size
+        grid = f"2D {world // C}x{C} (rows x cols), {'RCCL' if args.comm == 'rccl' else 'torch.distributed/gloo'}"
 
     out = {
         "metric": "PageRank edges/sec + BFS MTEPS on RMAT-24 at 1/2/4/8 MI355X",
@@ -247,11 +309,13 @@ def main():
             "edges": r["E"],
             "iterations_per_step": r["iters"][0] if r["iters"] else 0,
             "graph_build_s": round(r["build_s"], 3),
-            "parallelism": "sg" if world == 1 else f"replicas{world}",
+            "parallelism": "sg" if world == 1 else f"mg{world}: {grid}",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_pr_push + k_pr_apply (one PageRank iteration, HIP events around both)",
+            "kernel": ("k_pr_push + k_pr_apply (one PageRank iteration, HIP events around both)" if world == 1 else
+                       "one MG PageRank iteration per rank (row allgather + push + column reduce-scatter + apply + "
+                       "allreduce, HIP events around all); bytes = this rank's 1/N share"),
             "achieved": r["achieved"],
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -272,12 +336,12 @@ def main():
                 f"rocprofv3 --pmc passes: {detail}" if tb else f"unavailable: {detail}")
         except Exception as e:  # noqa: BLE001
             out["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline_leg(p, r, args)
         except Exception as e:  # noqa: BLE001
             out["cpu_baseline"] = {"error": repr(e)}
-    if args.bfs and world == 1:
+    if args.bfs:
         try:
             del r
             torch.cuda.empty_cache()
@@ -289,6 +353,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+        r = None
+        args.ctx.free()
         dist.destroy_process_group()
 
 

@@ -30,7 +30,7 @@ def _graph(scale, weighted, seed=5):
     return og.symmetrize_dedup(s, d, w)
 
 
-def _worker(rank, world, port, C, scale, weighted, algo):
+def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
     import sys
     sys.path.insert(0, PKG)
     sys.path.insert(0, ROOT)
@@ -49,7 +49,7 @@ def _worker(rank, world, port, C, scale, weighted, algo):
     s, d, w = _graph(scale, weighted)
     E = s.size
     lo, hi = rank * E // world, (rank + 1) * E // world
-    ctx = plc.comms.init_torch(C)
+    ctx = plc.comms.init_torch(C) if comm == "torch" else plc.comms.init_rccl(C)
     h = plc.ResourceHandle(ctx.ptr)
     assert h.get_rank() == rank
     st = torch.as_tensor(s[lo:hi].astype(np.int32), device="cuda")
@@ -114,3 +114,11 @@ def test_mg_pagerank_vs_oracle(world, C, weighted):
 def test_mg_bfs_vs_oracle(world, C, algo):
     import torch.multiprocessing as tmp
     tmp.spawn(_worker, args=(world, _free_port(), C, 12, False, algo), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("algo", ["pagerank", "bfs_do"])
+def test_mg_rccl_single_rank(algo):
+    """The RCCL communicators themselves (world / split row / split column), with the
+    one rank a single GPU allows: every collective of the MG path runs through RCCL."""
+    import torch.multiprocessing as tmp
+    tmp.spawn(_worker, args=(1, _free_port(), 1, 11, False, algo, "rccl"), nprocs=1, join=True)
