@@ -129,6 +129,14 @@ struct paths_result_t {
   std::unique_ptr<device_array_t> predecessors;
 };
 
+struct hits_result_t {
+  std::unique_ptr<device_array_t> vertices;
+  std::unique_ptr<device_array_t> hubs;
+  std::unique_ptr<device_array_t> authorities;
+  double hub_score_differences = 0;
+  size_t number_of_iterations  = 0;
+};
+
 struct clustering_result_t {
   std::unique_ptr<device_array_t> vertices;
   std::unique_ptr<device_array_t> clusters;

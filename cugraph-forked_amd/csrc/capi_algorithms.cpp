@@ -21,6 +21,11 @@ void run_sssp(handle_t& h, graph_t& g, size_t source, double cutoff, bool comput
               paths_result_t& res);
 void run_louvain(handle_t& h, graph_t& g, size_t max_level, double resolution, bool expensive,
                  clustering_result_t& res);
+void run_katz(handle_t& h, graph_t& g, array_view_t const* betas, double alpha, double beta, double eps,
+              size_t max_iter, bool expensive, centrality_result_t& res);
+void run_eigenvector(handle_t& h, graph_t& g, double eps, size_t max_iter, bool expensive, centrality_result_t& res);
+void run_hits(handle_t& h, graph_t& g, double eps, size_t max_iter, array_view_t const* guess_v,
+              array_view_t const* guess_s, bool normalize, bool expensive, hits_result_t& res);
 void mg_run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view_t const* pow_s,
                      array_view_t const* guess_v, array_view_t const* guess_s, array_view_t const* pers_v,
                      array_view_t const* pers_s, double alpha, double eps, size_t max_iter, bool expensive,
@@ -257,4 +262,110 @@ extern "C" double cugraph_heirarchical_clustering_result_get_modularity(
 extern "C" void cugraph_heirarchical_clustering_result_free(cugraph_heirarchical_clustering_result_t* result)
 {
   delete reinterpret_cast<clustering_result_t*>(result);
+}
+
+// ---------------------------------------------------------------- Katz / eigenvector / HITS
+// (reference c_api/katz.cpp, eigenvector_centrality.cpp, hits.cpp)
+extern "C" cugraph_error_code_t cugraph_katz_centrality(const cugraph_resource_handle_t* handle,
+                                                       cugraph_graph_t* graph,
+                                                       const cugraph_type_erased_device_array_view_t* betas,
+                                                       double alpha,
+                                                       double beta,
+                                                       double epsilon,
+                                                       size_t max_iterations,
+                                                       bool_t do_expensive_check,
+                                                       cugraph_centrality_result_t** result,
+                                                       cugraph_error_t** error)
+{
+  *result = nullptr;
+  *error  = nullptr;
+  return guarded(error, [&] {
+    CGX_EXPECTS(handle != nullptr, CUGRAPH_INVALID_HANDLE, "invalid resource handle");
+    CGX_INPUT(graph != nullptr, "Invalid input argument: graph is NULL");
+    auto& g = *G(graph);
+    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED, "multi-GPU Katz centrality is not implemented in this build");
+    auto res = std::make_unique<centrality_result_t>();
+    run_katz(*H(handle), g, betas ? AV(betas) : nullptr, alpha, beta, epsilon, max_iterations,
+             do_expensive_check == TRUE, *res);
+    HIP_CHECK(hipStreamSynchronize(H(handle)->stream));
+    *result = reinterpret_cast<cugraph_centrality_result_t*>(res.release());
+  });
+}
+
+extern "C" cugraph_error_code_t cugraph_eigenvector_centrality(const cugraph_resource_handle_t* handle,
+                                                              cugraph_graph_t* graph,
+                                                              double epsilon,
+                                                              size_t max_iterations,
+                                                              bool_t do_expensive_check,
+                                                              cugraph_centrality_result_t** result,
+                                                              cugraph_error_t** error)
+{
+  *result = nullptr;
+  *error  = nullptr;
+  return guarded(error, [&] {
+    CGX_EXPECTS(handle != nullptr, CUGRAPH_INVALID_HANDLE, "invalid resource handle");
+    CGX_INPUT(graph != nullptr, "Invalid input argument: graph is NULL");
+    auto& g = *G(graph);
+    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED,
+                "multi-GPU eigenvector centrality is not implemented in this build");
+    auto res = std::make_unique<centrality_result_t>();
+    run_eigenvector(*H(handle), g, epsilon, max_iterations, do_expensive_check == TRUE, *res);
+    HIP_CHECK(hipStreamSynchronize(H(handle)->stream));
+    *result = reinterpret_cast<cugraph_centrality_result_t*>(res.release());
+  });
+}
+
+extern "C" cugraph_error_code_t cugraph_hits(const cugraph_resource_handle_t* handle,
+                                            cugraph_graph_t* graph,
+                                            double epsilon,
+                                            size_t max_iterations,
+                                            const cugraph_type_erased_device_array_view_t* initial_hubs_guess_vertices,
+                                            const cugraph_type_erased_device_array_view_t* initial_hubs_guess_values,
+                                            bool_t normalize,
+                                            bool_t do_expensive_check,
+                                            cugraph_hits_result_t** result,
+                                            cugraph_error_t** error)
+{
+  *result = nullptr;
+  *error  = nullptr;
+  return guarded(error, [&] {
+    CGX_EXPECTS(handle != nullptr, CUGRAPH_INVALID_HANDLE, "invalid resource handle");
+    CGX_INPUT(graph != nullptr, "Invalid input argument: graph is NULL");
+    CGX_INPUT((initial_hubs_guess_vertices == nullptr) == (initial_hubs_guess_values == nullptr),
+              "Invalid input argument: initial hubs guess vertices and values must be given together");
+    auto& g = *G(graph);
+    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED, "multi-GPU HITS is not implemented in this build");
+    auto res = std::make_unique<hits_result_t>();
+    run_hits(*H(handle), g, epsilon, max_iterations,
+             initial_hubs_guess_vertices ? AV(initial_hubs_guess_vertices) : nullptr,
+             initial_hubs_guess_values ? AV(initial_hubs_guess_values) : nullptr, normalize == TRUE,
+             do_expensive_check == TRUE, *res);
+    HIP_CHECK(hipStreamSynchronize(H(handle)->stream));
+    *result = reinterpret_cast<cugraph_hits_result_t*>(res.release());
+  });
+}
+
+extern "C" cugraph_type_erased_device_array_view_t* cugraph_hits_result_get_vertices(cugraph_hits_result_t* result)
+{
+  return new_view(reinterpret_cast<hits_result_t*>(result)->vertices.get());
+}
+extern "C" cugraph_type_erased_device_array_view_t* cugraph_hits_result_get_hubs(cugraph_hits_result_t* result)
+{
+  return new_view(reinterpret_cast<hits_result_t*>(result)->hubs.get());
+}
+extern "C" cugraph_type_erased_device_array_view_t* cugraph_hits_result_get_authorities(cugraph_hits_result_t* result)
+{
+  return new_view(reinterpret_cast<hits_result_t*>(result)->authorities.get());
+}
+extern "C" double cugraph_hits_result_get_hub_score_differences(cugraph_hits_result_t* result)
+{
+  return reinterpret_cast<hits_result_t*>(result)->hub_score_differences;
+}
+extern "C" size_t cugraph_hits_result_get_number_of_iterations(cugraph_hits_result_t* result)
+{
+  return reinterpret_cast<hits_result_t*>(result)->number_of_iterations;
+}
+extern "C" void cugraph_hits_result_free(cugraph_hits_result_t* result)
+{
+  delete reinterpret_cast<hits_result_t*>(result);
 }

@@ -10,8 +10,10 @@ this image: edge lists are pandas DataFrames (or dicts of numpy arrays / torch
 tensors) and results come back as pandas DataFrames.
 """
 from .structure import DiGraph, Graph, from_edgelist, from_pandas_edgelist
-from .algorithms import bfs, louvain, pagerank, shortest_path, shortest_path_length, sssp
+from .algorithms import (bfs, eigenvector_centrality, hits, katz_centrality, louvain, pagerank, shortest_path,
+                         shortest_path_length, sssp)
 from . import generators
 
 __all__ = ["Graph", "DiGraph", "from_edgelist", "from_pandas_edgelist", "pagerank", "bfs", "sssp",
-           "shortest_path", "shortest_path_length", "louvain", "generators"]
+           "shortest_path", "shortest_path_length", "louvain", "katz_centrality", "eigenvector_centrality", "hits",
+           "generators"]

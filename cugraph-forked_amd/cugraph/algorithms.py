@@ -217,3 +217,83 @@ def louvain(G, max_iter=100, resolution=1.0):
     if nxv is not None:
         return dict(zip(nxv.label(df["vertex"]), df["partition"])), q
     return df, q
+
+
+def _max_degree(G):
+    import torch
+    e = G.edgelist
+    ids = torch.cat([e["src"], e["dst"]]) if G.is_directed() else e["src"]
+    return int(torch.bincount(ids.to(torch.int64)).max().item()) if ids.numel() else 0
+
+
+def katz_centrality(G, alpha=None, beta=1.0, max_iter=100, tol=1.0e-6, nstart=None, normalized=True):
+    """centrality/katz_centrality.py:24-170.  Returns DataFrame ['vertex', 'katz_centrality']
+    (dict for a NetworkX input).  As the reference, ``nstart`` is passed as the betas."""
+    import pandas as pd
+    import torch
+    nxv = None
+    if _is_nx(G):
+        nxv = _NxView(G, store_transposed=True)
+        G = nxv.G
+    if alpha is None:
+        alpha = 1.0 / _max_degree(G)
+    if alpha <= 0.0:
+        raise ValueError(f"'alpha' must be a positive float or None, got: {alpha}")
+    if not isinstance(beta, float) or beta <= 0.0:
+        raise ValueError(f"'beta' must be a positive float or None, got: {beta}")
+    if not isinstance(max_iter, int) or max_iter <= 0:
+        raise ValueError(f"'max_iter' must be a positive integer, got: {max_iter}")
+    if not isinstance(tol, float) or tol <= 0.0:
+        raise ValueError(f"'tol' must be a positive float, got: {tol}")
+    betas = None
+    if nstart is not None:
+        wt = torch.float32 if G.edgelist["weights"] is None else G.edgelist["weights"].dtype
+        betas = _cuda_like(_frame_col(nstart, "values"), wt)
+    p = _plc()
+    vertex, values = p.katz_centrality(p.ResourceHandle(), G._plc_graph, betas, alpha, beta, tol, max_iter, False)
+    df = pd.DataFrame({"vertex": vertex.cpu().numpy(), "katz_centrality": values.cpu().numpy()})
+    if nxv is not None:
+        return dict(zip(nxv.label(df["vertex"]), df["katz_centrality"]))
+    return df
+
+
+def eigenvector_centrality(G, max_iter=100, tol=1.0e-6):
+    """centrality/eigenvector_centrality.py.  Returns DataFrame ['vertex', 'eigenvector_centrality']."""
+    import pandas as pd
+    nxv = None
+    if _is_nx(G):
+        nxv = _NxView(G, store_transposed=True)
+        G = nxv.G
+    p = _plc()
+    vertex, values = p.eigenvector_centrality(p.ResourceHandle(), G._plc_graph, tol, max_iter, False)
+    df = pd.DataFrame({"vertex": vertex.cpu().numpy(), "eigenvector_centrality": values.cpu().numpy()})
+    if nxv is not None:
+        return dict(zip(nxv.label(df["vertex"]), df["eigenvector_centrality"]))
+    return df
+
+
+def hits(G, max_iter=100, tol=1.0e-5, nstart=None, normalized=True):
+    """link_analysis/hits.py:26-120.  Returns DataFrame ['vertex', 'hubs', 'authorities']
+    ((hubs dict, authorities dict) for a NetworkX input)."""
+    import pandas as pd
+    import torch
+    nxv = None
+    if _is_nx(G):
+        nxv = _NxView(G, store_transposed=True)
+        G = nxv.G
+    if G.store_transposed is False:
+        warnings.warn("HITS expects the 'store_transposed' flag to be set to 'True' for optimal performance during "
+                      "the graph creation", UserWarning)
+    gv = gx = None
+    if nstart is not None:
+        wt = torch.float32 if G.edgelist["weights"] is None else G.edgelist["weights"].dtype
+        v = (torch.as_tensor(nxv.ids(list(nstart["vertex"]))) if nxv is not None else _frame_col(nstart, "vertex"))
+        gv, gx = _cuda_like(v, _vertex_dtype(G)), _cuda_like(_frame_col(nstart, "values"), wt)
+    p = _plc()
+    vertex, hubs_, auth = p.hits(p.ResourceHandle(), G._plc_graph, tol, max_iter, gv, gx, normalized, False)
+    df = pd.DataFrame({"vertex": vertex.cpu().numpy(), "hubs": hubs_.cpu().numpy(),
+                       "authorities": auth.cpu().numpy()})
+    if nxv is not None:
+        lab = nxv.label(df["vertex"])
+        return dict(zip(lab, df["hubs"])), dict(zip(lab, df["authorities"]))
+    return df

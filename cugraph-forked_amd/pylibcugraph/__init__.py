@@ -20,7 +20,8 @@ from . import generators  # noqa: E402,F401  (MI355X build extensions)
 from . import comms  # noqa: E402,F401  (multi-GPU communicator contexts)
 
 __all__ = ["ResourceHandle", "GraphProperties", "SGGraph", "MGGraph", "pagerank",
-           "personalized_pagerank", "bfs", "sssp", "louvain", "version"]
+           "personalized_pagerank", "katz_centrality", "eigenvector_centrality", "hits", "bfs", "sssp",
+           "louvain", "version"]
 
 
 def version():
@@ -217,6 +218,40 @@ def _paths(resource_handle, res):
     finally:
         _lib.lib.cugraph_paths_result_free(res)
     return v, d, p
+
+
+def katz_centrality(resource_handle, graph, betas, alpha, beta, epsilon, max_iterations, do_expensive_check):
+    """katz_centrality.pyx:57-155.  betas (optional) indexed by external vertex id.
+    Returns (vertices, values)."""
+    b = optional_view(betas)
+    return _centrality("cugraph_katz_centrality", resource_handle, graph, vptr(b), float(alpha), float(beta),
+                       float(epsilon), int(max_iterations), int(bool(do_expensive_check)))
+
+
+def eigenvector_centrality(resource_handle, graph, epsilon, max_iterations, do_expensive_check):
+    """eigenvector_centrality.pyx:57-136.  Returns (vertices, values)."""
+    return _centrality("cugraph_eigenvector_centrality", resource_handle, graph, float(epsilon),
+                       int(max_iterations), int(bool(do_expensive_check)))
+
+
+def hits(resource_handle, graph, tol, max_iter, initial_hubs_guess_vertices, initial_hubs_guess_values,
+         normalized, do_expensive_check):
+    """hits.pyx:58-193.  Returns (vertices, hubs, authorities)."""
+    gv = optional_view(initial_hubs_guess_vertices)
+    gs = optional_view(initial_hubs_guess_values)
+    res = ctypes.c_void_p()
+    _lib.call("cugraph_hits", resource_handle.ptr, graph.c_graph_ptr, float(tol), int(max_iter), vptr(gv), vptr(gs),
+              int(bool(normalized)), int(bool(do_expensive_check)), ctypes.byref(res))
+    h = resource_handle.ptr
+    try:
+        v = copy_view_to_tensor(h, _lib.lib.cugraph_hits_result_get_vertices(res))
+        hb = copy_view_to_tensor(h, _lib.lib.cugraph_hits_result_get_hubs(res))
+        au = copy_view_to_tensor(h, _lib.lib.cugraph_hits_result_get_authorities(res))
+        resource_handle._last_hits = (_lib.lib.cugraph_hits_result_get_hub_score_differences(res),
+                                      _lib.lib.cugraph_hits_result_get_number_of_iterations(res))
+    finally:
+        _lib.lib.cugraph_hits_result_free(res)
+    return v, hb, au
 
 
 def bfs(handle, graph, sources, direction_optimizing, depth_limit, compute_predecessors,

@@ -96,6 +96,15 @@ _proto("cugraph_personalized_pagerank", c_int, P, P, P, P, P, P, P, P, c_double,
 _proto("cugraph_centrality_result_get_vertices", P, P)
 _proto("cugraph_centrality_result_get_values", P, P)
 _proto("cugraph_centrality_result_free", None, P)
+_proto("cugraph_katz_centrality", c_int, P, P, P, c_double, c_double, c_double, c_size_t, c_int, PP, PP)
+_proto("cugraph_eigenvector_centrality", c_int, P, P, c_double, c_size_t, c_int, PP, PP)
+_proto("cugraph_hits", c_int, P, P, c_double, c_size_t, P, P, c_int, c_int, PP, PP)
+_proto("cugraph_hits_result_get_vertices", P, P)
+_proto("cugraph_hits_result_get_hubs", P, P)
+_proto("cugraph_hits_result_get_authorities", P, P)
+_proto("cugraph_hits_result_get_hub_score_differences", c_double, P)
+_proto("cugraph_hits_result_get_number_of_iterations", c_size_t, P)
+_proto("cugraph_hits_result_free", None, P)
 _proto("cugraph_bfs", c_int, P, P, P, c_int, c_size_t, c_int, c_int, PP, PP)
 _proto("cugraph_sssp", c_int, P, P, c_size_t, c_double, c_int, c_int, PP, PP)
 _proto("cugraph_paths_result_get_vertices", P, P)

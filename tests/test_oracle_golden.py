@@ -183,3 +183,34 @@ def test_rmat_oracle_properties():
 def test_symmetrize_dedup_min_weight():
     s, d, w = graph.symmetrize_dedup([0, 0, 1], [1, 1, 0], [3.0, 1.0, 2.0])
     assert s.tolist() == [0, 1] and d.tolist() == [1, 0] and w.tolist() == [1.0, 1.0]
+
+
+def test_katz_c_vector(golden):
+    from oracle import centrality
+    g = golden["katz_c"]
+    w = np.asarray(g["w"], np.float32).astype(np.float64)
+    x = centrality.katz(g["num_vertices"], g["src"], g["dst"], w, g["alpha"], g["beta"], g["epsilon"],
+                        g["max_iterations"])
+    assert near(x, g["expected"], g["tol"])
+
+
+def test_eigenvector_c_vector(golden):
+    from oracle import centrality
+    g = golden["eigenvector_c"]
+    w = np.asarray(g["w"], np.float32).astype(np.float64)
+    x = centrality.eigenvector_centrality(g["num_vertices"], g["src"], g["dst"], w, g["epsilon"],
+                                          g["max_iterations"])
+    assert near(x, g["expected"], g["tol"])
+
+
+def test_hits_c_vectors(golden):
+    from oracle import centrality
+    for c in golden["hits_c"]["cases"]:
+        init = None
+        if "initial_vertices" in c:
+            init = np.zeros(c["num_vertices"])
+            init[c["initial_vertices"]] = c["initial_hubs"]
+        h, a, _, _ = centrality.hits(c["num_vertices"], c["src"], c["dst"], c["epsilon"], c["max_iterations"],
+                                     init, normalize=False)
+        assert near(h, c["hubs"], golden["hits_c"]["tol"]), c["name"]
+        assert near(a, c["authorities"], golden["hits_c"]["tol"]), c["name"]
