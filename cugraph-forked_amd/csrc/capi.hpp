@@ -129,6 +129,11 @@ struct paths_result_t {
   std::unique_ptr<device_array_t> predecessors;
 };
 
+struct extract_paths_result_t {
+  size_t max_path_length = 0;
+  std::unique_ptr<device_array_t> paths;  // [destinations x max_path_length], row major
+};
+
 struct hits_result_t {
   std::unique_ptr<device_array_t> vertices;
   std::unique_ptr<device_array_t> hubs;
@@ -187,6 +192,8 @@ adjacency_t& ensure_adjacency(handle_t& h, graph_t& g, bool transposed);  // bui
 void ensure_schedule(handle_t& h, graph_t& g, adjacency_t& adj);
 // external ids (device, graph vertex type) -> internal ids, in place; throws on unknown ids
 void renumber_ext_to_int(handle_t& h, graph_t& g, void* ids, size_t n, bool check);
+// sorted external ids + their internal ids (g.ext_sorted / g.ext_internal), renumbered graphs
+void ensure_ext_lookup(handle_t& h, graph_t& g);
 // internal ids -> external ids (values < 0 or >= V are left untouched), in place
 void unrenumber_int_to_ext(handle_t& h, graph_t& g, void* ids, size_t n);
 // copy of the number map as a result array

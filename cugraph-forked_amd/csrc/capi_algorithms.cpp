@@ -26,6 +26,8 @@ void run_katz(handle_t& h, graph_t& g, array_view_t const* betas, double alpha, 
 void run_eigenvector(handle_t& h, graph_t& g, double eps, size_t max_iter, bool expensive, centrality_result_t& res);
 void run_hits(handle_t& h, graph_t& g, double eps, size_t max_iter, array_view_t const* guess_v,
               array_view_t const* guess_s, bool normalize, bool expensive, hits_result_t& res);
+void run_extract_paths(handle_t& h, graph_t& g, paths_result_t const& pr, array_view_t const* dests,
+                       extract_paths_result_t& res);
 void mg_run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view_t const* pow_s,
                      array_view_t const* guess_v, array_view_t const* guess_s, array_view_t const* pers_v,
                      array_view_t const* pers_s, double alpha, double eps, size_t max_iter, bool expensive,
@@ -368,4 +370,44 @@ extern "C" size_t cugraph_hits_result_get_number_of_iterations(cugraph_hits_resu
 extern "C" void cugraph_hits_result_free(cugraph_hits_result_t* result)
 {
   delete reinterpret_cast<hits_result_t*>(result);
+}
+
+// ---------------------------------------------------------------- extract paths (c_api/extract_paths.cpp)
+extern "C" cugraph_error_code_t cugraph_extract_paths(const cugraph_resource_handle_t* handle,
+                                                     cugraph_graph_t* graph,
+                                                     const cugraph_type_erased_device_array_view_t* sources,
+                                                     const cugraph_paths_result_t* paths_result,
+                                                     const cugraph_type_erased_device_array_view_t* destinations,
+                                                     cugraph_extract_paths_result_t** result,
+                                                     cugraph_error_t** error)
+{
+  *result = nullptr;
+  *error  = nullptr;
+  return guarded(error, [&] {
+    CGX_EXPECTS(handle != nullptr, CUGRAPH_INVALID_HANDLE, "invalid resource handle");
+    CGX_INPUT(graph != nullptr && paths_result != nullptr && destinations != nullptr,
+              "Invalid input argument: graph, paths result and destinations must be given");
+    (void)sources;
+    auto& g = *G(graph);
+    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED, "multi-GPU extract_paths is not implemented in this build");
+    auto res = std::make_unique<extract_paths_result_t>();
+    run_extract_paths(*H(handle), g, *reinterpret_cast<paths_result_t const*>(paths_result), AV(destinations), *res);
+    *result = reinterpret_cast<cugraph_extract_paths_result_t*>(res.release());
+  });
+}
+
+extern "C" size_t cugraph_extract_paths_result_get_max_path_length(cugraph_extract_paths_result_t* result)
+{
+  return reinterpret_cast<extract_paths_result_t*>(result)->max_path_length;
+}
+
+extern "C" cugraph_type_erased_device_array_view_t* cugraph_extract_paths_result_get_paths(
+  cugraph_extract_paths_result_t* result)
+{
+  return new_view(reinterpret_cast<extract_paths_result_t*>(result)->paths.get());
+}
+
+extern "C" void cugraph_extract_paths_result_free(cugraph_extract_paths_result_t* result)
+{
+  delete reinterpret_cast<extract_paths_result_t*>(result);
 }

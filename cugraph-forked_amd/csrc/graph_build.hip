@@ -575,6 +575,13 @@ void renumber_ext_to_int(handle_t& h, graph_t& g, void* ids, size_t n, bool /*ch
   CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: vertex id not in the graph.");
 }
 
+void ensure_ext_lookup(handle_t& h, graph_t& g)
+{
+  if (!g.renumbered || g.ext_lookup_valid) return;
+  if (g.vertex_type == INT32) ext_lookup_impl<int32_t>(h, g);
+  else ext_lookup_impl<int64_t>(h, g);
+}
+
 void unrenumber_int_to_ext(handle_t& h, graph_t& g, void* ids, size_t n)
 {
   if (!n || !g.renumbered) return;

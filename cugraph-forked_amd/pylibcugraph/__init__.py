@@ -270,6 +270,32 @@ def bfs(handle, graph, sources, direction_optimizing, depth_limit, compute_prede
     return d, p, v
 
 
+def bfs_paths(resource_handle, graph, sources, destinations, depth_limit=0):
+    """BFS (predecessors on) followed by ``cugraph_extract_paths`` on its result
+    (reference traversal/extract_bfs_paths_impl.cuh; the reference declares the C
+    entry in _cugraph_c/algorithms.pxd without a Python wrapper).  Returns
+    (paths [len(destinations) x max_path_length] tensor, max_path_length)."""
+    src = DeviceView(to_device_tensor(sources).clone())
+    dst = DeviceView(to_device_tensor(destinations), src.tensor.dtype)
+    if depth_limit is None or depth_limit <= 0:
+        depth_limit = 2 ** 31 - 2
+    res = ctypes.c_void_p()
+    _lib.call("cugraph_bfs", resource_handle.ptr, graph.c_graph_ptr, src.ptr, 0, int(depth_limit), 1, 0,
+              ctypes.byref(res))
+    ep = ctypes.c_void_p()
+    try:
+        _lib.call("cugraph_extract_paths", resource_handle.ptr, graph.c_graph_ptr, src.ptr, res, dst.ptr,
+                  ctypes.byref(ep))
+    finally:
+        _lib.lib.cugraph_paths_result_free(res)
+    try:
+        L = _lib.lib.cugraph_extract_paths_result_get_max_path_length(ep)
+        paths = copy_view_to_tensor(resource_handle.ptr, _lib.lib.cugraph_extract_paths_result_get_paths(ep))
+    finally:
+        _lib.lib.cugraph_extract_paths_result_free(ep)
+    return paths.reshape(-1, L) if L else paths, L
+
+
 def sssp(resource_handle, graph, source, cutoff, compute_predecessors, do_expensive_check):
     """sssp.pyx:52-178.  Returns (vertices, distances, predecessors)."""
     res = ctypes.c_void_p()

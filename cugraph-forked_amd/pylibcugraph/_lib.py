@@ -105,6 +105,10 @@ _proto("cugraph_hits_result_get_authorities", P, P)
 _proto("cugraph_hits_result_get_hub_score_differences", c_double, P)
 _proto("cugraph_hits_result_get_number_of_iterations", c_size_t, P)
 _proto("cugraph_hits_result_free", None, P)
+_proto("cugraph_extract_paths", c_int, P, P, P, P, P, PP, PP)
+_proto("cugraph_extract_paths_result_get_max_path_length", c_size_t, P)
+_proto("cugraph_extract_paths_result_get_paths", P, P)
+_proto("cugraph_extract_paths_result_free", None, P)
 _proto("cugraph_bfs", c_int, P, P, P, c_int, c_size_t, c_int, c_int, PP, PP)
 _proto("cugraph_sssp", c_int, P, P, c_size_t, c_double, c_int, c_int, PP, PP)
 _proto("cugraph_paths_result_get_vertices", P, P)

@@ -60,6 +60,28 @@ cugraph_error_code_t cugraph_sssp(const cugraph_resource_handle_t* handle,
                                   cugraph_paths_result_t** result,
                                   cugraph_error_t** error);
 
+/* extract_paths result, reference traversal_algorithms.h:147-204 */
+typedef struct {
+  int32_t align_;
+} cugraph_extract_paths_result_t;
+
+/*
+ * Paths from a BFS/SSSP result back to the source (reference traversal_algorithms.h:173-180,
+ * traversal/extract_bfs_paths_impl.cuh): row-major [destinations x max_path_length]
+ * matrix of external vertex ids, -1 padded.
+ */
+cugraph_error_code_t cugraph_extract_paths(const cugraph_resource_handle_t* handle,
+                                           cugraph_graph_t* graph,
+                                           const cugraph_type_erased_device_array_view_t* sources,
+                                           const cugraph_paths_result_t* paths_result,
+                                           const cugraph_type_erased_device_array_view_t* destinations,
+                                           cugraph_extract_paths_result_t** result,
+                                           cugraph_error_t** error);
+size_t cugraph_extract_paths_result_get_max_path_length(cugraph_extract_paths_result_t* result);
+cugraph_type_erased_device_array_view_t* cugraph_extract_paths_result_get_paths(
+  cugraph_extract_paths_result_t* result);
+void cugraph_extract_paths_result_free(cugraph_extract_paths_result_t* result);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,3 +112,36 @@ def test_isolated_source_and_unrenumbered_gaps():
     h, G = make_graph([0, 1, 2, 6], [1, 2, 3, 7], None, renumber=False, symmetric=False)
     v, dist, pred = run(h, G, [5], False)
     assert dist[v == 5][0] == 0 and np.all(dist[v != 5] == INT32_MAX)
+
+
+@pytest.mark.parametrize("transposed", [False, True])
+def test_extract_paths_c_golden(golden, transposed):
+    g = golden["extract_paths_c"]
+    h, G = make_graph(g["src"], g["dst"], g["w"], transposed=transposed, renumber=False)
+    paths, L = plc().bfs_paths(h, G, np.asarray(g["sources"], np.int32), np.asarray(g["destinations"], np.int32),
+                               g["depth_limit"])
+    assert L == g["expected_max_path_length"]
+    assert host(paths).ravel().tolist() == g["expected_paths"]
+
+
+def test_extract_paths_rmat_renumbered():
+    """Every extracted path starts at the source, follows edges, ends at its destination
+    and has distance + 1 vertices; unreachable destinations give an all -1 row."""
+    s, d = rmat.rmat(10, 16 << 10, seed=3)
+    s, d, _ = og.symmetrize_dedup(s, d)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    root = int(s[0])
+    dests = np.unique(np.concatenate([s[:50], d[:50]])).astype(np.int32)
+    paths, L = plc().bfs_paths(h, G, np.asarray([root], np.int32), dests)
+    dist, _, verts = plc().bfs(h, G, np.asarray([root], np.int32), False, 0, True, False)
+    dmap = dict(zip(host(verts).tolist(), host(dist).tolist()))
+    P = host(paths)
+    edges = set(zip(s.tolist(), d.tolist()))
+    assert L == 1 + max(dmap[int(x)] for x in dests if dmap[int(x)] < 2**31 - 1)
+    for row, dv in zip(P, dests):
+        seq = [int(x) for x in row if x != -1]
+        if dmap[int(dv)] == 2**31 - 1:
+            assert seq == []
+            continue
+        assert seq[0] == root and seq[-1] == dv and len(seq) == dmap[int(dv)] + 1
+        assert all((a, b) in edges for a, b in zip(seq, seq[1:]))
