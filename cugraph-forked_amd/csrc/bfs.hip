@@ -23,6 +23,9 @@
 #include "prims.hpp"
 #include "schedule.hpp"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 
 namespace cgx {
@@ -30,7 +33,8 @@ namespace cgx {
 namespace {
 
 constexpr int kSmallDeg = 16;    // 4-lane groups
-constexpr int kMidDeg   = 1024;  // one wave; above: one block
+constexpr int kMidDeg   = 1024;  // one wave; above: edge chunks over blocks
+constexpr int kChunk    = 2048;  // edges per large-class chunk
 
 struct bfs_ctr {
   unsigned long long qlen[3];  // next queues: small / mid / large
@@ -92,25 +96,69 @@ struct bfs_args {
   long long blk_mid_start, blk_small_start;  // top-down grid segmentation
 };
 
+// Next-queue appends are staged per wave in LDS (kStage entries per class) and
+// written out in bulk: one global atomic per ~450 discovered vertices instead of one
+// per wave and class per 64-edge batch -- at a hub level (hundreds of frontier hubs,
+// ~1M discoveries) the per-batch atomics serialised on the three queue tails.
+constexpr int kStage = 512;
+
+template <typename V>
+struct wave_stage {
+  V* buf;     // this wave's 3 * kStage LDS entries
+  int n[3];   // wave-uniform fill counts
+};
+
 template <typename V, typename E>
-__device__ __forceinline__ void push_next(bfs_args<V, E> const& a, V v, bool take, unsigned long long& my_m)
+__device__ __forceinline__ void stage_flush(bfs_args<V, E> const& a, wave_stage<V>& st, int c)
+{
+  int const cnt = st.n[c];
+  if (cnt == 0) return;
+  // DS operations of one wave complete in order; the barrier only pins the compiler
+  __builtin_amdgcn_wave_barrier();
+  int const lane          = threadIdx.x & 63;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(&a.ctr->qlen[c], (unsigned long long)cnt);
+  base = __shfl(base, 0, 64);
+  for (int j = lane; j < cnt; j += 64) a.qnext[c][base + j] = st.buf[c * kStage + j];
+  __builtin_amdgcn_wave_barrier();
+  st.n[c] = 0;
+}
+
+template <typename V, typename E>
+__device__ __forceinline__ void push_next(bfs_args<V, E> const& a, wave_stage<V>& st, V v, bool take,
+                                          unsigned long long& my_m)
 {
   int cls = 0;
-  E deg   = 0;
   if (take) {
-    deg = a.off[v + 1] - a.off[v];
-    cls = deg <= kSmallDeg ? 0 : (deg <= kMidDeg ? 1 : 2);
+    E deg = a.off[v + 1] - a.off[v];
+    cls   = deg <= kSmallDeg ? 0 : (deg <= kMidDeg ? 1 : 2);
     my_m += (unsigned long long)deg;
   }
+  int const lane = threadIdx.x & 63;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    long long slot = wave_append(&a.ctr->qlen[c], take && cls == c);
-    if (slot >= 0) a.qnext[c][slot] = v;
+    bool const mine          = take && cls == c;
+    unsigned long long const mask = __ballot(mine);
+    if (mask == 0) continue;
+    if (mine) st.buf[c * kStage + st.n[c] + __popcll(mask & ((1ull << lane) - 1ull))] = v;
+    st.n[c] += __popcll(mask);
+    if (st.n[c] > kStage - 64) stage_flush<V, E>(a, st, c);
   }
 }
 
 template <typename V, typename E>
-__device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, V u, V v, bool active, unsigned long long& my_m)
+__device__ __forceinline__ void stage_flush_all(bfs_args<V, E> const& a, wave_stage<V>& st)
+{
+  for (int c = 0; c < 3; ++c) stage_flush<V, E>(a, st, c);
+}
+
+#define CGX_WAVE_STAGE(V, st)                                   \
+  __shared__ V s_stage_[4][3 * kStage];                         \
+  wave_stage<V> st{s_stage_[threadIdx.x >> 6], {0, 0, 0}}
+
+template <typename V, typename E>
+__device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, wave_stage<V>& st, V u, V v, bool active,
+                                           unsigned long long& my_m)
 {
   bool take = false;
   if (active) {
@@ -120,7 +168,7 @@ __device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, V u, V v, bo
       take = cas_claim<V>(a.dist, v, (V)(a.depth + 1));
     }
   }
-  push_next<V, E>(a, v, take, my_m);
+  push_next<V, E>(a, st, v, take, my_m);
 }
 
 __device__ __forceinline__ void flush_counts(bfs_ctr* ctr, unsigned long long n, unsigned long long m)
@@ -154,20 +202,36 @@ __device__ __forceinline__ void flush_counts(bfs_ctr* ctr, unsigned long long n,
 template <typename V, typename E>
 __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
 {
+  CGX_WAVE_STAGE(V, st);
   unsigned long long my_m = 0, my_n = 0;
   long long b = blockIdx.x;
   int tid     = threadIdx.x;
   if (b < a.blk_mid_start) {
-    for (long long i = b; i < (long long)a.ncur[2]; i += a.blk_mid_start) {
-      V u    = a.qcur[2][i];
-      E beg  = a.off[u], end = a.off[u + 1];
-      for (E base = beg; base < end; base += 256) {
-        E e = base + tid;
-        bool act = e < end;
+    // large class, edge-parallel: every vertex's row is cut into kChunk-edge chunks
+    // and the blocks stride over the global chunk index (a root of degree 4e5 would
+    // otherwise serialise on one block)
+    long long const nb = a.blk_mid_start;
+    long long i = 0, chunk_base = 0;
+    for (long long c = b;; c += nb) {
+      V u = 0;
+      E beg = 0, end = 0;
+      while (i < (long long)a.ncur[2]) {
+        u   = a.qcur[2][i];
+        beg = a.off[u];
+        end = a.off[u + 1];
+        long long nch = ((long long)(end - beg) + kChunk - 1) / kChunk;
+        if (c < chunk_base + nch) break;
+        chunk_base += nch;
+        ++i;
+      }
+      if (i >= (long long)a.ncur[2]) break;
+      E cb = beg + (E)((c - chunk_base) * kChunk);
+      E ce = cb + (E)kChunk < end ? cb + (E)kChunk : end;
+      for (E base = cb; base < ce; base += 256) {
+        E e      = base + tid;
+        bool act = e < ce;
         V v      = act ? a.idx[e] : V(0);
-        unsigned long long m0 = my_m;
-        visit_edge<V, E>(a, u, v, act, my_m);
-        (void)m0;
+        visit_edge<V, E>(a, st, u, v, act, my_m);
       }
     }
   } else if (b < a.blk_small_start) {
@@ -181,7 +245,7 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
         E e      = base + lane;
         bool act = e < end;
         V v      = act ? a.idx[e] : V(0);
-        visit_edge<V, E>(a, u, v, act, my_m);
+        visit_edge<V, E>(a, st, u, v, act, my_m);
       }
     }
   } else {
@@ -198,12 +262,13 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
         E e      = beg + r * 4 + lane;
         bool act = e < end;
         V v      = act ? a.idx[e] : V(0);
-        visit_edge<V, E>(a, u, v, act, my_m);
+        visit_edge<V, E>(a, st, u, v, act, my_m);
       }
     }
     (void)g;
   }
   (void)my_n;
+  stage_flush_all<V, E>(a, st);
   flush_counts(a.ctr, 0, my_m);
 }
 
@@ -226,6 +291,7 @@ __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, u
 template <typename V, typename E>
 __global__ __launch_bounds__(256) void k_bitmap_to_queues(bfs_args<V, E> a, uint32_t const* bm, int64_t nwords)
 {
+  CGX_WAVE_STAGE(V, st);
   unsigned long long my_m = 0;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += (int64_t)gridDim.x * blockDim.x) {
     int64_t w     = base + threadIdx.x;
@@ -240,9 +306,10 @@ __global__ __launch_bounds__(256) void k_bitmap_to_queues(bfs_args<V, E> a, uint
         v = (V)(w * 32 + bit);
       }
       if (!__any(take)) break;
-      push_next<V, E>(a, v, take, my_m);
+      push_next<V, E>(a, st, v, take, my_m);
     }
   }
+  stage_flush_all<V, E>(a, st);
   flush_counts(a.ctr, 0, my_m);
 }
 
@@ -293,7 +360,16 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
     int const gbase  = (tid & 63) & ~(w - 1);  // first lane of my group within the wave
     int const groups = 256 / w;
     unsigned long long const gmask = (w == 64) ? ~0ull : ((1ull << w) - 1ull);
+    // identity order (degree-sorted renumbering): a block step covers <= 256
+    // consecutive vertices, so the next/visited bits are gathered in LDS and
+    // published with one global atomicOr per 32-vertex word instead of per vertex
+    __shared__ uint32_t s_bits[kBlock / 32 + 2];
+    bool const agg = a.order == nullptr;
     for (int64_t p0 = it.begin; p0 < it.end; p0 += groups) {
+      if (agg) {
+        if (tid < kBlock / 32 + 2) s_bits[tid] = 0;
+        __syncthreads();
+      }
       int64_t p  = p0 + tid / w;
       bool valid = p < it.end;
       V v        = valid ? (a.order ? a.order[p] : (V)p) : V(0);
@@ -315,12 +391,27 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
           if (lane == first) {
             a.dist[v] = nd;
             if (a.pred) a.pred[v] = u;
-            atomicOr(a.nxt + (v >> 5), bit);
-            atomicOr(a.vis + (v >> 5), bit);
+            if (agg) {
+              atomicOr(&s_bits[(int64_t(v) >> 5) - (p0 >> 5)], bit);
+            } else {
+              atomicOr(a.nxt + (v >> 5), bit);
+              atomicOr(a.vis + (v >> 5), bit);
+            }
             my_n += 1;
             my_m += (unsigned long long)(end - beg);
           }
           break;
+        }
+      }
+      if (agg) {
+        __syncthreads();
+        if (tid < kBlock / 32 + 2) {
+          uint32_t const b = s_bits[tid];
+          if (b) {
+            int64_t const wd = (p0 >> 5) + tid;
+            atomicOr(a.nxt + wd, b);
+            atomicOr(a.vis + wd, b);
+          }
         }
       }
     }
@@ -445,7 +536,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     V limit = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
                                               (unsigned long long)std::numeric_limits<V>::max());
     size_t levels = 0, bu_steps = 0;
+    bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
     while (n_f > 0 && depth < limit) {
+      auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
         if (!bottom_up && (double)m_f > (double)m_u / 14.0) bottom_up = true;
         else if (bottom_up && (double)n_f < (double)nv / 24.0) bottom_up = false;
@@ -486,7 +579,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           a.ncur[c]  = ncur[c];
           a.qnext[c] = qb[c].data();
         }
-        long long nb_large = (long long)std::min<unsigned long long>(ncur[2], 1024);
+        long long nb_large = ncur[2] ? (long long)std::min<unsigned long long>(std::max<unsigned long long>(ncur[2] * 8, 256), 4096) : 0;
         long long nb_mid   = (long long)std::min<unsigned long long>((ncur[1] + 3) / 4, 4096);
         long long nb_small = (long long)std::min<unsigned long long>((ncur[0] + 63) / 64, 8192);
         a.blk_mid_start    = nb_large;
@@ -508,6 +601,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         for (int c = 0; c < 3; ++c) std::swap(qa[c], qb[c]);
         have_bitmap = false;
       }
+      if (dbg)
+        std::fprintf(stderr, "[bfs] level %d %s n_f=%llu m_f=%llu m_u=%llu %.1f us\n", (int)depth,
+                     bottom_up ? "bottom-up" : "top-down", n_f, m_f, m_u,
+                     1e6 * std::chrono::duration<double>(std::chrono::steady_clock::now() - tl).count());
       m_u = m_u > m_f ? m_u - m_f : 0;
       ++depth;
       ++levels;

@@ -74,6 +74,7 @@ struct pr_push_t {
   buffer ew;           // weight_t[E] for weighted graphs
   buffer units;        // push_unit[nunits]
   int64_t nunits = 0;
+  std::vector<int64_t> seg_start;  // first unit of every source segment (+ end)
   buffer acc;          // u64[nacc] fixed-point sums, zero between iterations
   int64_t nacc = 0;
 };

@@ -295,15 +295,20 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 constexpr int kWinBits     = 13;
 constexpr int kWin         = 1 << kWinBits;
 constexpr int kSrcBits     = 32 - kWinBits;  // 19
+constexpr int kXcds        = 8;   // MI355X XCDs (workgroups are dealt to them round-robin)
+constexpr int kXcdSegs     = 1;   // source segments of equal entry counts per XCD (8 measured 60% slower: all
+                                  // XCDs then flush the same windows at once; 1 = no split)
 constexpr int kPushThreads = 1024;
-constexpr int kPushUnit    = 8 * kPushThreads;
+constexpr int kPerThread   = 8;  // entries per thread per unit
+constexpr int kPushUnit    = kPerThread * kPushThreads;
 constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
 constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 
 struct push_unit {
   int64_t k0, k1;  // entries [k0, k1)
   int64_t base;    // source id of offset 0
-  int64_t win;     // destination window
+  int32_t win;     // destination window
+  int32_t seg;     // source segment (XCD) of the unit
 };
 
 template <typename V, typename E, typename R>
@@ -313,6 +318,7 @@ struct push_args {
   R const* ew;  // entry weights (weighted graphs)
   push_unit const* units;
   int64_t nunits;
+  int64_t seg_start[kXcdSegs + 1];  // first unit of every source segment
   unsigned long long* acc;  // [nwin * kWin] fixed-point sums, zero between iterations
   int ablate;  // measurement only (CGX_PR_ABLATE): 1 no gathers, 2 no LDS atomics, 4 no push
 };
@@ -353,17 +359,28 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
   // contiguous runs of units (window-major order; measured faster than an
   // XCD-blocked or segment-major schedule, which multiply the window flushes)
-  int64_t const u0 = blockIdx.x * sa.nunits / gridDim.x;
-  int64_t const u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
+  // XCD-aware: workgroup b runs on XCD b % 8, and the XCD's workgroups share the
+  // units of one source segment -- whose x~ slice then stays in that XCD's L2
+  int64_t u0, u1;
+  if (kXcdSegs == kXcds && gridDim.x % kXcds == 0) {
+    int const seg    = blockIdx.x % kXcds;
+    int64_t const lb = blockIdx.x / kXcds, nbx = gridDim.x / kXcds;
+    int64_t const a0 = sa.seg_start[seg], cnt = sa.seg_start[seg + 1] - a0;
+    u0 = a0 + lb * cnt / nbx;
+    u1 = a0 + (lb + 1) * cnt / nbx;
+  } else {
+    u0 = blockIdx.x * sa.nunits / gridDim.x;
+    u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
+  }
   int64_t cur      = u0 < u1 ? sa.units[u0].win : -1;
   __syncthreads();
-  uint32_t ent[8];
-  R w[8];
+  uint32_t ent[kPerThread];
+  R w[kPerThread];
   push_unit pu{};
   auto load_unit = [&](int64_t un, push_unit& p, uint32_t* e, R* ww) {
     p = sa.units[un];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kPerThread; ++j) {
       int64_t k = p.k0 + j * kPushThreads + tid;
       e[j]      = k < p.k1 ? nt_load(sa.ent + k) : 0u;
       if constexpr (WEIGHTED) ww[j] = k < p.k1 ? nt_load(sa.ew + k) : R(0);
@@ -371,23 +388,23 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
   };
   if (u0 < u1) load_unit(u0, pu, ent, w);
   for (int64_t un = u0; un < u1; ++un) {
-    uint32_t ent_n[8];
-    R w_n[8];
+    uint32_t ent_n[kPerThread];
+    R w_n[kPerThread];
     push_unit pu_n{};
     if (un + 1 < u1) load_unit(un + 1, pu_n, ent_n, w_n);
     if (pu.win != cur) {
       flush_window<V, E, R>(sa, acc, cur);
       cur = pu.win;
     }
-    R x[8];
+    R x[kPerThread];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kPerThread; ++j) {
       bool const ok = pu.k0 + j * kPushThreads + tid < pu.k1;
       if (sa.ablate & 1) x[j] = ok ? R(1e-9) : R(0);
       else x[j] = ok ? a.x_in[pu.base + (int64_t)(ent[j] >> kWinBits)] : R(0);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kPerThread; ++j) {
       if (x[j] != R(0) && !(sa.ablate & 2)) {
         double v = (double)x[j];
         if constexpr (WEIGHTED) v *= (double)w[j];
@@ -396,7 +413,7 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
     }
     pu = pu_n;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kPerThread; ++j) {
       ent[j] = ent_n[j];
       if constexpr (WEIGHTED) w[j] = w_n[j];
     }
@@ -435,17 +452,65 @@ __global__ void k_edge_rows(E const* off, int64_t nv, int64_t ne, uint32_t* rows
   }
 }
 
+struct seg_bounds {
+  int64_t lo[kXcdSegs + 1];  // source segment s = [lo[s], lo[s + 1])
+};
+
 template <typename V>
-__global__ void k_push_keys(V const* idx, uint32_t const* rows, int64_t ne, uint64_t* keys, uint32_t* vals)
+__global__ void k_push_keys(V const* idx, uint32_t const* rows, int64_t ne, seg_bounds sb, uint64_t* keys,
+                            uint32_t* vals)
 {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-    keys[e] = ((uint64_t)(rows[e] >> kWinBits) << 32) | (uint64_t)(uint32_t)idx[e];
+    uint64_t src = (uint32_t)idx[e];
+    uint64_t seg = 0;
+    while (seg + 1 < kXcdSegs && (int64_t)src >= sb.lo[seg + 1]) ++seg;
+    keys[e] = (seg << 51) | ((uint64_t)(rows[e] >> kWinBits) << 32) | src;
     vals[e] = (uint32_t)e;
   }
 }
 
-// key = (window, source); unit starts: a new segment (window, 2^kSrcBits source
-// block) or every kPushUnit-th entry
+// per-source entry counts (for segments of equal work)
+template <typename C>
+__global__ void k_src_counts(C const* cols, int64_t ne, unsigned long long* cnt)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(cnt + (uint32_t)cols[e], 1ull);
+}
+
+// lo[s] = first source whose entry prefix reaches s * ne / kXcdSegs
+__global__ void k_seg_bounds(unsigned long long const* pre, int64_t n_cols, int64_t ne, int64_t* lo)
+{
+  int sg = threadIdx.x;
+  if (sg > kXcdSegs) return;
+  if (sg == kXcdSegs) {
+    lo[sg] = n_cols;
+    return;
+  }
+  unsigned long long target = (unsigned long long)(sg * ne / kXcdSegs);
+  int64_t a = 0, b = n_cols;  // first source with pre >= target
+  while (a < b) {
+    int64_t mid = (a + b) >> 1;
+    if (pre[mid] < target) a = mid + 1;
+    else b = mid;
+  }
+  lo[sg] = sg == 0 ? 0 : a;
+}
+
+__global__ void k_seg_unit_start(push_unit const* units, int64_t nunits, int64_t* start)
+{
+  int sg = threadIdx.x;
+  if (sg > kXcdSegs) return;
+  int64_t a = 0, b = nunits;  // first unit with seg >= sg
+  while (a < b) {
+    int64_t mid = (a + b) >> 1;
+    if (units[mid].seg < sg) a = mid + 1;
+    else b = mid;
+  }
+  start[sg] = a;
+}
+
+// key = (source segment, window, source); unit starts: a new (segment, window,
+// 2^kSrcBits source block) or every kPushUnit-th entry
 __global__ void k_unit_flags(uint64_t const* keys, int64_t ne, uint32_t* flag)
 {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
@@ -465,7 +530,9 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
     uint32_t src = (uint32_t)key;
     ent[k]       = ((src & ((1u << kSrcBits) - 1)) << kWinBits) | (rows[e] & (kWin - 1));
     if (w) ew[k] = w[e];
-    if (flag[k]) units[uid[k]] = push_unit{k, 0, (int64_t)(src >> kSrcBits) << kSrcBits, (int64_t)(key >> 32)};
+    if (flag[k])
+      units[uid[k]] = push_unit{k, 0, (int64_t)(src >> kSrcBits) << kSrcBits, (int32_t)((key >> 32) & ((1u << 19) - 1)),
+                                (int32_t)(key >> 51)};
   }
 }
 
@@ -494,14 +561,27 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   if (ne == 0) return;
   dbuf<uint64_t> keys_out(ne, s);
   dbuf<uint32_t> vals_out(ne, s);
+  seg_bounds sb{};
+  {  // source segments of equal entry counts (one per XCD)
+    dbuf<unsigned long long> cnt(n_cols + 1, s), pre(n_cols + 1, s);
+    fill<unsigned long long>(cnt.data(), n_cols + 1, 0ull, s);
+    hipLaunchKernelGGL(k_src_counts<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, ne, cnt.data());
+    CGX_LAUNCH_CHECK();
+    exclusive_scan<unsigned long long, unsigned long long>(cnt.data(), pre.data(), n_cols + 1, s);
+    dbuf<int64_t> lo(kXcdSegs + 1, s);
+    hipLaunchKernelGGL(k_seg_bounds, dim3(1), dim3(64), 0, s, pre.data(), n_cols, ne, lo.data());
+    CGX_LAUNCH_CHECK();
+    auto hl = to_host(lo.data(), kXcdSegs + 1, s);
+    for (int i = 0; i <= kXcdSegs; ++i) sb.lo[i] = hl[i];
+  }
   {
     dbuf<uint64_t> keys(ne, s);
     dbuf<uint32_t> vals(ne, s);
-    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne,
+    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, sb,
                        keys.data(), vals.data());
     CGX_LAUNCH_CHECK();
     radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
-                                         32 + bits_for((unsigned long long)(nwin - 1)), s);
+                                         51 + bits_for(kXcdSegs - 1), s);
   }
   dbuf<uint32_t> flag(ne + 1, s), uid(ne + 1, s);
   hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
@@ -525,6 +605,12 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      pp.units.data<push_unit>(), nunits, ne);
   CGX_LAUNCH_CHECK();
   pp.nunits = nunits;
+  {
+    dbuf<int64_t> st(kXcdSegs + 1, s);
+    hipLaunchKernelGGL(k_seg_unit_start, dim3(1), dim3(64), 0, s, pp.units.data<push_unit>(), nunits, st.data());
+    CGX_LAUNCH_CHECK();
+    pp.seg_start = to_host(st.data(), kXcdSegs + 1, s);
+  }
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -712,6 +798,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.ew     = g.weighted ? adj.pr.ew.data<R>() : nullptr;
     sa.units  = adj.pr.units.data<push_unit>();
     sa.nunits = adj.pr.nunits;
+    for (int i = 0; i <= kXcdSegs; ++i) sa.seg_start[i] = i < (int)adj.pr.seg_start.size() ? adj.pr.seg_start[i] : 0;
     sa.acc    = adj.pr.acc.data<unsigned long long>();
     if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
     nblk_push  = (int)std::min<int64_t>(sa.nunits, 256 * 2);  // 64 KB LDS: two blocks per CU
@@ -948,6 +1035,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t 
   sp.ew     = g.weighted ? blk.pp.ew.data<R>() : nullptr;
   sp.units  = blk.pp.units.data<push_unit>();
   sp.nunits = blk.pp.nunits;
+  for (int i = 0; i <= kXcdSegs; ++i) sp.seg_start[i] = i < (int)blk.pp.seg_start.size() ? blk.pp.seg_start[i] : 0;
   sp.acc    = blk.pp.acc.data<unsigned long long>();
   sap       = sp;
   sap.acc   = acc_own.data();
