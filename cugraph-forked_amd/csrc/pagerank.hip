@@ -320,7 +320,7 @@ struct push_args {
   int64_t nunits;
   int64_t seg_start[kXcdSegs + 1];  // first unit of every source segment
   unsigned long long* acc;  // [nwin * kWin] fixed-point sums, zero between iterations
-  int ablate;  // measurement only (CGX_PR_ABLATE): 1 no gathers, 2 no LDS atomics, 4 no push
+  int ablate;  // measurement only (CGX_PR_ABLATE): 1 no gathers, 2 no LDS atomics, 4 no push, 8 no flush
 };
 
 template <typename T>
@@ -341,7 +341,7 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
   unsigned long long* g = sa.acc + win * kWin;
   for (int i = threadIdx.x; i < kWin; i += kPushThreads) {
     unsigned long long v = acc[i];
-    if (v) {
+    if (v && !(sa.ablate & 8)) {
       atomicAdd(g + i, v);
       acc[i] = 0ull;
     }
