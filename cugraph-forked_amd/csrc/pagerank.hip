@@ -213,7 +213,11 @@ __device__ __forceinline__ double row_partial_block(pr_args<V, E, R> const& a, E
   return (s0 + s1) + (s2 + s3);
 }
 
-template <typename V, typename E, typename R>
+__device__ __forceinline__ uint32_t encode_fixed(float x);
+
+// ENC: x~' is stored as its fixed-point word (encode_fixed) instead of the fp32
+// value -- the form the unweighted push kernel gathers
+template <typename V, typename E, typename R, bool ENC = false>
 __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, double s, double base, double pf,
                                               double& my_diff, double& my_dang)
 {
@@ -224,12 +228,11 @@ __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, do
   a.pr[v]  = nr;
   my_diff += fabs((double)nr - (double)old);
   R ow = a.outw[v];
-  if (ow == R(0)) {
-    my_dang += (double)nr;
-    a.x_out[v] = R(0);
-  } else {
-    a.x_out[v] = (R)((double)nr / (double)ow);
-  }
+  R xv = R(0);
+  if (ow == R(0)) my_dang += (double)nr;
+  else xv = (R)((double)nr / (double)ow);
+  if constexpr (ENC) reinterpret_cast<uint32_t*>(a.x_out)[v] = encode_fixed(xv);
+  else a.x_out[v] = xv;
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -334,6 +337,33 @@ __device__ __forceinline__ unsigned long long to_fixed(double v)
   return (unsigned long long)__double2ll_rn(v * kFixScale);
 }
 
+// Encoded x~ for unweighted fp32 graphs: a 32-bit word {shift:8, mantissa:24}
+// with to_fixed((double)x) == mantissa << shift exactly.  For x >= 2^-39 the
+// fixed-point value is the fp32 mantissa shifted left by e - 88 (e = biased
+// exponent); below that it is < 2^24 and is stored with shift 0.  The push kernel
+// then turns a gathered word into its 64-bit contribution with three integer
+// instructions (and, shift, 64-bit shift) instead of the fp64 conversion chain,
+// and the sums are the same bits as the fp64 form.  Requires 0 <= x < 2 (x~ <= 1).
+__device__ __forceinline__ uint32_t encode_fixed(float x)
+{
+  unsigned long long const f = to_fixed((double)x);
+  if (f < (1ull << 24)) return (uint32_t)f;
+  int const sh = 40 - __clzll((long long)f);  // top bit p = 63 - clz; shift = p - 23
+  return (uint32_t)(f >> sh) | ((uint32_t)sh << 24);
+}
+
+__device__ __forceinline__ unsigned long long decode_fixed(uint32_t w)
+{
+  return (unsigned long long)(w & 0xffffffu) << (w >> 24);
+}
+
+template <typename R>
+__global__ void k_encode_x(R* x, int64_t n)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint32_t*>(x)[v] = encode_fixed((float)x[v]);
+}
+
 template <typename V, typename E, typename R>
 __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win)
 {
@@ -421,7 +451,73 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
   if (cur >= 0) flush_window<V, E, R>(sa, acc, cur);
 }
 
+// Unweighted fp32 push over encoded x~ (the benchmark path).  Same schedule and
+// sums as k_pr_push, leaner inner loop (~8 VALU per edge instead of ~25, from the
+// SQ_INSTS_VALU counter): unit descriptors come through scalar loads, entry and
+// x~ addresses are 32-bit offsets from scalar bases, the contribution is
+// decode_fixed of the gathered word, and only partial units pay for lane masks.
+// The x~ gathers of a unit are issued before the next unit's entry loads, so the
+// wait for the gathers does not include the HBM latency of the prefetch.
 template <typename V, typename E, typename R>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push_enc(push_args<V, E, R> sa)
+{
+  __shared__ unsigned long long acc[kWin];
+  if (sa.a.st->done) return;
+  int const tid = threadIdx.x;
+  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
+  int64_t const u0 = blockIdx.x * sa.nunits / gridDim.x;
+  int64_t const u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
+  if (u0 >= u1) return;  // uniform
+  using cunit_t            = __attribute__((address_space(4))) push_unit const;
+  cunit_t* const units     = (cunit_t*)sa.units;  // read-only here: scalar loads
+  uint32_t const* const xe = reinterpret_cast<uint32_t const*>(sa.a.x_in);
+  int64_t cur              = units[u0].win;
+  __syncthreads();
+  uint32_t ent[kPerThread];
+  int64_t k0   = units[u0].k0;
+  int n        = (int)(units[u0].k1 - k0);
+  int64_t base = units[u0].base;
+  int win      = units[u0].win;
+#pragma unroll
+  for (int j = 0; j < kPerThread; ++j) ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent is padded
+  for (int64_t un = u0; un < u1; ++un) {
+    if (win != cur) {
+      flush_window<V, E, R>(sa, acc, cur);
+      cur = win;
+    }
+    uint32_t const* xb = xe + base;
+    uint32_t xw[kPerThread];
+    if (n == kPushUnit) {
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) xw[j] = xb[ent[j] >> kWinBits];
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) xw[j] = j * kPushThreads + tid < n ? xb[ent[j] >> kWinBits] : 0u;
+    }
+    uint32_t ent_n[kPerThread];
+    int64_t k0n = 0, basen = 0;
+    int nn = 0, winn = 0;
+    if (un + 1 < u1) {
+      k0n   = units[un + 1].k0;
+      nn    = (int)(units[un + 1].k1 - k0n);
+      basen = units[un + 1].base;
+      winn  = units[un + 1].win;
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
+    }
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) atomicAdd(&acc[ent[j] & (kWin - 1)], decode_fixed(xw[j]));
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) ent[j] = ent_n[j];
+    k0   = k0n;
+    n    = nn;
+    base = basen;
+    win  = winn;
+  }
+  flush_window<V, E, R>(sa, acc, cur);
+}
+
+template <typename V, typename E, typename R, bool ENC = false>
 __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 {
   auto const& a = sa.a;
@@ -432,7 +528,7 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < a.nv; v += (int64_t)gridDim.x * blockDim.x) {
     unsigned long long f = sa.acc[v];
     if (f) sa.acc[v] = 0ull;
-    vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
+    vertex_update<V, E, R, ENC>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
 }
@@ -591,7 +687,8 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
   int64_t nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
   pp.ent.set_stream(s);
-  pp.ent.resize(ne * sizeof(uint32_t));
+  pp.ent.resize((ne + kPushUnit) * sizeof(uint32_t));  // padded: k_pr_push_enc loads whole units
+  HIP_CHECK(hipMemsetAsync(pp.ent.data<uint32_t>() + ne, 0, kPushUnit * sizeof(uint32_t), s));
   pp.ew.set_stream(s);
   if (w) pp.ew.resize(ne * sizeof(R));
   else pp.ew.release();
@@ -667,6 +764,18 @@ dbuf<V> internal_ids(handle_t& h, graph_t& g, array_view_t const* ext)
     HIP_CHECK(hipMemcpyAsync(ids.data(), ext->data, ext->size * sizeof(V), hipMemcpyDefault, h.stream));
   renumber_ext_to_int(h, g, ids.data(), ext->size, true);
   return ids;
+}
+
+// The encoded-x~ push (k_pr_push_enc) is opt-in for unweighted fp32 runs
+// (CGX_PR_PUSH=enc).  Its sums are the same bits as k_pr_push, but on RMAT-22 it
+// measured no faster (0.228 vs 0.225 ms/iteration, same-box A/B): the push is
+// bound by gather latency, not VALU, so the default stays the plain kernel.
+template <typename R>
+bool use_encoded_push(bool weighted)
+{
+  if (weighted || !std::is_same_v<R, float>) return false;
+  char const* e = std::getenv("CGX_PR_PUSH");
+  return e && std::string(e) == "enc";
 }
 
 template <typename V, typename E, typename R>
@@ -792,7 +901,11 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   push = push && adj.pr.ok;
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  auto pkernel = g.weighted ? k_pr_push<V, E, R, true> : k_pr_push<V, E, R, false>;
+  bool const enc = push && use_encoded_push<R>(g.weighted);
+  auto pkernel   = g.weighted ? k_pr_push<V, E, R, true>
+                   : enc      ? k_pr_push_enc<V, E, R>
+                              : k_pr_push<V, E, R, false>;
+  auto akernel   = enc ? k_pr_apply<V, E, R, true> : k_pr_apply<V, E, R, false>;
   if (push) {
     sa.ent    = adj.pr.ent.data<uint32_t>();
     sa.ew     = g.weighted ? adj.pr.ew.data<R>() : nullptr;
@@ -801,6 +914,10 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     for (int i = 0; i <= kXcdSegs; ++i) sa.seg_start[i] = i < (int)adj.pr.seg_start.size() ? adj.pr.seg_start[i] : 0;
     sa.acc    = adj.pr.acc.data<unsigned long long>();
     if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
+    if (enc) {
+      hipLaunchKernelGGL((k_encode_x<R>), dim3(grid_for(nv, kBlock, 4096)), dim3(kBlock), 0, s, xa.data(), nv);
+      CGX_LAUNCH_CHECK();
+    }
     nblk_push  = (int)std::min<int64_t>(sa.nunits, 256 * 2);  // 64 KB LDS: two blocks per CU
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
@@ -829,7 +946,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
         if (push) {
           sa.a = a;
           if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
-          hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sa);
+          hipLaunchKernelGGL(akernel, dim3(nblk_apply), dim3(kBlock), 0, s, sa);
         } else {
           hipLaunchKernelGGL(kernel, dim3(nblk_iter), dim3(kBlock), 0, s, a);
         }
@@ -1037,6 +1154,11 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t 
   sp.nunits = blk.pp.nunits;
   for (int i = 0; i <= kXcdSegs; ++i) sp.seg_start[i] = i < (int)blk.pp.seg_start.size() ? blk.pp.seg_start[i] : 0;
   sp.acc    = blk.pp.acc.data<unsigned long long>();
+  bool const enc = use_encoded_push<R>(g.weighted);
+  if (enc && n_own > 0) {  // x~ of the init pass -> encoded words before the first allgather
+    hipLaunchKernelGGL((k_encode_x<R>), dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s, x_send.data(), n_own);
+    CGX_LAUNCH_CHECK();
+  }
   sap       = sp;
   sap.acc   = acc_own.data();
   int const nblk_push  = (int)std::min<int64_t>(sp.nunits, 256 * 2);
@@ -1061,12 +1183,15 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t 
         }
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
         if (nblk_push)
-          hipLaunchKernelGGL((g.weighted ? k_pr_push<V, E, R, true> : k_pr_push<V, E, R, false>), dim3(nblk_push),
-                             dim3(kPushThreads), 0, s, sp);
+          hipLaunchKernelGGL((g.weighted ? k_pr_push<V, E, R, true>
+                              : enc      ? k_pr_push_enc<V, E, R>
+                                         : k_pr_push<V, E, R, false>),
+                             dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
         CGX_LAUNCH_CHECK();
         ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
         if (block_acc_bytes) HIP_CHECK(hipMemsetAsync(sp.acc, 0, block_acc_bytes, s));
-        hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
+        hipLaunchKernelGGL((enc ? k_pr_apply<V, E, R, true> : k_pr_apply<V, E, R, false>), dim3(nblk_apply),
+                           dim3(kBlock), 0, s, sap);
         CGX_LAUNCH_CHECK();
         ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
         hipLaunchKernelGGL((k_mg_finish_guarded<V, E, R>), dim3(1), dim3(64), 0, s, a, true);

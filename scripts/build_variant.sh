@@ -5,7 +5,7 @@ set -eu
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 PKG="$ROOT/cugraph-forked_amd"
 OBJ=$(mktemp /tmp/variant.XXXXXX.o)
-/opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -I"$PKG/../include" -I"$PKG/csrc" -Wno-unused-result \
+/opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -I"$PKG/../include" -I"$PKG/csrc" -Wno-unused-result ${VARIANT_FLAGS:-} \
   -x hip -c "$1" -o "$OBJ"
 OTHERS=$(ls "$PKG"/build/*.o | grep -v "/pagerank.hip.o$")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -o "$2" $OBJ $OTHERS

@@ -172,3 +172,18 @@ def test_rmat_multi_window_push(weighted, symmetric, renumber):
     v2, pr2 = plc().pagerank(h, G, verts, wsum[verts].astype(np.float32), None, None, 0.85, 1e-6, 500, False)
     got2 = by_ext(v2, pr2)
     assert np.max(np.abs(got2[vv] - got[vv]) / got[vv]) < REL
+
+
+@pytest.mark.parametrize("scale", [12, 20])
+def test_encoded_push_bitwise_equals_plain(scale, monkeypatch):
+    """The opt-in unweighted fp32 push that gathers x~ as encoded fixed-point
+    words (pagerank.hip k_pr_push_enc, CGX_PR_PUSH=enc) must give the same bits
+    as the default fp64-conversion kernel."""
+    s, d, _ = rmat_graph(scale, False, True)
+    h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
+    r_plain = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    it_plain = h.last_iterations()
+    monkeypatch.setenv("CGX_PR_PUSH", "enc")
+    r_enc = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    assert h.last_iterations() == it_plain
+    assert np.array_equal(r_enc, r_plain)
