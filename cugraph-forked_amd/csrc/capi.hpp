@@ -147,6 +147,10 @@ struct clustering_result_t {
   std::unique_ptr<device_array_t> vertices;
   std::unique_ptr<device_array_t> clusters;
   double modularity = 0;
+  // dendrogram (reference Dendrogram<vertex_t>, dendrogram.hpp): level i holds the
+  // cluster of every level-i vertex this rank owns, in global-id order; its values
+  // are level-(i+1) vertex ids (the last level: that level's cluster ids)
+  std::vector<std::unique_ptr<device_array_t>> levels;
 };
 
 // ------------------------------------------------------------------ helpers

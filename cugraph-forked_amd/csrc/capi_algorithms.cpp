@@ -235,7 +235,6 @@ extern "C" cugraph_error_code_t cugraph_louvain(const cugraph_resource_handle_t*
     CGX_EXPECTS(handle != nullptr, CUGRAPH_INVALID_HANDLE, "invalid resource handle");
     CGX_INPUT(graph != nullptr, "Invalid input argument: graph is NULL");
     auto& g = *G(graph);
-    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED, "multi-GPU Louvain is not implemented in this build");
     auto res = std::make_unique<clustering_result_t>();
     run_louvain(*H(handle), g, max_level, resolution, do_expensive_check == TRUE, *res);
     HIP_CHECK(hipStreamSynchronize(H(handle)->stream));
@@ -247,6 +246,19 @@ extern "C" cugraph_type_erased_device_array_view_t* cugraph_heirarchical_cluster
   cugraph_heirarchical_clustering_result_t* result)
 {
   return new_view(reinterpret_cast<clustering_result_t*>(result)->vertices.get());
+}
+
+extern "C" size_t cugraph_amd_heirarchical_clustering_result_get_num_levels(
+  cugraph_heirarchical_clustering_result_t* result)
+{
+  return reinterpret_cast<clustering_result_t*>(result)->levels.size();
+}
+
+extern "C" cugraph_type_erased_device_array_view_t* cugraph_amd_heirarchical_clustering_result_get_level(
+  cugraph_heirarchical_clustering_result_t* result, size_t level)
+{
+  auto* r = reinterpret_cast<clustering_result_t*>(result);
+  return level < r->levels.size() ? new_view(r->levels[level].get()) : nullptr;
 }
 
 extern "C" cugraph_type_erased_device_array_view_t* cugraph_heirarchical_clustering_result_get_clusters(

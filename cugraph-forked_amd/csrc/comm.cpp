@@ -102,6 +102,9 @@ template dbuf<double> exchange<double>(comm_t&, double const*, std::vector<size_
                                        hipStream_t);
 template dbuf<uint32_t> exchange<uint32_t>(comm_t&, uint32_t const*, std::vector<size_t> const&,
                                            std::vector<size_t>&, hipStream_t);
+template dbuf<unsigned long long> exchange<unsigned long long>(comm_t&, unsigned long long const*,
+                                                               std::vector<size_t> const&, std::vector<size_t>&,
+                                                               hipStream_t);
 
 namespace {
 

@@ -22,6 +22,8 @@
 // reductions are rocPRIM's fixed-partition scans or block-ordered sums: the run is
 // deterministic.
 #include "capi.hpp"
+#include "comm.hpp"
+#include "mg_graph.hpp"
 #include "prims.hpp"
 
 #include <rocprim/device/device_reduce_by_key.hpp>
@@ -36,8 +38,12 @@ namespace {
 
 using u64 = unsigned long long;
 
+// One level's edges.  Single GPU: every vertex is a row (base 0, nrows = nv).
+// Multi-GPU: the rows are this rank's vertices [base, base + nrows) of the nv
+// global ids; `src` holds row indices (global id - base), `dst` global ids.
 struct level_graph {
   int64_t nv = 0, ne = 0;
+  int64_t base = 0, nrows = 0;
   dbuf<uint32_t> src, dst;  // sorted by (src, dst)
   dbuf<double> w;
 };
@@ -106,13 +112,13 @@ __global__ void k_row_offsets(uint32_t const* src, int64_t ne, int64_t nv, int64
 
 // vertex weights k[v] (row sums, in edge order) and self-loop weights
 __global__ void k_vertex_weights(int64_t const* off, uint32_t const* src, uint32_t const* dst, double const* w,
-                                 int64_t nv, double* k, double* self, uint8_t* has_edges)
+                                 int64_t nv, uint32_t base, double* k, double* self, uint8_t* has_edges)
 {
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
     double s = 0, sl = 0;
     for (int64_t e = off[v]; e < off[v + 1]; ++e) {
       s += w[e];
-      if (dst[e] == (uint32_t)v) sl += w[e];
+      if (dst[e] == (uint32_t)v + base) sl += w[e];
     }
     k[v]         = s;
     self[v]      = sl;
@@ -127,40 +133,43 @@ __global__ void k_sweep_keys(uint32_t const* src, uint32_t const* dst, uint32_t 
 }
 
 // old_sum[u] = weight from u into its own cluster, self loops excluded
-__global__ void k_old_sum(u64 const* uk, double const* psum, int64_t np, uint32_t const* c, double const* self,
-                          double* old_sum)
+// (u is a row index; its cluster is c[u + base])
+__global__ void k_old_sum(u64 const* uk, double const* psum, int64_t np, uint32_t const* c, uint32_t base,
+                          double const* self, double* old_sum)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t u = (uint32_t)(uk[i] >> 32), cc = (uint32_t)uk[i];
-    if (cc == c[u]) old_sum[u] = psum[i] - self[u];
+    if (cc == c[u + base]) old_sum[u] = psum[i] - self[u];
   }
 }
 
 // delta modularity of moving u into cluster cc (common_methods.cuh:49-74)
-__global__ void k_gain(u64 const* uk, double const* psum, int64_t np, uint32_t const* c, double const* self,
-                       double const* old_sum, double const* a, uint8_t const* present, double const* k, double m,
-                       double gamma, gain_t* out)
+__global__ void k_gain(u64 const* uk, double const* psum, int64_t np, uint32_t const* c, uint32_t base,
+                       double const* self, double const* old_sum, double const* a, uint8_t const* present,
+                       double const* k, double m, double gamma, gain_t* out)
 {
 #pragma clang fp contract(off)
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t u = (uint32_t)(uk[i] >> 32), cc = (uint32_t)uk[i];
+    uint32_t const cu = c[u + base];
     double s   = psum[i];
-    if (cc == c[u]) s = s - self[u];
+    if (cc == cu) s = s - self[u];
     double a_new = present[cc] ? a[cc] : (double)FLT_MAX;
-    double a_old = a[c[u]];
+    double a_old = a[cu];
     double kk    = k[u];
     double dq    = 2.0 * (((s - old_sum[u]) / m) - gamma * (a_new * kk - a_old * kk + kk * kk) / (m * m));
     out[i]       = gain_t{dq, cc};
   }
 }
 
-__global__ void k_move(uint32_t const* uu, gain_t const* best, int64_t n, uint32_t const* c, uint32_t* next,
-                       bool up_down)
+// next[u] for row u (next is indexed by row)
+__global__ void k_move(uint32_t const* uu, gain_t const* best, int64_t n, uint32_t const* c, uint32_t base,
+                       uint32_t* next, bool up_down)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t u = uu[i];
     gain_t b   = best[i];
-    if (b.dq > 0.0 && ((b.c > c[u]) == up_down)) next[u] = b.c;
+    if (b.dq > 0.0 && ((b.c > c[u + base]) == up_down)) next[u] = b.c;
   }
 }
 
@@ -170,6 +179,7 @@ __global__ void k_scatter_cluster_weights(uint32_t const* ck, double const* cw, 
     a[ck[i]] = cw[i];
 }
 
+// rows v with edges mark their cluster c[v] (c points at the rows' clusters)
 __global__ void k_mark_present(uint32_t const* c, uint8_t const* has_edges, int64_t nv, uint8_t* present)
 {
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x)
@@ -181,7 +191,8 @@ struct internal_f {
   uint32_t const* d;
   double const* w;
   uint32_t const* c;
-  __device__ double operator()(size_t i) const { return c[s[i]] == c[d[i]] ? w[i] : 0.0; }
+  uint32_t base;
+  __device__ double operator()(size_t i) const { return c[s[i] + base] == c[d[i]] ? w[i] : 0.0; }
 };
 struct sumsq_f {
   double const* a;
@@ -263,48 +274,64 @@ struct louvain_state {
   hipStream_t s;
   double m;
   double gamma;
-  dbuf<double> scratch;  // device_sum partials
-  dbuf<double> scal;     // 2 scalars
+  comm_t* comm = nullptr;  // multi-GPU: the world communicator; nullptr on one GPU
+  dbuf<double> scratch;    // device_sum partials
+  dbuf<double> scal;       // 2 scalars
   explicit louvain_state(hipStream_t st) : s(st), scratch(1024, st), scal(2, st) {}
 };
 
+// Q = internal / m - gamma * sum_c a_c^2 / m^2 (compute_modularity,
+// common_methods.cuh:121-170).  Each rank sums its own edges and the a_c of the
+// cluster ids in its own range; the two partials are allreduced.
 double modularity(louvain_state& S, level_graph const& g, uint32_t const* c, double const* a, uint8_t const* present)
 {
-  device_sum(internal_f{g.src.data(), g.dst.data(), g.w.data(), c}, (size_t)g.ne, S.scal.data(), S.scratch.data(), S.s);
-  device_sum(sumsq_f{a, present}, (size_t)g.nv, S.scal.data() + 1, S.scratch.data(), S.s);
+  device_sum(internal_f{g.src.data(), g.dst.data(), g.w.data(), c, (uint32_t)g.base}, (size_t)g.ne, S.scal.data(),
+             S.scratch.data(), S.s);
+  device_sum(sumsq_f{a + g.base, present + g.base}, (size_t)g.nrows, S.scal.data() + 1, S.scratch.data(), S.s);
+  if (S.comm) S.comm->allreduce<double>(S.scal.data(), S.scal.data(), 2, CGX_COMM_SUM, S.s);
   auto hv = to_host(S.scal.data(), 2, S.s);
   return hv[0] / S.m - (S.gamma * hv[1]) / (S.m * S.m);
 }
 
-// cluster weights a[c] = sum of k[v] over v in c; present[c] = some v in c has edges
+// cluster weights a[c] = sum of k[v] over v in c; present[c] = some v in c has
+// edges.  a and present are indexed by cluster id (all nv ids); k and has_edges by
+// row.  Multi-GPU: per-rank partial sums, then a SUM / MAX allreduce.
 void cluster_weights(louvain_state& S, level_graph const& g, uint32_t const* c, double const* k,
                      uint8_t const* has_edges, double* a, uint8_t* present)
 {
   hipStream_t s = S.s;
-  int64_t nv    = g.nv;
-  dbuf<uint32_t> ck(nv, s), ck2(nv, s);
-  dbuf<double> kv2(nv, s);
-  HIP_CHECK(hipMemcpyAsync(ck.data(), c, nv * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  radix_sort_pairs<uint32_t, double>(ck.data(), ck2.data(), k, kv2.data(), (size_t)nv, 0, bits_for(nv - 1), s);
-  dbuf<uint32_t> uk(nv, s);
-  dbuf<double> uw(nv, s);
-  int64_t nu = reduce_by_key(ck2.data(), kv2.data(), (size_t)nv, uk.data(), uw.data(), rocprim::plus<double>(),
-                             rocprim::equal_to<uint32_t>(), s);
+  int64_t nv = g.nv, nr = g.nrows;
   fill<double>(a, nv, 0.0, s);
   fill<uint8_t>(present, nv, 0, s);
-  hipLaunchKernelGGL(k_scatter_cluster_weights, dim3(blocks(nu)), dim3(kBlock), 0, s, uk.data(), uw.data(), nu, a);
-  CGX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_mark_present, dim3(blocks(nv)), dim3(kBlock), 0, s, c, has_edges, nv, present);
-  CGX_LAUNCH_CHECK();
+  if (nr > 0) {
+    dbuf<uint32_t> ck(nr, s), ck2(nr, s);
+    dbuf<double> kv2(nr, s);
+    HIP_CHECK(hipMemcpyAsync(ck.data(), c + g.base, nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    radix_sort_pairs<uint32_t, double>(ck.data(), ck2.data(), k, kv2.data(), (size_t)nr, 0, bits_for(nv - 1), s);
+    dbuf<uint32_t> uk(nr, s);
+    dbuf<double> uw(nr, s);
+    int64_t nu = reduce_by_key(ck2.data(), kv2.data(), (size_t)nr, uk.data(), uw.data(), rocprim::plus<double>(),
+                               rocprim::equal_to<uint32_t>(), s);
+    hipLaunchKernelGGL(k_scatter_cluster_weights, dim3(blocks(nu)), dim3(kBlock), 0, s, uk.data(), uw.data(), nu, a);
+    CGX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_mark_present, dim3(blocks(nr)), dim3(kBlock), 0, s, c + g.base, has_edges, nr, present);
+    CGX_LAUNCH_CHECK();
+  }
+  if (S.comm) {
+    S.comm->allreduce<double>(a, a, (size_t)nv, CGX_COMM_SUM, s);
+    S.comm->allreduce<uint8_t>(present, present, (size_t)nv, CGX_COMM_MAX, s);
+  }
 }
 
-// one synchronous local-move sweep (update_clustering_by_delta_modularity)
+// one synchronous local-move sweep (update_clustering_by_delta_modularity) over
+// this rank's rows; next[row] = the row's cluster after the sweep
 void sweep(louvain_state& S, level_graph const& g, uint32_t const* c, uint32_t* next, double const* k,
            double const* self, double const* a, uint8_t const* present, bool up_down)
 {
   hipStream_t s = S.s;
-  int64_t nv = g.nv, ne = g.ne;
-  HIP_CHECK(hipMemcpyAsync(next, c, nv * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  int64_t nv = g.nv, nr = g.nrows, ne = g.ne;
+  uint32_t const base = (uint32_t)g.base;
+  if (nr) HIP_CHECK(hipMemcpyAsync(next, c + g.base, nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   if (ne == 0) return;
   dbuf<u64> keys(ne, s), keys2(ne, s);
   dbuf<double> w2(ne, s), psum(ne, s);
@@ -312,25 +339,26 @@ void sweep(louvain_state& S, level_graph const& g, uint32_t const* c, uint32_t* 
                      keys.data());
   CGX_LAUNCH_CHECK();
   radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0,
-                                32 + bits_for(nv - 1), s);
-  // (vertex, neighbour cluster) -> sum of weights; `keys` reused for the pair keys
+                                32 + bits_for(std::max<int64_t>(nr - 1, 0)), s);
+  // (row, neighbour cluster) -> sum of weights; `keys` reused for the pair keys
   int64_t np = reduce_by_key(keys2.data(), w2.data(), (size_t)ne, keys.data(), psum.data(), rocprim::plus<double>(),
                              rocprim::equal_to<u64>(), s);
-  dbuf<double> old_sum(nv, s);
-  fill<double>(old_sum.data(), nv, 0.0, s);
-  hipLaunchKernelGGL(k_old_sum, dim3(blocks(np)), dim3(kBlock), 0, s, keys.data(), psum.data(), np, c, self,
+  dbuf<double> old_sum(nr, s);
+  fill<double>(old_sum.data(), nr, 0.0, s);
+  hipLaunchKernelGGL(k_old_sum, dim3(blocks(np)), dim3(kBlock), 0, s, keys.data(), psum.data(), np, c, base, self,
                      old_sum.data());
   CGX_LAUNCH_CHECK();
-  dbuf<gain_t> gains(np, s), best(nv, s);
-  hipLaunchKernelGGL(k_gain, dim3(blocks(np)), dim3(kBlock), 0, s, keys.data(), psum.data(), np, c, self,
+  dbuf<gain_t> gains(np, s), best(nr, s);
+  hipLaunchKernelGGL(k_gain, dim3(blocks(np)), dim3(kBlock), 0, s, keys.data(), psum.data(), np, c, base, self,
                      old_sum.data(), a, present, k, S.m, S.gamma, gains.data());
   CGX_LAUNCH_CHECK();
-  dbuf<uint32_t> uu(nv, s);
+  dbuf<uint32_t> uu(nr, s);
   auto ukeys = rocprim::make_transform_iterator(keys.data(), key_hi());
   int64_t nu = reduce_by_key(ukeys, gains.data(), (size_t)np, uu.data(), best.data(), best_gain_op(),
                              rocprim::equal_to<uint32_t>(), s);
-  hipLaunchKernelGGL(k_move, dim3(blocks(nu)), dim3(kBlock), 0, s, uu.data(), best.data(), nu, c, next, up_down);
+  hipLaunchKernelGGL(k_move, dim3(blocks(nu)), dim3(kBlock), 0, s, uu.data(), best.data(), nu, c, base, next, up_down);
   CGX_LAUNCH_CHECK();
+  (void)nv;
 }
 
 // contract the level graph by `labels` (graph_contraction / coarsen_graph): sum
@@ -372,8 +400,9 @@ level_graph contract(louvain_state& S, level_graph const& g, uint32_t* labels)
   hipLaunchKernelGGL(k_new_ids, dim3(blocks(nu)), dim3(kBlock), 0, s, nmap.data(), nu, nl.data());
   CGX_LAUNCH_CHECK();
   level_graph out;
-  out.nv = nu;
-  out.ne = nce;
+  out.nv    = nu;
+  out.nrows = nu;
+  out.ne    = nce;
   out.src.resize(std::max<int64_t>(nce, 1), s);
   out.dst.resize(std::max<int64_t>(nce, 1), s);
   out.w.resize(std::max<int64_t>(nce, 1), s);
@@ -409,8 +438,9 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
   louvain_state S(s);
   S.gamma = resolution;
   level_graph cur;
-  cur.nv = nv0;
-  cur.ne = g.num_edges;
+  cur.nv    = nv0;
+  cur.nrows = nv0;
+  cur.ne    = g.num_edges;
   cur.src.resize(std::max<int64_t>(cur.ne, 1), s);
   cur.dst.resize(std::max<int64_t>(cur.ne, 1), s);
   cur.w.resize(std::max<int64_t>(cur.ne, 1), s);
@@ -436,7 +466,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     dbuf<double> k(nv, s), self(nv, s), a(nv, s);
     dbuf<uint8_t> has_edges(nv, s), present(nv, s);
     hipLaunchKernelGGL(k_vertex_weights, dim3(blocks(nv)), dim3(kBlock), 0, s, off.data(), cur.src.data(),
-                       cur.dst.data(), cur.w.data(), nv, k.data(), self.data(), has_edges.data());
+                       cur.dst.data(), cur.w.data(), nv, 0u, k.data(), self.data(), has_edges.data());
     CGX_LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(a.data(), k.data(), nv * sizeof(double), hipMemcpyDeviceToDevice, s));
     fill<uint8_t>(present.data(), nv, 1, s);
@@ -468,6 +498,396 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
   hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(nv0)), dim3(kBlock), 0, s, flat.data(), nv0,
                      res.clusters->buf.data<V>());
   CGX_LAUNCH_CHECK();
+  for (auto& lvl : dendrogram) {
+    res.levels.push_back(std::make_unique<device_array_t>(lvl.n, g.vertex_type, s));
+    hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(lvl.n)), dim3(kBlock), 0, s, lvl.data(), (int64_t)lvl.n,
+                       res.levels.back()->buf.data<V>());
+    CGX_LAUNCH_CHECK();
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  res.modularity        = best_q;
+  h.last_louvain_levels = dendrogram.size();
+}
+
+// ================================================================ multi-GPU
+//
+// Reference: louvain_impl.cuh:46-237 with multi_gpu = true, the MG branches of
+// common_methods.cuh:200-382 (cluster weights shuffled to the key owner, the
+// neighbour clusters' weights collected from their owners) and
+// coarsen_graph_impl.cuh:243-516 (coarse edges shuffled to the owner of their
+// source, renumbered per owner).  The MI355X layout:
+//
+//  * rows: every rank holds the out-edges of the vertices it owns ([voff[p],
+//    voff[p+1]) of the level's global ids, a 1D partition by source owner),
+//    sorted by (row, destination) with fp64 weights;
+//  * the clustering c, the cluster weights a and the present flags are dense
+//    arrays over all of the level's ids on every rank (4 + 8 + 1 bytes per vertex:
+//    1 GB at RMAT-26 against 288 GB of HBM).  A sweep runs the single-GPU local
+//    move on the rank's rows, then one allgather of the moved rows' clusters and
+//    one SUM / MAX allreduce of the per-rank cluster-weight partials re-replicate
+//    them -- no per-edge exchange at all;
+//  * modularity: per-rank partials (own edges, own cluster-id range) + a 2-double
+//    allreduce, so every rank takes the same branch of the level loop;
+//  * contraction: coarse pairs (label(u), label(v)) are reduced locally, sent to
+//    the owner of label(u) with one all-to-all and merged there; each owner numbers
+//    its used labels by descending coarse degree (ties: ascending label), the
+//    owners' ranges stay contiguous, and a dense label -> new id table is
+//    allgathered.
+//
+// With one rank this is exactly the single-GPU algorithm (same ids, same sums).
+// With several, every decision is the single-GPU decision on the same
+// (MG-numbered) level graph whenever the sums are exact (integer weights), which is
+// what the reference's MG test checks level by level (mg_louvain_test.cpp:82-151).
+
+template <typename V>
+__global__ void k_owner_of_src(V const* src, int64_t n, int64_t const* voff, int P, int* dest)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dest[i] = mg_owner_of_global((int64_t)src[i], voff, P);
+}
+
+// first position of rank q's run in a sorted owner array, q = 0..P
+__global__ void k_rank_bounds(int const* sorted, int64_t n, int P, int64_t* out)
+{
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > P) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (sorted[mid] < q) lo = mid + 1;
+    else hi = mid;
+  }
+  out[q] = lo;
+}
+
+// first position of keys with (key >> 32) >= voff[q], q = 0..P (keys sorted)
+__global__ void k_key_bounds(u64 const* keys, int64_t n, int64_t const* voff, int P, int64_t* out)
+{
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > P) return;
+  u64 const t = (u64)voff[q] << 32;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < t) lo = mid + 1;
+    else hi = mid;
+  }
+  out[q] = lo;
+}
+
+template <typename V>
+__global__ void k_mg_row_keys(V const* src, V const* dst, int64_t n, int64_t base, u64* keys)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    keys[i] = ((u64)((int64_t)src[i] - base) << 32) | (u64)(uint32_t)dst[i];
+}
+
+// coarse pair key (label(row + base), label(dst)) of every local edge
+__global__ void k_mg_pair_keys(uint32_t const* src, uint32_t const* dst, uint32_t const* lab, uint32_t base,
+                               int64_t ne, u64* keys)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+    keys[e] = ((u64)lab[src[e] + base] << 32) | (u64)lab[dst[e]];
+}
+
+// used[l - lo] = 1 for every label l in [lo, hi) that some vertex carries
+__global__ void k_mark_used_range(uint32_t const* lab, int64_t nv, int64_t lo, int64_t hi, uint32_t* used)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    int64_t l = lab[v];
+    if (l >= lo && l < hi) used[l - lo] = 1u;
+  }
+}
+
+__global__ void k_count_src_off(u64 const* keys, int64_t n, int64_t lo, uint32_t* deg)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(deg + ((int64_t)(keys[i] >> 32) - lo), 1u);
+}
+
+__global__ void k_new_ids_off(uint32_t const* nmap, int64_t n, uint32_t first, uint32_t* new_of_label)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    new_of_label[nmap[i]] = first + (uint32_t)i;
+}
+
+// (label(u), label(v)) -> (new(u) - new_lo, new(v))
+__global__ void k_relabel_pairs_local(u64 const* keys, int64_t n, uint32_t const* nl, uint32_t new_lo, u64* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = ((u64)(nl[(uint32_t)(keys[i] >> 32)] - new_lo) << 32) | (u64)nl[(uint32_t)keys[i]];
+}
+
+// out[voff[q] ..] = every rank's `own` slice (allgather padded to the largest slice)
+template <typename T>
+void allgatherv_dense(comm_t& comm, T const* own, std::vector<int64_t> const& voff, T* out, hipStream_t s)
+{
+  int const P = comm.size, p = comm.rank;
+  int64_t nmax = 0;
+  for (int q = 0; q < P; ++q) nmax = std::max(nmax, voff[q + 1] - voff[q]);
+  if (nmax == 0) return;
+  dbuf<T> sb(nmax, s), rb((size_t)nmax * P, s);
+  int64_t const n = voff[p + 1] - voff[p];
+  if (n) HIP_CHECK(hipMemcpyAsync(sb.data(), own, n * sizeof(T), hipMemcpyDeviceToDevice, s));
+  comm.allgather<T>(sb.data(), rb.data(), (size_t)nmax, s);
+  for (int q = 0; q < P; ++q) {
+    int64_t nq = voff[q + 1] - voff[q];
+    if (nq)
+      HIP_CHECK(hipMemcpyAsync(out + voff[q], rb.data() + (size_t)q * nmax, nq * sizeof(T), hipMemcpyDeviceToDevice,
+                               s));
+  }
+}
+
+std::vector<int64_t> bounds_to_counts(dbuf<int64_t> const& b, int P, hipStream_t s)
+{
+  auto hb = to_host(b.data(), P + 1, s);
+  std::vector<int64_t> c(P);
+  for (int q = 0; q < P; ++q) c[q] = hb[q + 1] - hb[q];
+  return c;
+}
+
+// level 0: the 2D block's edges -> rows of this rank's sources
+template <typename V, typename R>
+level_graph mg_level0(handle_t& h, graph_t& g)
+{
+  hipStream_t s = h.stream;
+  mg_graph_t& mg = *g.mg;
+  comm_t& comm   = *h.mg->world;
+  int const P    = mg.P;
+  dbuf<int64_t> voff_d(P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  int64_t const ne = mg.ne, n1 = std::max<int64_t>(ne, 1);
+  dbuf<int> dest(n1, s), d2(n1, s);
+  dbuf<int64_t> iv(n1, s), perm(n1, s), bnd(P + 1, s);
+  dbuf<V> ps(n1, s), pd(n1, s);
+  dbuf<R> pw(n1, s);
+  if (ne) {
+    hipLaunchKernelGGL(k_owner_of_src<V>, dim3(blocks(ne)), dim3(kBlock), 0, s, mg.src.data<V>(), ne, voff_d.data(),
+                       P, dest.data());
+    CGX_LAUNCH_CHECK();
+    iota<int64_t>(iv.data(), ne, 0, s);
+    radix_sort_pairs<int, int64_t>(dest.data(), d2.data(), iv.data(), perm.data(), ne, 0, bits_for(P), s);
+    gather<V, int64_t>(ps.data(), mg.src.data<V>(), perm.data(), ne, s);
+    gather<V, int64_t>(pd.data(), mg.dst.data<V>(), perm.data(), ne, s);
+    gather<R, int64_t>(pw.data(), mg.w.data<R>(), perm.data(), ne, s);
+  }
+  hipLaunchKernelGGL(k_rank_bounds, dim3(1), dim3(256), 0, s, d2.data(), ne, P, bnd.data());
+  CGX_LAUNCH_CHECK();
+  auto c64 = bounds_to_counts(bnd, P, s);
+  std::vector<size_t> counts(c64.begin(), c64.end()), rc;
+  auto rs = exchange<V>(comm, ps.data(), counts, rc, s);
+  auto rd = exchange<V>(comm, pd.data(), counts, rc, s);
+  auto rw = exchange<R>(comm, pw.data(), counts, rc, s);
+  level_graph out;
+  out.nv    = g.num_vertices;
+  out.base  = mg.voff[mg.p];
+  out.nrows = mg.n_own();
+  out.ne    = (int64_t)rs.n;
+  int64_t const m = out.ne, m1 = std::max<int64_t>(m, 1);
+  out.src.resize(m1, s);
+  out.dst.resize(m1, s);
+  out.w.resize(m1, s);
+  if (m) {
+    dbuf<u64> k1(m, s), k2(m, s);
+    dbuf<double> w1(m, s);
+    hipLaunchKernelGGL(k_mg_row_keys<V>, dim3(blocks(m)), dim3(kBlock), 0, s, rs.data(), rd.data(), m, out.base,
+                       k1.data());
+    CGX_LAUNCH_CHECK();
+    convert<double, R>(w1.data(), rw.data(), m, s);
+    radix_sort_pairs<u64, double>(k1.data(), k2.data(), w1.data(), out.w.data(), (size_t)m, 0,
+                                  32 + bits_for(std::max<int64_t>(out.nrows - 1, 0)), s);
+    hipLaunchKernelGGL(k_split_pairs, dim3(blocks(m)), dim3(kBlock), 0, s, k2.data(), m, out.src.data(),
+                       out.dst.data());
+    CGX_LAUNCH_CHECK();
+  }
+  return out;
+}
+
+// contract by the dense level labels `lab` (nv entries, values in [0, nv)); on
+// return `voff` holds the coarse level's vertex ranges and `lab` the coarse ids
+level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, std::vector<int64_t>& voff)
+{
+  hipStream_t s = S.s;
+  comm_t& comm  = *S.comm;
+  int const P = comm.size, p = comm.rank;
+  int64_t const nv = g.nv, ne = g.ne, nr = g.nrows, lo = g.base;
+  int64_t const n1 = std::max<int64_t>(ne, 1);
+  dbuf<int64_t> voff_d(P + 1, s), bnd(P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  // 1. local coarse pairs, summed
+  dbuf<u64> keys(n1, s), keys2(n1, s);
+  dbuf<double> w2(n1, s), cw(n1, s);
+  int64_t nce = 0;
+  if (ne) {
+    hipLaunchKernelGGL(k_mg_pair_keys, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), lab,
+                       (uint32_t)lo, ne, keys.data());
+    CGX_LAUNCH_CHECK();
+    radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0,
+                                  32 + bits_for(nv - 1), s);
+    nce = reduce_by_key(keys2.data(), w2.data(), (size_t)ne, keys.data(), cw.data(), rocprim::plus<double>(),
+                        rocprim::equal_to<u64>(), s);
+  }
+  // 2. to the owner of label(u) (keys are sorted, owner ranges ascending)
+  hipLaunchKernelGGL(k_key_bounds, dim3(1), dim3(256), 0, s, keys.data(), nce, voff_d.data(), P, bnd.data());
+  CGX_LAUNCH_CHECK();
+  auto c64 = bounds_to_counts(bnd, P, s);
+  std::vector<size_t> counts(c64.begin(), c64.end()), rc;
+  auto rk = exchange<u64>(comm, keys.data(), counts, rc, s);
+  auto rw = exchange<double>(comm, cw.data(), counts, rc, s);
+  int64_t const nrcv = (int64_t)rk.n, r1 = std::max<int64_t>(nrcv, 1);
+  dbuf<u64> mk(r1, s), mk2(r1, s);
+  dbuf<double> mw(r1, s), mw2(r1, s);
+  int64_t nm = 0;
+  if (nrcv) {
+    radix_sort_pairs<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0,
+                                  32 + bits_for(nv - 1), s);
+    nm = reduce_by_key(mk2.data(), mw2.data(), (size_t)nrcv, mk.data(), mw.data(), rocprim::plus<double>(),
+                       rocprim::equal_to<u64>(), s);
+  }
+  // 3. my used labels, numbered by descending coarse out-degree (stable)
+  dbuf<uint32_t> used(nr + 1, s), pos(nr + 1, s), deg(std::max<int64_t>(nr, 1), s);
+  fill<uint32_t>(used.data(), nr + 1, 0u, s);
+  fill<uint32_t>(deg.data(), std::max<int64_t>(nr, 1), 0u, s);
+  hipLaunchKernelGGL(k_mark_used_range, dim3(blocks(nv)), dim3(kBlock), 0, s, lab, nv, lo, lo + nr, used.data());
+  CGX_LAUNCH_CHECK();
+  if (nm) hipLaunchKernelGGL(k_count_src_off, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, lo, deg.data());
+  CGX_LAUNCH_CHECK();
+  exclusive_scan<uint32_t, uint32_t>(used.data(), pos.data(), nr + 1, s);
+  int64_t const nu = (int64_t)to_host_scalar(pos.data() + nr, s), u1 = std::max<int64_t>(nu, 1);
+  dbuf<uint32_t> uniq(u1, s), udeg(u1, s), udeg2(u1, s), nmap(u1, s), nl_own(std::max<int64_t>(nr, 1), s);
+  if (nr)
+    hipLaunchKernelGGL(k_compact_labels, dim3(blocks(nr)), dim3(kBlock), 0, s, used.data(), pos.data(), deg.data(), nr,
+                       uniq.data(), udeg.data());
+  CGX_LAUNCH_CHECK();
+  if (nu)
+    radix_sort_pairs<uint32_t, uint32_t>(udeg.data(), udeg2.data(), uniq.data(), nmap.data(), (size_t)nu, 0,
+                                         bits_for((unsigned long long)std::max<int64_t>(nm, 1)), s,
+                                         /*descending=*/true);
+  auto all_nu = comm.host_allgather<int64_t>(nu, s);
+  std::vector<int64_t> nvoff(P + 1, 0);
+  for (int q = 0; q < P; ++q) nvoff[q + 1] = nvoff[q] + all_nu[q];
+  uint32_t const new_lo = (uint32_t)nvoff[p];
+  if (nu)
+    hipLaunchKernelGGL(k_new_ids_off, dim3(blocks(nu)), dim3(kBlock), 0, s, nmap.data(), nu, new_lo, nl_own.data());
+  CGX_LAUNCH_CHECK();
+  // 4. dense label -> new id table (entries of unused labels are never read)
+  dbuf<uint32_t> nl(std::max<int64_t>(nv, 1), s);
+  allgatherv_dense<uint32_t>(comm, nl_own.data(), voff, nl.data(), s);
+  level_graph out;
+  out.nv    = nvoff[P];
+  out.base  = nvoff[p];
+  out.nrows = nu;
+  out.ne    = nm;
+  out.src.resize(std::max<int64_t>(nm, 1), s);
+  out.dst.resize(std::max<int64_t>(nm, 1), s);
+  out.w.resize(std::max<int64_t>(nm, 1), s);
+  if (nm) {
+    hipLaunchKernelGGL(k_relabel_pairs_local, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, nl.data(), new_lo,
+                       mk2.data());
+    CGX_LAUNCH_CHECK();
+    radix_sort_pairs<u64, double>(mk2.data(), mk.data(), mw.data(), out.w.data(), (size_t)nm, 0,
+                                  32 + bits_for(std::max<int64_t>(nu - 1, 0)), s);
+    hipLaunchKernelGGL(k_split_pairs, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, out.src.data(),
+                       out.dst.data());
+    CGX_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_gather_u32, dim3(blocks(nv)), dim3(kBlock), 0, s, nl.data(), lab, nv);
+  CGX_LAUNCH_CHECK();
+  voff = nvoff;
+  return out;
+}
+
+template <typename V, typename E, typename R>
+void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, clustering_result_t& res)
+{
+  hipStream_t s = h.stream;
+  CGX_EXPECTS(g.weighted, CUGRAPH_UNKNOWN_ERROR, "Graph must be weighted");  // louvain_impl.cuh:290
+  mg_graph_t& mg = *g.mg;
+  comm_t& comm   = *h.mg->world;
+  int const p    = mg.p;
+  int64_t const nv0 = g.num_vertices, n_own = mg.n_own();
+  CGX_EXPECTS((uint64_t)nv0 < (1ull << 32), CUGRAPH_NOT_IMPLEMENTED, "Louvain: more than 2^32 vertices");
+  res.vertices = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
+  if (n_own)
+    HIP_CHECK(hipMemcpyAsync(res.vertices->buf.data(), g.number_map.data(), n_own * sizeof(V), hipMemcpyDeviceToDevice,
+                             s));
+  res.clusters = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
+  h.last_louvain_levels = 0;
+  res.modularity        = 0;
+  if (nv0 == 0) return;
+
+  louvain_state S(s);
+  S.gamma        = resolution;
+  S.comm         = &comm;
+  level_graph cur = mg_level0<V, R>(h, g);
+  device_sum(plain_f{cur.w.data()}, (size_t)cur.ne, S.scal.data(), S.scratch.data(), s);
+  comm.allreduce<double>(S.scal.data(), S.scal.data(), 1, CGX_COMM_SUM, s);
+  S.m = to_host_scalar(S.scal.data(), s);
+
+  std::vector<int64_t> voff = mg.voff;
+  std::vector<dbuf<uint32_t>> dendrogram;  // dense: every level-i id on every rank
+  std::vector<std::vector<int64_t>> level_voff;
+  double best_q = -1.0;
+  while (dendrogram.size() < max_level) {
+    int64_t const nv = cur.nv, nr = cur.nrows, r1 = std::max<int64_t>(nr, 1);
+    dendrogram.emplace_back(std::max<int64_t>(nv, 1), s);
+    level_voff.push_back(voff);
+    uint32_t* level = dendrogram.back().data();
+    iota<uint32_t>(level, nv, 0u, s);
+    dbuf<int64_t> off(nr + 1, s);
+    hipLaunchKernelGGL(k_row_offsets, dim3(blocks(nr + 1)), dim3(kBlock), 0, s, cur.src.data(), cur.ne, nr,
+                       off.data());
+    CGX_LAUNCH_CHECK();
+    dbuf<double> k(r1, s), self(r1, s), a(nv, s);
+    dbuf<uint8_t> has_edges(r1, s), present(nv, s);
+    if (nr)
+      hipLaunchKernelGGL(k_vertex_weights, dim3(blocks(nr)), dim3(kBlock), 0, s, off.data(), cur.src.data(),
+                         cur.dst.data(), cur.w.data(), nr, (uint32_t)cur.base, k.data(), self.data(),
+                         has_edges.data());
+    CGX_LAUNCH_CHECK();
+    allgatherv_dense<double>(comm, k.data(), voff, a.data(), s);
+    fill<uint8_t>(present.data(), nv, 1, s);
+    dbuf<uint32_t> clusters(nv, s), next(r1, s);
+    iota<uint32_t>(clusters.data(), nv, 0u, s);
+    double new_q = modularity(S, cur, clusters.data(), a.data(), present.data());
+    double cur_q = new_q - 1.0;
+    bool up_down = true;
+    while (new_q > cur_q + 0.0001) {
+      cur_q = new_q;
+      sweep(S, cur, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down);
+      allgatherv_dense<uint32_t>(comm, next.data(), voff, clusters.data(), s);
+      cluster_weights(S, cur, clusters.data(), k.data(), has_edges.data(), a.data(), present.data());
+      up_down = !up_down;
+      new_q   = modularity(S, cur, clusters.data(), a.data(), present.data());
+      if (new_q > cur_q)
+        HIP_CHECK(hipMemcpyAsync(level, clusters.data(), nv * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    }
+    if (cur_q <= best_q) break;
+    best_q = cur_q;
+    cur    = mg_contract(S, cur, level, voff);
+  }
+  // flatten_dendrogram for the owned level-0 vertices
+  int64_t const lo0 = mg.voff[p];
+  dbuf<uint32_t> flat(std::max<int64_t>(n_own, 1), s);
+  if (n_own) {
+    HIP_CHECK(hipMemcpyAsync(flat.data(), dendrogram[0].data() + lo0, n_own * sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, s));
+    for (size_t i = 1; i < dendrogram.size(); ++i)
+      hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n_own)), dim3(kBlock), 0, s, dendrogram[i].data(), flat.data(),
+                         n_own);
+    CGX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, flat.data(), n_own,
+                       res.clusters->buf.data<V>());
+    CGX_LAUNCH_CHECK();
+  }
+  for (size_t i = 0; i < dendrogram.size(); ++i) {
+    int64_t const b = level_voff[i][p], n = level_voff[i][p + 1] - b;
+    res.levels.push_back(std::make_unique<device_array_t>((size_t)n, g.vertex_type, s));
+    if (n)
+      hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(n)), dim3(kBlock), 0, s, dendrogram[i].data() + b, n,
+                         res.levels.back()->buf.data<V>());
+    CGX_LAUNCH_CHECK();
+  }
   HIP_CHECK(hipStreamSynchronize(s));
   res.modularity        = best_q;
   h.last_louvain_levels = dendrogram.size();
@@ -480,7 +900,11 @@ void run_louvain(handle_t& h, graph_t& g, size_t max_level, double resolution, b
 {
   dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
     using T = decltype(t);
-    louvain_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, max_level, resolution, res);
+    if (g.multi_gpu)
+      mg_louvain_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, max_level, resolution,
+                                                                                      res);
+    else
+      louvain_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, max_level, resolution, res);
   });
 }
 

@@ -317,3 +317,24 @@ def louvain(resource_handle, graph, max_level, resolution, do_expensive_check):
     finally:
         _lib.lib.cugraph_heirarchical_clustering_result_free(res)
     return v, c, q
+
+
+def louvain_dendrogram(resource_handle, graph, max_level, resolution, do_expensive_check=False):
+    """Extension (the reference C++ ``cugraph::louvain`` returns the Dendrogram,
+    louvain_impl.cuh:280-301).  Returns (vertices, clusters, modularity, levels):
+    ``levels[i]`` is this rank's slice of dendrogram level i (its level-i vertices
+    in global-id order; values are level-(i+1) ids)."""
+    res = ctypes.c_void_p()
+    _lib.call("cugraph_louvain", resource_handle.ptr, graph.c_graph_ptr, int(max_level), float(resolution),
+              int(bool(do_expensive_check)), ctypes.byref(res))
+    h = resource_handle.ptr
+    try:
+        v = copy_view_to_tensor(h, _lib.lib.cugraph_heirarchical_clustering_result_get_vertices(res))
+        c = copy_view_to_tensor(h, _lib.lib.cugraph_heirarchical_clustering_result_get_clusters(res))
+        q = _lib.lib.cugraph_heirarchical_clustering_result_get_modularity(res)
+        n = _lib.lib.cugraph_amd_heirarchical_clustering_result_get_num_levels(res)
+        levels = [copy_view_to_tensor(h, _lib.lib.cugraph_amd_heirarchical_clustering_result_get_level(res, i))
+                  for i in range(n)]
+    finally:
+        _lib.lib.cugraph_heirarchical_clustering_result_free(res)
+    return v, c, q, levels

@@ -120,6 +120,8 @@ _proto("cugraph_heirarchical_clustering_result_get_vertices", P, P)
 _proto("cugraph_heirarchical_clustering_result_get_clusters", P, P)
 _proto("cugraph_heirarchical_clustering_result_get_modularity", c_double, P)
 _proto("cugraph_heirarchical_clustering_result_free", None, P)
+_proto("cugraph_amd_heirarchical_clustering_result_get_num_levels", c_size_t, P)
+_proto("cugraph_amd_heirarchical_clustering_result_get_level", P, P, c_size_t)
 # extensions (include/cugraph_amd/ext.h)
 _proto("cugraph_amd_generate_rmat_edgelist", c_int, P, c_size_t, c_size_t, c_double, c_double, c_double,
        ctypes.c_uint64, c_int, c_int, c_size_t, c_int, PP, PP, PP)

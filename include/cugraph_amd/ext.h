@@ -92,6 +92,14 @@ size_t cugraph_amd_last_bfs_levels(const cugraph_resource_handle_t* handle);
 size_t cugraph_amd_last_bfs_bottom_up_steps(const cugraph_resource_handle_t* handle);
 /* Louvain: levels of the last call */
 size_t cugraph_amd_last_louvain_levels(const cugraph_resource_handle_t* handle);
+/* Louvain dendrogram (the reference C++ API returns Dendrogram<vertex_t>,
+ * louvain_impl.cuh:280-301; the C ABI only exposes the flattened clustering).
+ * Level i holds the cluster of every level-i vertex this rank owns, in global-id
+ * order (a rank's level-i vertices are one contiguous id range, ranks in order);
+ * its values are level-(i+1) vertex ids.  The view lives as long as the result. */
+size_t cugraph_amd_heirarchical_clustering_result_get_num_levels(cugraph_heirarchical_clustering_result_t* result);
+cugraph_type_erased_device_array_view_t* cugraph_amd_heirarchical_clustering_result_get_level(
+  cugraph_heirarchical_clustering_result_t* result, size_t level);
 
 /* Library build string, e.g. "cugraph-forked_amd gfx950 <date>". */
 const char* cugraph_amd_version(void);

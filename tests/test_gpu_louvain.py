@@ -126,3 +126,21 @@ def test_repeat_is_deterministic():
     a = run(h, G)
     b = run(h, G)
     assert np.array_equal(a[1], b[1]) and a[2] == b[2]
+
+
+def test_dendrogram_levels_compose_to_clusters():
+    """cugraph_amd_heirarchical_clustering_result_get_level: the levels (reference
+    Dendrogram) compose to the flattened clustering (flatten_dendrogram,
+    louvain_impl.cuh:239-255) and the level count is the reported one."""
+    s, d = rmat.rmat(11, 16 << 11, seed=3)
+    w = np.floor(rmat.rmat_weights(s.size, seed=4).astype(np.float64) * 8.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    h, G = make_graph(s, d, w, renumber=True, symmetric=True)
+    v, c, q, levels = plc().louvain_dendrogram(h, G, 100, 1.0)
+    lv = [host(x).astype(np.int64) for x in levels]
+    assert len(lv) == h.last_louvain_levels() >= 2
+    flat = np.arange(lv[0].size)
+    for i, x in enumerate(lv):
+        assert i == 0 or x.size == lv[i - 1].max() + 1
+        flat = x[flat]
+    assert np.array_equal(flat, host(c))

@@ -122,3 +122,112 @@ def test_mg_rccl_single_rank(algo):
     one rank a single GPU allows: every collective of the MG path runs through RCCL."""
     import torch.multiprocessing as tmp
     tmp.spawn(_worker, args=(1, _free_port(), 1, 11, False, algo, "rccl"), nprocs=1, join=True)
+
+
+def _same_partition(a, b):
+    """renumbered_vectors_same (cpp/tests/utilities): equal up to a relabelling."""
+    a, b = np.asarray(a), np.asarray(b)
+    if a.shape != b.shape:
+        return False
+    pairs = np.unique(np.stack([a, b]), axis=1).shape[1]
+    return pairs == np.unique(a).size == np.unique(b).size
+
+
+def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
+    """MG Louvain checked as cpp/tests/community/mg_louvain_test.cpp:82-151 does:
+    the SG algorithm (here the oracle) on the graph renumbered by the MG number map
+    reproduces every MG dendrogram level as a partition, the SG graph is coarsened
+    by the MG level, and the final modularities agree."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pylibcugraph as plc
+    from oracle import graph as og
+    from oracle import louvain as olv
+    from oracle import rmat
+
+    s, d = rmat.rmat(scale, 16 << scale, seed=7)
+    w = rmat.rmat_weights(s.size, seed=8).astype(np.float64)
+    if integer:
+        w = np.floor(w * 8.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    w = w.astype(np.float32).astype(np.float64)
+    E = s.size
+    lo, hi = rank * E // world, (rank + 1) * E // world
+    ctx = plc.comms.init_torch(C) if comm == "torch" else plc.comms.init_rccl(C)
+    h = plc.ResourceHandle(ctx.ptr)
+    st = torch.as_tensor(s[lo:hi].astype(np.int32), device="cuda")
+    dt = torch.as_tensor(d[lo:hi].astype(np.int32), device="cuda")
+    wt = torch.as_tensor(w[lo:hi].astype(np.float32), device="cuda")
+    G = plc.MGGraph(h, plc.GraphProperties(is_symmetric=True, is_multigraph=False), st, dt, wt,
+                    store_transposed=False, num_edges=E)
+    v, c, q, levels = plc.louvain_dendrogram(h, G, 100, 1.0)
+    mine = (v.cpu().numpy(), c.cpu().numpy(), q, [x.cpu().numpy() for x in levels])
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    if rank == 0:
+        assert all(a[2] == q for a in allr)  # every rank returns the same modularity
+        nmap = np.concatenate([a[0] for a in allr]).astype(np.int64)  # global id -> external id
+        assert np.array_equal(np.sort(nmap), np.unique(np.concatenate([s, d])))
+        inv = np.zeros(int(nmap.max()) + 1, dtype=np.int64)
+        inv[nmap] = np.arange(nmap.size)
+        L = len(levels)
+        lv = [np.concatenate([a[3][i] for a in allr]).astype(np.int64) for i in range(L)]
+        gs, gd, gw, V = inv[s], inv[d], w, nmap.size
+        best, qs = -1.0, []
+        for i in range(L):
+            assert lv[i].size == V
+            oc, oq, _ = olv.louvain(V, gs, gd, gw, max_level=1)
+            if integer:
+                assert _same_partition(oc, lv[i]), f"level {i}"
+            qs.append(oq)
+            if oq <= best:
+                assert i == L - 1, "MG went on after a level without gain"
+                break
+            best = oq
+            if i + 1 < L:  # coarsen the SG graph by the MG level (mg_louvain_helper coarsen_graph)
+                cs, cd = lv[i][gs], lv[i][gd]
+                key = cs * (lv[i].max() + 1) + cd
+                uk, inv_k = np.unique(key, return_inverse=True)
+                gw = np.bincount(inv_k, weights=gw)
+                gs, gd = uk // (lv[i].max() + 1), uk % (lv[i].max() + 1)
+                V = lv[i + 1].size
+        if integer:
+            assert q == pytest.approx(best, rel=1e-12, abs=1e-12)
+        else:
+            assert q == pytest.approx(best, rel=1e-6)
+        # the flattened clustering is the composition of the levels
+        flat = np.arange(nmap.size)
+        for x in lv:
+            flat = x[flat]
+        clus = np.concatenate([a[1] for a in allr]).astype(np.int64)
+        assert np.array_equal(clus, flat)
+        assert olv.modularity(inv[s], inv[d], w, flat) >= q - 1e-9
+        if world == 1 and integer:  # one rank: exactly the single-GPU algorithm
+            OG = og.create_graph(s, d, w, renumber=True)
+            os_, od, ow = OG.coo()
+            oc, oq, olevels = olv.louvain(OG.num_vertices, os_, od, ow, 100, 1.0)
+            assert np.array_equal(OG.number_map, nmap) and np.array_equal(oc, clus)
+            assert q == oq and olevels == L
+    dist.barrier()
+    h = None
+    G = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C,integer", [(2, 2, True), (3, 3, True), (4, 2, True), (2, 1, False)])
+def test_mg_louvain_levels_vs_oracle(world, C, integer):
+    import torch.multiprocessing as tmp
+    tmp.spawn(_louvain_worker, args=(world, _free_port(), C, 10, integer), nprocs=world, join=True)
+
+
+def test_mg_louvain_rccl_single_rank():
+    import torch.multiprocessing as tmp
+    tmp.spawn(_louvain_worker, args=(1, _free_port(), 1, 11, True, "rccl"), nprocs=1, join=True)
