@@ -16,6 +16,8 @@ Extra fields on the same JSON line:
                    oracle/baseline.py) for a few iterations on the SAME graph.
   bfs           -- configs[2]: RMAT scale-24 BFS MTEPS (Graph500 counting), when
                    the BFS path is available.
+  louvain       -- configs[4]: Louvain time-to-solution, modularity and levels on
+                   RMAT scale 23 + log2(N) (scale 26 at 8 GPUs), uniform weights.
 
 Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU):
 weak scaling, R-MAT scale 22 + log2(N) for PageRank (the headline value); the
@@ -202,6 +204,32 @@ def bfs_leg(p, args):
             "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)"}
 
 
+def louvain_leg(p, args):
+    """configs[4]: Louvain time-to-solution on a symmetrised R-MAT graph with uniform
+    [0, 1) fp32 weights (seed 42, cugraph_funcs.py:56-58), max_level 100,
+    resolution 1.0.  SG at N=1, the MG path (rows by source owner, RCCL) at N>1."""
+    import torch
+    h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
+    small, _, _ = build_rmat_graph(p, h, 10, weighted=True, transposed=False, mg=args.mg)
+    p.louvain(h, small, 100, 1.0, False)  # module load + allocator warm-up off the clock
+    del small
+    scale = args.louvain_scale
+    t0 = time.perf_counter()
+    g, _, _ = build_rmat_graph(p, h, scale, weighted=True, transposed=False, mg=args.mg)
+    build_s = time.perf_counter() - t0
+    V, E = g.number_of_vertices(), g.number_of_edges()
+    torch.cuda.synchronize()
+    barrier(args)
+    t0 = time.perf_counter()
+    _, _, q = p.louvain(h, g, 100, 1.0, False)
+    torch.cuda.synchronize()
+    barrier(args)
+    t = max_over_ranks(args, time.perf_counter() - t0)
+    return {"scale": scale, "vertices": V, "edges": E, "weights": "uniform [0,1) fp32, seed 43",
+            "time_s": t, "modularity": q, "levels": h.last_louvain_levels(), "graph_build_s": round(build_s, 3),
+            "n_gpus": args.world, "path": "sg" if args.world == 1 else f"mg{args.world} (RCCL)"}
+
+
 def barrier(args):
     if args.world > 1:
         import torch.distributed as dist
@@ -241,6 +269,9 @@ def main():
     ap.add_argument("--bfs", dest="bfs", action="store_true", default=True)
     ap.add_argument("--no-bfs", dest="bfs", action="store_false")
     ap.add_argument("--bfs-scale", type=int, default=None)
+    ap.add_argument("--louvain", dest="louvain", action="store_true", default=True)
+    ap.add_argument("--no-louvain", dest="louvain", action="store_false")
+    ap.add_argument("--louvain-scale", type=int, default=None, help="default 23 + log2(N): RMAT-26 at 8 GPUs")
     ap.add_argument("--row-comm-size", type=int, default=None, help="C of the R x C grid (default: R <= C)")
     ap.add_argument("--comm", choices=["rccl", "torch"], default="rccl",
                     help="MG collectives: RCCL inside libcugraph_c (default), or torch.distributed callbacks "
@@ -257,6 +288,8 @@ def main():
         args.scale = 22 + grow
     if args.bfs_scale is None:
         args.bfs_scale = 24  # BASELINE: BFS on RMAT-24 at 1/2/4/8 GPUs (fixed graph)
+    if args.louvain_scale is None:
+        args.louvain_scale = 23 + grow  # BASELINE configs[4]: RMAT-26 Louvain on 8 GPUs
     args.world, args.rank = world, rank
     args.mg = (rank, world) if world > 1 else None
 
@@ -348,6 +381,14 @@ def main():
             out["bfs"] = bfs_leg(p, args)
         except Exception as e:  # noqa: BLE001
             out["bfs"] = {"status": "failed", "error": repr(e)[:300]}
+    if args.louvain:
+        try:
+            torch.cuda.empty_cache()
+            out["louvain"] = louvain_leg(p, args)
+            log(f"[bench] louvain: RMAT-{out['louvain']['scale']} {out['louvain']['time_s']:.3f}s "
+                f"Q={out['louvain']['modularity']:.6f} levels={out['louvain']['levels']}")
+        except Exception as e:  # noqa: BLE001
+            out["louvain"] = {"status": "failed", "error": repr(e)[:300]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1,0 +1,109 @@
+// Stream-ordered caching allocator for HBM (the role RMM's pool resource plays
+// under the reference, cpp/include/cugraph/... via rmm::mr::device_memory_resource).
+//
+// Blocks are rounded to size classes (4 per power of two, <= 25 % slack).  A
+// freed block is cached on the stream it was freed on; an allocation on the same
+// stream reuses a cached block of its class (or up to twice its class) with no
+// driver call and no synchronisation -- stream order already places the new
+// user's work after the old user's.  Blocks never move between streams.  When the
+// driver is out of memory the device is synchronised, every cached block is
+// returned, and the allocation is retried once.
+#include "common.hpp"
+
+#include <map>
+#include <mutex>
+#include <unordered_map>
+
+namespace cgx {
+
+namespace {
+
+struct cache_t {
+  std::mutex mu;
+  std::unordered_map<hipStream_t, std::multimap<size_t, void*>> free_blocks;
+  std::unordered_map<void*, size_t> live;  // block -> class size
+  size_t cached = 0;
+};
+
+cache_t& cache()
+{
+  static cache_t* c = new cache_t();  // never destroyed: frees may run during static teardown
+  return *c;
+}
+
+size_t size_class(size_t b)
+{
+  if (b <= 512) return 512;
+  int const e       = 63 - __builtin_clzll((unsigned long long)(b - 1));  // 2^e < b <= 2^(e+1)
+  size_t const step = (size_t)1 << (e >= 2 ? e - 2 : 0);
+  return (b + step - 1) / step * step;
+}
+
+size_t trim_locked(cache_t& c)
+{
+  if (c.cached == 0) return 0;
+  (void)hipDeviceSynchronize();
+  size_t freed = 0;
+  for (auto& kv : c.free_blocks)
+    for (auto& blk : kv.second) {
+      (void)hipFree(blk.second);
+      freed += blk.first;
+    }
+  c.free_blocks.clear();
+  c.cached = 0;
+  return freed;
+}
+
+}  // namespace
+
+void* device_alloc(size_t bytes, hipStream_t s)
+{
+  cache_t& c       = cache();
+  size_t const cls = size_class(bytes);
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.free_blocks.find(s);
+  if (it != c.free_blocks.end()) {
+    auto& m = it->second;
+    auto b  = m.lower_bound(cls);
+    if (b != m.end() && b->first <= 2 * cls) {
+      void* p = b->second;
+      c.live[p] = b->first;
+      c.cached -= b->first;
+      m.erase(b);
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, cls) != hipSuccess) {
+    (void)hipGetLastError();
+    trim_locked(c);
+    if (hipMalloc(&p, cls) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+  }
+  c.live[p] = cls;
+  return p;
+}
+
+void device_free(void* p, hipStream_t s)
+{
+  if (!p) return;
+  cache_t& c = cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.live.find(p);
+  if (it == c.live.end()) return;  // not ours
+  size_t const cls = it->second;
+  c.live.erase(it);
+  c.free_blocks[s].emplace(cls, p);
+  c.cached += cls;
+}
+
+size_t device_cache_trim()
+{
+  cache_t& c = cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  return trim_locked(c);
+}
+
+}  // namespace cgx

@@ -19,7 +19,7 @@ using namespace cgx;
 namespace {
 
 // Process-wide pool of handle streams.  A stream is never destroyed: memory
-// allocated on it with hipMallocAsync may be freed (stream-ordered) after the
+// cached on it by the caching allocator (alloc.cpp) may be freed after the
 // handle that owned it is gone.
 std::mutex g_stream_mutex;
 std::vector<std::pair<int, hipStream_t>> g_free_streams;
@@ -452,4 +452,5 @@ extern "C" size_t cugraph_amd_last_louvain_levels(const cugraph_resource_handle_
 {
   return H(handle)->last_louvain_levels;
 }
+extern "C" size_t cugraph_amd_trim_device_cache(void) { return cgx::device_cache_trim(); }
 extern "C" const char* cugraph_amd_version(void) { return "cugraph-forked_amd libcugraph_c gfx950 " __DATE__; }

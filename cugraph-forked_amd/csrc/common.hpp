@@ -66,8 +66,15 @@ constexpr data_type_id_t dtype_of()
 }
 
 // ---------------------------------------------------------------- device buffer
-// Stream-ordered HBM allocation (hipMallocAsync from the device's default pool,
-// release threshold raised at handle creation so freed blocks stay cached).
+// HBM blocks come from a stream-ordered caching allocator (alloc.cpp): a freed
+// block goes back to a per-stream cache and the next allocation of the same size
+// class on that stream takes it without a driver call.  (The reference runs on an
+// RMM pool for the same reason; hipFreeAsync of multi-GB blocks measured 250 ms
+// stalls per Louvain sweep on MI355X, see DESIGN.md.)
+void* device_alloc(size_t bytes, hipStream_t s);
+void device_free(void* p, hipStream_t s);
+size_t device_cache_trim();  // returns the cached bytes released
+
 class buffer {
  public:
   buffer() = default;
@@ -90,12 +97,10 @@ class buffer {
     release();
     bytes_ = bytes;
     if (bytes) {
-      hipError_t e = hipMallocAsync(&ptr_, bytes, stream_);
-      if (e != hipSuccess) {
-        ptr_   = nullptr;
+      ptr_ = device_alloc(bytes, stream_);
+      if (!ptr_) {
         bytes_ = 0;
-        fail(CUGRAPH_ALLOC_ERROR, std::string("hipMallocAsync failed: ") + hipGetErrorString(e) +
-                                    " (" + std::to_string(bytes) + " bytes)");
+        fail(CUGRAPH_ALLOC_ERROR, "device allocation failed (" + std::to_string(bytes) + " bytes)");
       }
     }
   }
@@ -105,11 +110,11 @@ class buffer {
   // outlive the handle that allocated it (graphs/results freed after their handle).
   void release()
   {
-    if (ptr_) { (void)hipFreeAsync(ptr_, stream_); }
+    if (ptr_) device_free(ptr_, stream_);
     ptr_   = nullptr;
     bytes_ = 0;
   }
-  // give up ownership (caller frees with hipFreeAsync/hipFree)
+  // give up ownership (caller frees with device_free)
   void* detach()
   {
     void* p = ptr_;

@@ -30,6 +30,9 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 
 namespace cgx {
@@ -454,6 +457,16 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
 
   std::vector<dbuf<uint32_t>> dendrogram;
   double best_q = -1.0;
+  bool const trace = std::getenv("CGX_LOUVAIN_TRACE") != nullptr;  // measurement only
+  auto t_last      = std::chrono::steady_clock::now();
+  auto lap         = [&](char const* what, int64_t nv, int64_t ne, double q) {
+    if (!trace) return;
+    auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[louvain] %-9s nv=%lld ne=%lld q=%.6f %.2f ms\n", what, (long long)nv, (long long)ne, q,
+                 std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
+  lap("start", cur.nv, cur.ne, 0.0);
   while (dendrogram.size() < max_level) {
     int64_t nv = cur.nv;
     dendrogram.emplace_back(std::max<int64_t>(nv, 1), s);
@@ -473,6 +486,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     dbuf<uint32_t> clusters(nv, s), next(nv, s);
     iota<uint32_t>(clusters.data(), nv, 0u, s);
     double new_q = modularity(S, cur, clusters.data(), a.data(), present.data());
+    lap("setup", nv, cur.ne, new_q);
     double cur_q = new_q - 1.0;
     bool up_down = true;
     while (new_q > cur_q + 0.0001) {
@@ -484,10 +498,12 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
       new_q   = modularity(S, cur, clusters.data(), a.data(), present.data());
       if (new_q > cur_q)
         HIP_CHECK(hipMemcpyAsync(level, clusters.data(), nv * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      lap("sweep", nv, cur.ne, new_q);
     }
     if (cur_q <= best_q) break;
     best_q = cur_q;
     cur    = contract(S, cur, level);
+    lap("contract", cur.nv, cur.ne, best_q);
   }
   // flatten_dendrogram (louvain_impl.cuh:239-255)
   dbuf<uint32_t> flat(nv0, s);

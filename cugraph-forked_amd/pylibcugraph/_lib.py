@@ -138,6 +138,7 @@ _proto("cugraph_amd_last_hot_kernel_launches", c_size_t, P)
 _proto("cugraph_amd_last_bfs_levels", c_size_t, P)
 _proto("cugraph_amd_last_bfs_bottom_up_steps", c_size_t, P)
 _proto("cugraph_amd_last_louvain_levels", c_size_t, P)
+_proto("cugraph_amd_trim_device_cache", c_size_t)
 _proto("cugraph_amd_version", ctypes.c_char_p)
 # multi-GPU communicator contexts (include/cugraph_amd/comm.h)
 _proto("cugraph_amd_comm_unique_id_size", c_size_t)

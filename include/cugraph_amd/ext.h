@@ -101,6 +101,11 @@ size_t cugraph_amd_heirarchical_clustering_result_get_num_levels(cugraph_heirarc
 cugraph_type_erased_device_array_view_t* cugraph_amd_heirarchical_clustering_result_get_level(
   cugraph_heirarchical_clustering_result_t* result, size_t level);
 
+/* Return every cached HBM block of libcugraph_c's caching allocator to the driver
+ * (synchronises the device).  Returns the bytes released.  The reference's
+ * equivalent is releasing its RMM pool. */
+size_t cugraph_amd_trim_device_cache(void);
+
 /* Library build string, e.g. "cugraph-forked_amd gfx950 <date>". */
 const char* cugraph_amd_version(void);
 
