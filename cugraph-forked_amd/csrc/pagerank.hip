@@ -299,8 +299,13 @@ constexpr int kWinBits     = 13;
 constexpr int kWin         = 1 << kWinBits;
 constexpr int kSrcBits     = 32 - kWinBits;  // 19
 constexpr int kXcds        = 8;   // MI355X XCDs (workgroups are dealt to them round-robin)
-constexpr int kXcdSegs     = 1;   // source segments of equal entry counts per XCD (8 measured 60% slower: all
-                                  // XCDs then flush the same windows at once; 1 = no split)
+#ifndef CGX_XCD_SEGS
+#define CGX_XCD_SEGS 1
+#endif
+// source segments of equal entry counts per XCD; 1 = no split.  8 measured 60%
+// slower (0.367 vs 0.229 ms/iteration on RMAT-22) even with the XCDs' starting
+// windows rotated apart, although each XCD's x~ slice then fits its L2.
+constexpr int kXcdSegs     = CGX_XCD_SEGS;
 constexpr int kPushThreads = 1024;
 constexpr int kPerThread   = 8;  // entries per thread per unit
 constexpr int kPushUnit    = kPerThread * kPushThreads;
@@ -394,7 +399,9 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
   int64_t u0, u1;
   if (kXcdSegs == kXcds && gridDim.x % kXcds == 0) {
     int const seg    = blockIdx.x % kXcds;
-    int64_t const lb = blockIdx.x / kXcds, nbx = gridDim.x / kXcds;
+    int64_t const nbx = gridDim.x / kXcds;
+    // rotate the XCDs' starting windows apart so they do not flush one window at once
+    int64_t const lb = (blockIdx.x / kXcds + seg * nbx / kXcds) % nbx;
     int64_t const a0 = sa.seg_start[seg], cnt = sa.seg_start[seg + 1] - a0;
     u0 = a0 + lb * cnt / nbx;
     u1 = a0 + (lb + 1) * cnt / nbx;
@@ -1094,8 +1101,100 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
   return *blk;
 }
 
+template <typename V>
+__global__ void k_pr_owner(V const* gid, int64_t n, int64_t const* voff, int P, int* dest)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dest[i] = mg_owner_of_global((int64_t)gid[i], voff, P);
+}
+
+template <typename V, typename R>
+__global__ void k_scatter_owned(V const* gid, R const* val, int64_t n, int64_t lo, double scale, R* owned)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    owned[(int64_t)gid[i] - lo] = (R)((double)val[i] * scale);
+}
+
+// user out-weights that are far below the graph's own would let a fixed-point sum
+// pass 2 (the push kernel's range); count them
+template <typename R>
+__global__ void k_count_small_outw(R const* given, R const* actual, int64_t n, int* bad)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (given[i] > R(0) && (double)actual[i] > 1.5 * (double)given[i]) atomicAdd(bad, 1);
+}
+
+struct mg_pairs_info {
+  double sum        = 0;  // over every rank's values
+  int64_t count     = 0;
+  int64_t negatives = 0;
+};
+
+// (external id, value) pairs given on any rank -> a dense array over this rank's
+// owned vertices, value * scale(sum) where given and 0 elsewhere (the reference
+// shuffles such pairs to their owners, c_api/pagerank.cpp:115-170 MG branch).
+// Collective; errors are raised on every rank alike.
+template <typename V, typename R, typename Scale>
+mg_pairs_info mg_pairs_to_owned(handle_t& h, graph_t& g, array_view_t const* vv, array_view_t const* vs, R* owned,
+                                Scale scale_of)
+{
+  hipStream_t s  = h.stream;
+  mg_graph_t& mg = *g.mg;
+  comm_t& comm   = *h.mg->world;
+  int const P    = mg.P;
+  size_t const n = vv ? vv->size : 0;
+  int64_t const n_own = mg.n_own(), lo = mg.voff[mg.p];
+  if (n_own) fill<R>(owned, n_own, R(0), s);
+  dbuf<V> ids(std::max<size_t>(n, 1), s);
+  dbuf<R> vals(std::max<size_t>(n, 1), s);
+  if (n) {
+    HIP_CHECK(hipMemcpyAsync(ids.data(), vv->data, n * sizeof(V), hipMemcpyDeviceToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(vals.data(), vs->data, n * sizeof(R), hipMemcpyDeviceToDevice, s));
+  }
+  mg_ext_to_global(h, g, ids.data(), n, /*check=*/true);
+  mg_pairs_info info;
+  double lsum  = 0;
+  int64_t lneg = 0;
+  for (auto x : to_host(vals.data(), n, s)) {
+    lsum += (double)x;
+    lneg += x < R(0) ? 1 : 0;
+  }
+  info.sum       = comm.host_allreduce<double>(lsum, CGX_COMM_SUM, s);
+  info.count     = comm.host_allreduce<int64_t>((int64_t)n, CGX_COMM_SUM, s);
+  info.negatives = comm.host_allreduce<int64_t>(lneg, CGX_COMM_SUM, s);
+  double const scale = scale_of(info);
+  // to the owners: sort by owner, exchange, scatter
+  dbuf<int64_t> voff_d(P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  dbuf<int> dest(std::max<size_t>(n, 1), s), d2(std::max<size_t>(n, 1), s);
+  dbuf<int64_t> iv(std::max<size_t>(n, 1), s), perm(std::max<size_t>(n, 1), s);
+  dbuf<V> sid(std::max<size_t>(n, 1), s);
+  dbuf<R> sval(std::max<size_t>(n, 1), s);
+  std::vector<size_t> counts(P, 0), rc;
+  if (n) {
+    hipLaunchKernelGGL(k_pr_owner<V>, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, ids.data(), (int64_t)n,
+                       voff_d.data(), P, dest.data());
+    CGX_LAUNCH_CHECK();
+    iota<int64_t>(iv.data(), n, 0, s);
+    radix_sort_pairs<int, int64_t>(dest.data(), d2.data(), iv.data(), perm.data(), n, 0, bits_for(P), s);
+    gather<V, int64_t>(sid.data(), ids.data(), perm.data(), n, s);
+    gather<R, int64_t>(sval.data(), vals.data(), perm.data(), n, s);
+    for (int q : to_host(d2.data(), n, s)) counts[q]++;
+  }
+  auto rid  = exchange<V>(comm, sid.data(), counts, rc, s);
+  auto rval = exchange<R>(comm, sval.data(), counts, rc, s);
+  if (rid.n)
+    hipLaunchKernelGGL((k_scatter_owned<V, R>), dim3(grid_for(rid.n, kBlock, 4096)), dim3(kBlock), 0, s, rid.data(),
+                       rval.data(), (int64_t)rid.n, lo, scale, owned);
+  CGX_LAUNCH_CHECK();
+  return info;
+}
+
 template <typename V, typename E, typename R>
-void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t max_iter, centrality_result_t& res)
+void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view_t const* pow_s,
+                      array_view_t const* guess_v, array_view_t const* guess_s, array_view_t const* pers_v,
+                      array_view_t const* pers_s, double alpha, double eps, size_t max_iter, bool expensive,
+                      centrality_result_t& res)
 {
   hipStream_t s   = h.stream;
   mg_context& ctx = *h.mg;
@@ -1114,9 +1213,55 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t 
   if (g.num_vertices == 0) return;
   mg_pr_block& blk = mg_block<V, E, R>(h, g);
   int const C = mg.C, R_ = mg.R;
+  int64_t const n1 = std::max<int64_t>(n_own, 1);
+  auto unit  = [](mg_pairs_info const&) { return 1.0; };
+  auto prob  = [](mg_pairs_info const& i) { return i.sum > 0.0 ? 1.0 / i.sum : 0.0; };
+
+  // precomputed out-weight sums (pagerank_impl.cuh:64-87)
+  dbuf<R> outw_user;
+  R const* outw = blk.outw.data<R>();
+  if (pow_v) {
+    outw_user.resize(n1, s);
+    auto info = mg_pairs_to_owned<V, R>(h, g, pow_v, pow_s, outw_user.data(), unit);
+    CGX_INPUT(!expensive || info.negatives == 0,
+              "Invalid input argument: outgoing edge weight sum values should be non-negative.");
+    dbuf<int> bad(1, s);
+    fill<int>(bad.data(), 1, 0, s);
+    if (n_own)
+      hipLaunchKernelGGL(k_count_small_outw<R>, dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s,
+                         outw_user.data(), blk.outw.data<R>(), n_own, bad.data());
+    CGX_LAUNCH_CHECK();
+    int64_t nbad = ctx.world->host_allreduce<int64_t>((int64_t)to_host_scalar(bad.data(), s), CGX_COMM_SUM, s);
+    CGX_EXPECTS(nbad == 0, CUGRAPH_NOT_IMPLEMENTED,
+                "multi-GPU PageRank: precomputed out-weight sums below 2/3 of the graph's own are not supported");
+    outw = outw_user.data();
+  }
+  // personalisation coefficients value / sum(values)
+  dbuf<R> pers;
+  bool personalized = false;
+  if (pers_v || pers_s) {
+    CGX_INPUT(pers_v && pers_s && pers_v->size == pers_s->size,
+              "Invalid input argument: personalization vertices and values must be given together.");
+    pers.resize(n1, s);
+    auto info = mg_pairs_to_owned<V, R>(h, g, pers_v, pers_s, pers.data(), prob);
+    CGX_INPUT(!expensive || info.negatives == 0,
+              "Invalid input argument: peresonalization values should be non-negative.");
+    if (info.count > 0) {
+      CGX_INPUT(info.sum > 0.0, "Invalid input argument: sum of personalization valuese should be positive.");
+      personalized = true;
+    }
+  }
 
   R* pr = res.values->buf.data<R>();
-  fill<R>(pr, std::max<int64_t>(n_own, 0), (R)(R(1.0) / (R)g.num_vertices), s);
+  if (guess_v || guess_s) {  // initial guess, normalised to sum 1
+    CGX_INPUT(guess_v && guess_s, "Invalid input argument: initial guess vertices and values must be given together.");
+    auto info = mg_pairs_to_owned<V, R>(h, g, guess_v, guess_s, pr, prob);
+    CGX_INPUT(!expensive || info.negatives == 0,
+              "Invalid input argument: initial guess values should be non-negative.");
+    CGX_INPUT(info.sum > 0.0, "Invalid input argument: sum of the PageRank initial guess values should be positive.");
+  } else {
+    fill<R>(pr, std::max<int64_t>(n_own, 0), (R)(R(1.0) / (R)g.num_vertices), s);
+  }
   dbuf<R> x_send(std::max<int64_t>(blk.nmax_row, 1), s), x_row(std::max<int64_t>(C * blk.nmax_row, 1), s);
   fill<R>(x_send.data(), std::max<int64_t>(blk.nmax_row, 1), R(0), s);
   dbuf<unsigned long long> acc_own(std::max<int64_t>(blk.nmax_col, 1), s);
@@ -1127,7 +1272,8 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, double alpha, double eps, size_t 
 
   pr_args<V, E, R> a{};
   a.pr        = pr;
-  a.outw      = blk.outw.data<R>();
+  a.outw      = outw;
+  a.pers      = personalized ? pers.data() : nullptr;
   a.alpha     = alpha;
   a.eps       = eps;
   a.max_iter  = (int)std::min<size_t>(max_iter, (size_t)INT32_MAX);
@@ -1244,17 +1390,14 @@ void run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view
 namespace cgx {
 void mg_run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_view_t const* pow_s,
                      array_view_t const* guess_v, array_view_t const* guess_s, array_view_t const* pers_v,
-                     array_view_t const* pers_s, double alpha, double eps, size_t max_iter, bool /*expensive*/,
+                     array_view_t const* pers_s, double alpha, double eps, size_t max_iter, bool expensive,
                      centrality_result_t& res)
 {
   CGX_EXPECTS(h.mg != nullptr, CUGRAPH_INVALID_HANDLE, "multi-GPU graph used with a single-GPU resource handle");
-  CGX_EXPECTS(pow_v == nullptr && pow_s == nullptr && guess_v == nullptr && guess_s == nullptr &&
-                pers_v == nullptr && pers_s == nullptr,
-              CUGRAPH_NOT_IMPLEMENTED,
-              "multi-GPU PageRank: precomputed out-weights, initial guess and personalization are not supported yet");
   dispatch_vew(g.vertex_type, g.edge_type, g.weight_type, [&](auto t) {
     using T = decltype(t);
-    mg_pagerank_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(h, g, alpha, eps, max_iter, res);
+    mg_pagerank_impl<typename T::vertex_t, typename T::edge_t, typename T::weight_t>(
+      h, g, pow_v, pow_s, guess_v, guess_s, pers_v, pers_s, alpha, eps, max_iter, expensive, res);
   });
 }
 }  // namespace cgx

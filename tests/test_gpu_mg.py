@@ -231,3 +231,75 @@ def test_mg_louvain_levels_vs_oracle(world, C, integer):
 def test_mg_louvain_rccl_single_rank():
     import torch.multiprocessing as tmp
     tmp.spawn(_louvain_worker, args=(1, _free_port(), 1, 11, True, "rccl"), nprocs=1, join=True)
+
+
+def _pr_options_worker(rank, world, port, C):
+    """MG personalized PageRank with an initial guess and precomputed out-weight sums,
+    each (vertex, value) list split unevenly over the ranks (the reference shuffles
+    such pairs to their owners, c_api/pagerank.cpp MG branch), vs the oracle."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pylibcugraph as plc
+    from oracle import graph as og
+    from oracle import pagerank as opr
+
+    s, d, w = _graph(10, True)
+    w = w.astype(np.float32).astype(np.float64)
+    E = s.size
+    lo, hi = rank * E // world, (rank + 1) * E // world
+    ctx = plc.comms.init_torch(C)
+    h = plc.ResourceHandle(ctx.ptr)
+    dev = lambda a, t: torch.as_tensor(np.ascontiguousarray(a).astype(t), device="cuda")  # noqa: E731
+    G = plc.MGGraph(h, plc.GraphProperties(is_symmetric=True, is_multigraph=False), dev(s[lo:hi], np.int32),
+                    dev(d[lo:hi], np.int32), dev(w[lo:hi], np.float32), store_transposed=True, num_edges=E)
+    verts = np.unique(np.concatenate([s, d]))
+    outw = np.zeros(int(verts.max()) + 1)
+    np.add.at(outw, s, w)
+    rng = np.random.default_rng(3)
+    pv = rng.choice(verts, 40, replace=False)
+    pval = rng.random(40) + 0.1
+    gv = rng.choice(verts, 200, replace=False)
+    gval = rng.random(200) + 0.5
+    mine = lambda a: a[rank::world] if rank < world - 1 else a[rank::world][:3]  # noqa: E731
+    ow_v = verts if rank == 0 else verts[:0]  # all out-weights given by rank 0
+    v, x = plc.personalized_pagerank(
+        h, G, dev(ow_v, np.int32), dev(outw[ow_v], np.float32), dev(mine(gv), np.int32),
+        dev(mine(gval), np.float32), dev(mine(pv), np.int32), dev(mine(pval), np.float32), 0.85, 1e-6, 500, True)
+    res = (v.cpu().numpy(), x.cpu().numpy(), mine(pv), mine(pval), mine(gv), mine(gval))
+    allr = [None] * world
+    dist.all_gather_object(allr, res)
+    if rank == 0:
+        vv = np.concatenate([a[0] for a in allr])
+        xx = np.concatenate([a[1] for a in allr])
+        pv_all = np.concatenate([a[2] for a in allr])
+        pval_all = np.concatenate([a[3] for a in allr]).astype(np.float32).astype(np.float64)
+        g = og.create_graph(s, d, w, store_transposed=True, renumber=True)
+        inv = np.zeros(int(g.number_map.max()) + 1, dtype=np.int64)
+        inv[g.number_map] = np.arange(g.number_map.size)
+        guess = np.zeros(g.number_map.size)
+        guess[inv[np.concatenate([a[4] for a in allr])]] = np.concatenate([a[5] for a in allr]).astype(np.float32)
+        ref = opr.pagerank_from_graph(g, alpha=0.85, epsilon=1e-6, max_iterations=500, initial_guess=guess,
+                                      personalization_vertices=inv[pv_all], personalization_values=pval_all)
+        got = np.zeros(g.number_map.size)
+        got[inv[vv]] = xx
+        live = ref > 1e-9
+        rel = np.abs(got - ref)[live] / ref[live]
+        assert rel.max() < 1e-6, rel.max()
+    dist.barrier()
+    h = None
+    G = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C", [(2, 2), (3, 1)])
+def test_mg_personalized_pagerank_options(world, C):
+    import torch.multiprocessing as tmp
+    tmp.spawn(_pr_options_worker, args=(world, _free_port(), C), nprocs=world, join=True)
