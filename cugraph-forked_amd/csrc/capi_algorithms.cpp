@@ -34,6 +34,8 @@ void mg_run_pagerank(handle_t& h, graph_t& g, array_view_t const* pow_v, array_v
                      centrality_result_t& res);
 void mg_run_bfs(handle_t& h, graph_t& g, array_view_t* sources, bool direction_optimizing, size_t depth_limit,
                 bool compute_predecessors, bool expensive, paths_result_t& res);
+void mg_run_sssp(handle_t& h, graph_t& g, size_t source, double cutoff, bool compute_predecessors, bool expensive,
+                 paths_result_t& res);
 }  // namespace cgx
 
 namespace {
@@ -191,9 +193,9 @@ extern "C" cugraph_error_code_t cugraph_sssp(const cugraph_resource_handle_t* ha
     CGX_EXPECTS(handle != nullptr, CUGRAPH_INVALID_HANDLE, "invalid resource handle");
     CGX_INPUT(graph != nullptr, "Invalid input argument: graph is NULL");
     auto& g = *G(graph);
-    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED, "multi-GPU SSSP is not implemented in this build");
     auto res = std::make_unique<paths_result_t>();
-    run_sssp(*H(handle), g, source, cutoff, compute_predecessors == TRUE, do_expensive_check == TRUE, *res);
+    (g.multi_gpu ? mg_run_sssp : run_sssp)(*H(handle), g, source, cutoff, compute_predecessors == TRUE,
+                                           do_expensive_check == TRUE, *res);
     HIP_CHECK(hipStreamSynchronize(H(handle)->stream));
     *result = reinterpret_cast<cugraph_paths_result_t*>(res.release());
   });

@@ -34,9 +34,10 @@ struct mg_graph_t {
   // this rank's 2D block of edges (global ids), weights optional
   int64_t ne = 0;
   buffer src, dst, w;
-  // per-algorithm caches (pagerank.hip, mg_bfs.hip)
+  // per-algorithm caches (pagerank.hip, mg_bfs.hip, mg_sssp.hip)
   std::shared_ptr<void> pr_block;
   std::shared_ptr<void> bfs_rows;
+  std::shared_ptr<void> sssp_rows;  // weighted out-rows by source owner (mg_sssp.hip)
 };
 
 // owner of an external vertex id (hash), host and device

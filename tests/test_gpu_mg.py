@@ -303,3 +303,62 @@ def _pr_options_worker(rank, world, port, C):
 def test_mg_personalized_pagerank_options(world, C):
     import torch.multiprocessing as tmp
     tmp.spawn(_pr_options_worker, args=(world, _free_port(), C), nprocs=world, join=True)
+
+
+def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
+    """MG SSSP vs the oracle's fp32 min-plus fixed point: distances bit-identical,
+    predecessors = the tight in-neighbour with the smallest global id (the oracle's
+    tie_key set to the MG global order)."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pylibcugraph as plc
+    from oracle import graph as og
+    from oracle import rmat
+    from oracle import sssp as osssp
+
+    s, d = rmat.rmat(scale, 16 << scale, seed=11)
+    w = rmat.rmat_weights(s.size, seed=43).astype(np.float64)
+    s, d, w = og.symmetrize_dedup(s, d, w, symmetrize=symmetric)
+    E = s.size
+    lo, hi = rank * E // world, (rank + 1) * E // world
+    ctx = plc.comms.init_torch(C)
+    h = plc.ResourceHandle(ctx.ptr)
+    dev = lambda a, t: torch.as_tensor(np.ascontiguousarray(a).astype(t), device="cuda")  # noqa: E731
+    G = plc.MGGraph(h, plc.GraphProperties(is_symmetric=symmetric, is_multigraph=False), dev(s[lo:hi], np.int32),
+                    dev(d[lo:hi], np.int32), dev(w[lo:hi], np.float32), store_transposed=False, num_edges=E)
+    src = int(s[0])
+    v, dd, pp = plc.sssp(h, G, src, cutoff, True, True)
+    allr = [None] * world
+    dist.all_gather_object(allr, (v.cpu().numpy(), dd.cpu().numpy(), pp.cpu().numpy()))
+    if rank == 0:
+        vv = np.concatenate([a[0] for a in allr])  # global id order
+        dv = np.concatenate([a[1] for a in allr])
+        pv = np.concatenate([a[2] for a in allr])
+        n_ext = int(max(s.max(), d.max())) + 1
+        G2 = og.create_graph(s, d, w.astype(np.float32), renumber=False, vertices=np.arange(n_ext))
+        key = np.empty(n_ext, np.int64)  # a permutation: graph vertices in global order, then absent ids
+        key[vv] = np.arange(vv.size)
+        absent = np.setdiff1d(np.arange(n_ext), vv)
+        key[absent] = vv.size + np.arange(absent.size)
+        rd, rp = osssp.sssp(n_ext, G2.offsets, G2.indices, G2.weights, src, cutoff=cutoff, tie_key=key)
+        assert np.array_equal(dv, rd[vv])
+        assert np.array_equal(pv, rp[vv])
+    dist.barrier()
+    h = None
+    G = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C,symmetric,cutoff", [(2, 2, True, np.inf), (3, 3, False, np.inf),
+                                                       (4, 2, True, 0.05)])
+def test_mg_sssp_vs_oracle(world, C, symmetric, cutoff):
+    import torch.multiprocessing as tmp
+    tmp.spawn(_sssp_worker, args=(world, _free_port(), C, 11, symmetric, float(cutoff)), nprocs=world, join=True)
