@@ -174,7 +174,7 @@ def bfs_leg(p, args):
     if deg is None:  # SG: degrees from the CSR (internal order == result order)
         off, _, _ = g.adjacency(h, transposed=False)
         deg_int = (off[1:] - off[:-1]).to(torch.int64)
-    rates, levels, bu, times = [], [], [], []
+    rates, stored, levels, bu, times = [], [], [], [], []
     for r in roots:
         mine = [int(r)] if args.rank == 0 else []
         src = torch.tensor(mine, dtype=torch.int32, device="cuda")
@@ -196,9 +196,12 @@ def bfs_leg(p, args):
         levels.append(h.last_bfs_levels())
         bu.append(h.last_bfs_bottom_up_steps())
         rates.append((e_cc / 2) / t / 1e6)
+        stored.append(e_cc / t / 1e6)
     hm = len(rates) / sum(1.0 / m for m in rates)
+    hm_stored = len(stored) / sum(1.0 / m for m in stored)
     return {"scale": scale, "vertices": V, "edges": E, "roots": len(rates),
             "mteps_harmonic_mean": hm, "mteps_min": min(rates), "mteps_max": max(rates),
+            "stored_edge_mteps_harmonic_mean": hm_stored,
             "ms_mean": 1e3 * sum(times) / len(times), "levels": levels, "bottom_up_steps": bu,
             "direction_optimizing": True, "n_gpus": args.world,
             "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)"}
@@ -227,7 +230,27 @@ def louvain_leg(p, args):
     t = max_over_ranks(args, time.perf_counter() - t0)
     return {"scale": scale, "vertices": V, "edges": E, "weights": "uniform [0,1) fp32, seed 43",
             "time_s": t, "modularity": q, "levels": h.last_louvain_levels(), "graph_build_s": round(build_s, 3),
-            "n_gpus": args.world, "path": "sg" if args.world == 1 else f"mg{args.world} (RCCL)"}
+            "n_gpus": args.world,
+            "path": "sg" if args.world == 1 else f"mg{args.world} ({'RCCL' if args.comm == 'rccl' else 'torch'})"}
+
+
+def stream_copy_gbs(nbytes=4 << 30, reps=10):
+    """Measured HBM ceiling: device-to-device copy of a 4 GiB buffer,
+    read + write bytes / time, HIP events."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
 
 
 def barrier(args):
@@ -358,6 +381,14 @@ def main():
             "avg_kernel_ms": r["avg_ms"],
         },
     }
+    if world > 1:  # MG comm bytes per rank and iteration (x~ allgather + u64 sums reduce-scatter)
+        C = args.ctx.row_comm_size
+        Rr = world // C
+        out["roofline"]["comm_bytes_per_rank_iter"] = ((C - 1) * r["V"] / world * 4 + (Rr - 1) * r["V"] / world * 8)
+    try:
+        out["roofline"]["stream_copy_gbs"] = stream_copy_gbs()
+    except Exception as e:  # noqa: BLE001
+        out["roofline"]["stream_copy_gbs"] = f"unavailable: {e!r}"[:200]
     # (no nested profiler: a bench already running under rocprofv3 skips the traffic passes)
     under_prof = any(k.startswith("ROCPROF_") for k in os.environ)
     if rank == 0 and world == 1 and not args.no_traffic and not under_prof:
