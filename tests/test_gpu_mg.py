@@ -1,5 +1,5 @@
-"""Multi-GPU path (cugraph_mg_graph_create + MG PageRank / BFS) on ONE MI355X: 2 or
-4 ranks share cuda:0 and talk through torch.distributed/gloo callbacks
+"""Multi-GPU path (cugraph_mg_graph_create + MG PageRank / BFS / SSSP / Louvain) on ONE
+MI355X: 1-4 ranks share cuda:0 and talk through torch.distributed/gloo callbacks
 (pylibcugraph.comms.init_torch) -- RCCL refuses two ranks per GPU.  The 2D
 partition, the id routing and the per-iteration collectives are the same code as
 with RCCL; results are checked against the single-GPU oracle."""
@@ -20,6 +20,16 @@ def _free_port():
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def _slice(rank, world, E):
+    """This rank's slice of the edge list.  CGX_TEST_SKEW=1: rank 0 passes no edges
+    at all and the others split the list (ranks whose input is empty)."""
+    if os.environ.get("CGX_TEST_SKEW") and world > 1:
+        if rank == 0:
+            return 0, 0
+        return (rank - 1) * E // (world - 1), rank * E // (world - 1)
+    return rank * E // world, (rank + 1) * E // world
 
 
 def _graph(scale, weighted, seed=5):
@@ -48,7 +58,7 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
 
     s, d, w = _graph(scale, weighted)
     E = s.size
-    lo, hi = rank * E // world, (rank + 1) * E // world
+    lo, hi = _slice(rank, world, E)
     ctx = plc.comms.init_torch(C) if comm == "torch" else plc.comms.init_rccl(C)
     h = plc.ResourceHandle(ctx.ptr)
     assert h.get_rank() == rank
@@ -159,7 +169,7 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     s, d, w = og.symmetrize_dedup(s, d, w)
     w = w.astype(np.float32).astype(np.float64)
     E = s.size
-    lo, hi = rank * E // world, (rank + 1) * E // world
+    lo, hi = _slice(rank, world, E)
     ctx = plc.comms.init_torch(C) if comm == "torch" else plc.comms.init_rccl(C)
     h = plc.ResourceHandle(ctx.ptr)
     st = torch.as_tensor(s[lo:hi].astype(np.int32), device="cuda")
@@ -253,7 +263,7 @@ def _pr_options_worker(rank, world, port, C):
     s, d, w = _graph(10, True)
     w = w.astype(np.float32).astype(np.float64)
     E = s.size
-    lo, hi = rank * E // world, (rank + 1) * E // world
+    lo, hi = _slice(rank, world, E)
     ctx = plc.comms.init_torch(C)
     h = plc.ResourceHandle(ctx.ptr)
     dev = lambda a, t: torch.as_tensor(np.ascontiguousarray(a).astype(t), device="cuda")  # noqa: E731
@@ -327,7 +337,7 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
     w = rmat.rmat_weights(s.size, seed=43).astype(np.float64)
     s, d, w = og.symmetrize_dedup(s, d, w, symmetrize=symmetric)
     E = s.size
-    lo, hi = rank * E // world, (rank + 1) * E // world
+    lo, hi = _slice(rank, world, E)
     ctx = plc.comms.init_torch(C)
     h = plc.ResourceHandle(ctx.ptr)
     dev = lambda a, t: torch.as_tensor(np.ascontiguousarray(a).astype(t), device="cuda")  # noqa: E731
@@ -362,3 +372,17 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
 def test_mg_sssp_vs_oracle(world, C, symmetric, cutoff):
     import torch.multiprocessing as tmp
     tmp.spawn(_sssp_worker, args=(world, _free_port(), C, 11, symmetric, float(cutoff)), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("algo", ["pagerank", "bfs_do", "louvain", "sssp"])
+def test_mg_rank_without_edges(algo, monkeypatch):
+    """Rank 0 contributes no edges to cugraph_mg_graph_create (it still owns vertices)."""
+    import torch.multiprocessing as tmp
+    monkeypatch.setenv("CGX_TEST_SKEW", "1")
+    port = _free_port()
+    if algo == "louvain":
+        tmp.spawn(_louvain_worker, args=(3, port, 3, 10, True), nprocs=3, join=True)
+    elif algo == "sssp":
+        tmp.spawn(_sssp_worker, args=(3, port, 3, 10, True, float("inf")), nprocs=3, join=True)
+    else:
+        tmp.spawn(_worker, args=(3, port, 3, 10, False, algo), nprocs=3, join=True)
