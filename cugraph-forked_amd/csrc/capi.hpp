@@ -77,6 +77,9 @@ struct pr_push_t {
   std::vector<int64_t> seg_start;  // first unit of every source segment (+ end)
   buffer acc;          // u64[nacc] fixed-point sums, zero between iterations
   int64_t nacc = 0;
+  buffer tiles;        // int64[ntiles + 1]: first unit of every (source segment, window) tile
+  int64_t ntiles = 0;
+  buffer tile_ctr;     // uint32: the push kernel's tile queue head, zero between iterations
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

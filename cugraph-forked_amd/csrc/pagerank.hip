@@ -302,13 +302,19 @@ constexpr int kXcds        = 8;   // MI355X XCDs (workgroups are dealt to them r
 #ifndef CGX_XCD_SEGS
 #define CGX_XCD_SEGS 1
 #endif
-// source segments of equal entry counts per XCD; 1 = no split.  8 measured 60%
-// slower (0.367 vs 0.229 ms/iteration on RMAT-22) even with the XCDs' starting
-// windows rotated apart, although each XCD's x~ slice then fits its L2.
+// Source segments of equal entry counts (1 = none).  Measured on RMAT-22, ms per
+// iteration: 8 segments pinned to the 8 XCDs (static kernel, each XCD's x~ slice
+// fits its L2) 0.367; 8 segments taken segment-major from the tile queue (the
+// blocks running at once share one or two slices) 0.27; no segments 0.221.  The
+// x~ misses these save cost less than the extra flushes and partial units.
 constexpr int kXcdSegs     = CGX_XCD_SEGS;
 constexpr int kPushThreads = 1024;
 constexpr int kPerThread   = 8;  // entries per thread per unit
 constexpr int kPushUnit    = kPerThread * kPushThreads;
+#ifndef CGX_TILE_UNITS
+#define CGX_TILE_UNITS 8  // 8: 0.221, 16: 0.222, 32: 0.229, 64: 0.241 ms/iteration (RMAT-22)
+#endif
+constexpr int kTileUnits   = CGX_TILE_UNITS;  // units per queue tile at most (one LDS flush per tile)
 constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
 constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 
@@ -329,6 +335,9 @@ struct push_args {
   int64_t seg_start[kXcdSegs + 1];  // first unit of every source segment
   unsigned long long* acc;  // [nwin * kWin] fixed-point sums, zero between iterations
   int ablate;  // measurement only (CGX_PR_ABLATE): 1 no gathers, 2 no LDS atomics, 4 no push, 8 no flush
+  int64_t const* tiles;     // first unit of every (segment, window) tile, ntiles + 1 entries
+  int64_t ntiles;
+  unsigned int* tile_ctr;   // queue head (k_pr_apply resets it)
 };
 
 template <typename T>
@@ -487,6 +496,11 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_enc(push_args<V, E, R>
   int win      = units[u0].win;
 #pragma unroll
   for (int j = 0; j < kPerThread; ++j) ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent is padded
+  // Branch-free body: every lane loads (masked lanes read x~[base] and add 0), and
+  // the next unit's entries are always fetched (the last unit re-reads itself), so
+  // the waits the compiler places are "gathers done" (vmcnt = the 8 prefetches still
+  // in flight) and "prefetch done" -- not a full drain before every gather, which
+  // any per-lane branch around a load produces.
   for (int64_t un = u0; un < u1; ++un) {
     if (win != cur) {
       flush_window<V, E, R>(sa, acc, cur);
@@ -494,40 +508,112 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_enc(push_args<V, E, R>
     }
     uint32_t const* xb = xe + base;
     uint32_t xw[kPerThread];
-    if (n == kPushUnit) {
 #pragma unroll
-      for (int j = 0; j < kPerThread; ++j) xw[j] = xb[ent[j] >> kWinBits];
-    } else {
-#pragma unroll
-      for (int j = 0; j < kPerThread; ++j) xw[j] = j * kPushThreads + tid < n ? xb[ent[j] >> kWinBits] : 0u;
+    for (int j = 0; j < kPerThread; ++j) {
+      bool const ok = j * kPushThreads + tid < n;
+      xw[j]         = xb[ok ? (ent[j] >> kWinBits) : 0u];
+      xw[j]         = ok ? xw[j] : 0u;
     }
+    int64_t const nx  = un + 1 < u1 ? un + 1 : un;
+    int64_t const k0n = units[nx].k0;
+    int const nn      = (int)(units[nx].k1 - k0n);
+    int64_t const bsn = units[nx].base;
+    int const winn    = units[nx].win;
     uint32_t ent_n[kPerThread];
-    int64_t k0n = 0, basen = 0;
-    int nn = 0, winn = 0;
-    if (un + 1 < u1) {
-      k0n   = units[un + 1].k0;
-      nn    = (int)(units[un + 1].k1 - k0n);
-      basen = units[un + 1].base;
-      winn  = units[un + 1].win;
 #pragma unroll
-      for (int j = 0; j < kPerThread; ++j) ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
-    }
+    for (int j = 0; j < kPerThread; ++j) ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
 #pragma unroll
     for (int j = 0; j < kPerThread; ++j) atomicAdd(&acc[ent[j] & (kWin - 1)], decode_fixed(xw[j]));
 #pragma unroll
     for (int j = 0; j < kPerThread; ++j) ent[j] = ent_n[j];
-    k0   = k0n;
     n    = nn;
-    base = basen;
+    base = bsn;
     win  = winn;
   }
   flush_window<V, E, R>(sa, acc, cur);
+}
+
+// The push (default): persistent blocks take tiles -- runs of at most kTileUnits
+// units of one (source segment, window) -- from a queue in unit order.  A tile's
+// units are summed into the LDS window and flushed once.  The queue balances the
+// unequal cost of units (hub-source units gather from few lines, tail units from
+// many), which a static split cannot (0.221 vs 0.227 ms/iteration).  The unit body is
+// branch-free (masked lanes load x~[base] and add 0; the next unit of the tile is
+// always prefetched, the last re-reading itself), so the only waits are "gathers
+// done" and "prefetch done".
+template <typename V, typename E, typename R, bool WEIGHTED>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push_q(push_args<V, E, R> sa)
+{
+  __shared__ unsigned long long acc[kWin];
+  __shared__ int s_tile;
+  if (sa.a.st->done) return;
+  int const tid = threadIdx.x;
+  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
+  using cunit_t        = __attribute__((address_space(4))) push_unit const;
+  cunit_t* const units = (cunit_t*)sa.units;  // read-only here: scalar loads
+  R const* const x     = sa.a.x_in;
+  while (true) {
+    if (tid == 0) s_tile = (int)atomicAdd(sa.tile_ctr, 1u);
+    __syncthreads();
+    int64_t const t = s_tile;
+    if (t >= sa.ntiles) break;  // uniform
+    int64_t const ua = sa.tiles[t], ub = sa.tiles[t + 1];
+    int64_t const win = units[ua].win;
+    int64_t k0   = units[ua].k0;
+    int n        = (int)(units[ua].k1 - k0);
+    int64_t base = units[ua].base;
+    uint32_t ent[kPerThread];
+    R w[kPerThread];
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+      ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent (and ew) are padded by a unit
+      if constexpr (WEIGHTED) w[j] = nt_load(sa.ew + k0 + j * kPushThreads + tid);
+    }
+    for (int64_t un = ua; un < ub; ++un) {
+      R const* const xb = x + base;
+      R xv[kPerThread];
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        bool const ok = j * kPushThreads + tid < n;
+        xv[j]         = xb[ok ? (ent[j] >> kWinBits) : 0u];
+        xv[j]         = ok ? xv[j] : R(0);
+      }
+      int64_t const nx  = un + 1 < ub ? un + 1 : un;
+      int64_t const k0n = units[nx].k0;
+      int const nn      = (int)(units[nx].k1 - k0n);
+      int64_t const bsn = units[nx].base;
+      uint32_t ent_n[kPerThread];
+      R w_n[kPerThread];
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
+        if constexpr (WEIGHTED) w_n[j] = nt_load(sa.ew + k0n + j * kPushThreads + tid);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        double v = (double)xv[j];
+        if constexpr (WEIGHTED) v *= (double)w[j];
+        atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
+      }
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        ent[j] = ent_n[j];
+        if constexpr (WEIGHTED) w[j] = w_n[j];
+      }
+      n    = nn;
+      base = bsn;
+    }
+    flush_window<V, E, R>(sa, acc, win);  // ends with a barrier: s_tile may be rewritten
+  }
 }
 
 template <typename V, typename E, typename R, bool ENC = false>
 __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 {
   auto const& a = sa.a;
+  if (sa.tile_ctr && blockIdx.x == 0 && threadIdx.x == 0) *sa.tile_ctr = 0u;  // the push has finished
   if (a.st->done) return;
   double const base = a.st->base;
   double const pf   = a.st->pers_factor;
@@ -697,8 +783,12 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.ent.resize((ne + kPushUnit) * sizeof(uint32_t));  // padded: k_pr_push_enc loads whole units
   HIP_CHECK(hipMemsetAsync(pp.ent.data<uint32_t>() + ne, 0, kPushUnit * sizeof(uint32_t), s));
   pp.ew.set_stream(s);
-  if (w) pp.ew.resize(ne * sizeof(R));
-  else pp.ew.release();
+  if (w) {
+    pp.ew.resize((ne + kPushUnit) * sizeof(R));  // padded like ent
+    HIP_CHECK(hipMemsetAsync(pp.ew.data<R>() + ne, 0, kPushUnit * sizeof(R), s));
+  } else {
+    pp.ew.release();
+  }
   pp.units.set_stream(s);
   pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
   hipLaunchKernelGGL(k_push_pack<R>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
@@ -715,6 +805,22 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     CGX_LAUNCH_CHECK();
     pp.seg_start = to_host(st.data(), kXcdSegs + 1, s);
   }
+  {  // (segment, window) tiles: runs of units, in unit (= queue) order
+    auto hu = to_host(pp.units.data<push_unit>(), nunits, s);
+    std::vector<int64_t> tiles;
+    // hub windows hold millions of entries: a tile is at most kTileUnits units
+    for (int64_t u = 0; u < nunits; ++u)
+      if (u == 0 || hu[u].win != hu[u - 1].win || hu[u].seg != hu[u - 1].seg || u - tiles.back() >= kTileUnits)
+        tiles.push_back(u);
+    tiles.push_back(nunits);
+    pp.ntiles = (int64_t)tiles.size() - 1;
+    pp.tiles.set_stream(s);
+    pp.tiles.resize(tiles.size() * sizeof(int64_t));
+    to_device(pp.tiles.data<int64_t>(), tiles.data(), tiles.size(), s);
+  }
+  pp.tile_ctr.set_stream(s);
+  pp.tile_ctr.resize(sizeof(unsigned int));
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, sizeof(unsigned int), s));
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -783,6 +889,27 @@ bool use_encoded_push(bool weighted)
   if (weighted || !std::is_same_v<R, float>) return false;
   char const* e = std::getenv("CGX_PR_PUSH");
   return e && std::string(e) == "enc";
+}
+
+// Push kernel choice: the tile queue (k_pr_push_q, default); CGX_PR_PUSH=static
+// the statically split k_pr_push; CGX_PR_PUSH=enc the static encoded-x~ kernel
+// (unweighted fp32 only).  All give the same bits (integer sums).
+enum { kPushQueue = 0, kPushStatic = 1, kPushEnc = 2 };
+template <typename R>
+int push_mode(bool weighted)
+{
+  if (use_encoded_push<R>(weighted)) return kPushEnc;
+  char const* e = std::getenv("CGX_PR_PUSH");
+  return e && std::string(e) == "static" ? kPushStatic : kPushQueue;
+}
+
+template <typename V, typename E, typename R>
+void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
+{
+  sa.tiles    = pp.tiles.data<int64_t>();
+  sa.ntiles   = pp.ntiles;
+  sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
+  if (sa.tile_ctr) HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, sizeof(unsigned int), s));
 }
 
 template <typename V, typename E, typename R>
@@ -908,10 +1035,12 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   push = push && adj.pr.ok;
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  bool const enc = push && use_encoded_push<R>(g.weighted);
-  auto pkernel   = g.weighted ? k_pr_push<V, E, R, true>
-                   : enc      ? k_pr_push_enc<V, E, R>
-                              : k_pr_push<V, E, R, false>;
+  int const pmode = push_mode<R>(g.weighted);
+  bool const enc  = push && pmode == kPushEnc;
+  auto pkernel    = pmode == kPushQueue ? (g.weighted ? k_pr_push_q<V, E, R, true> : k_pr_push_q<V, E, R, false>)
+                    : g.weighted        ? k_pr_push<V, E, R, true>
+                    : enc               ? k_pr_push_enc<V, E, R>
+                                        : k_pr_push<V, E, R, false>;
   auto akernel   = enc ? k_pr_apply<V, E, R, true> : k_pr_apply<V, E, R, false>;
   if (push) {
     sa.ent    = adj.pr.ent.data<uint32_t>();
@@ -925,7 +1054,9 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       hipLaunchKernelGGL((k_encode_x<R>), dim3(grid_for(nv, kBlock, 4096)), dim3(kBlock), 0, s, xa.data(), nv);
       CGX_LAUNCH_CHECK();
     }
-    nblk_push  = (int)std::min<int64_t>(sa.nunits, 256 * 2);  // 64 KB LDS: two blocks per CU
+    set_queue_args(sa, adj.pr, s);
+    // 64 KB LDS: two blocks per CU
+    nblk_push  = (int)std::min<int64_t>(pmode == kPushQueue ? sa.ntiles : sa.nunits, 256 * 2);
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
   // chunked enqueue; profiling records HIP events around every iteration launch
@@ -1300,14 +1431,16 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   sp.nunits = blk.pp.nunits;
   for (int i = 0; i <= kXcdSegs; ++i) sp.seg_start[i] = i < (int)blk.pp.seg_start.size() ? blk.pp.seg_start[i] : 0;
   sp.acc    = blk.pp.acc.data<unsigned long long>();
-  bool const enc = use_encoded_push<R>(g.weighted);
+  int const pmode = push_mode<R>(g.weighted);
+  bool const enc  = pmode == kPushEnc;
+  set_queue_args(sp, blk.pp, s);
   if (enc && n_own > 0) {  // x~ of the init pass -> encoded words before the first allgather
     hipLaunchKernelGGL((k_encode_x<R>), dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s, x_send.data(), n_own);
     CGX_LAUNCH_CHECK();
   }
   sap       = sp;
   sap.acc   = acc_own.data();
-  int const nblk_push  = (int)std::min<int64_t>(sp.nunits, 256 * 2);
+  int const nblk_push  = (int)std::min<int64_t>(pmode == kPushQueue ? sp.ntiles : sp.nunits, 256 * 2);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
 
@@ -1329,9 +1462,10 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
         }
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
         if (nblk_push)
-          hipLaunchKernelGGL((g.weighted ? k_pr_push<V, E, R, true>
-                              : enc      ? k_pr_push_enc<V, E, R>
-                                         : k_pr_push<V, E, R, false>),
+          hipLaunchKernelGGL((pmode == kPushQueue ? (g.weighted ? k_pr_push_q<V, E, R, true> : k_pr_push_q<V, E, R, false>)
+                              : g.weighted        ? k_pr_push<V, E, R, true>
+                              : enc               ? k_pr_push_enc<V, E, R>
+                                                  : k_pr_push<V, E, R, false>),
                              dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
         CGX_LAUNCH_CHECK();
         ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);

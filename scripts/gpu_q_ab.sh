@@ -1,0 +1,7 @@
+set -o pipefail
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pagerank.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pt_pr.log 2>&1; rc=$?; tail -2 gpurun_out/pt_pr.log; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do
+  timeout -k 10 120 python bench.py --steps 10 --warmup 2 --epsilon 1e9 --no-cpu-baseline --no-bfs --no-louvain --no-traffic 2>&1 | grep "\[bench\] pagerank" | sed "s/^/queue8 /" || exit 1
+  CUGRAPH_AMD_LIB=scripts/variants/seg1.so CGX_PR_PUSH=static timeout -k 10 120 python bench.py --steps 10 --warmup 2 --epsilon 1e9 --no-cpu-baseline --no-bfs --no-louvain --no-traffic 2>&1 | grep "\[bench\] pagerank" | sed "s/^/static1 /" || exit 1
+  CUGRAPH_AMD_LIB=scripts/variants/seg1.so timeout -k 10 120 python bench.py --steps 10 --warmup 2 --epsilon 1e9 --no-cpu-baseline --no-bfs --no-louvain --no-traffic 2>&1 | grep "\[bench\] pagerank" | sed "s/^/queue1 /" || exit 1
+done
