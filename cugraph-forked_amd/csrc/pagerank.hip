@@ -1439,7 +1439,10 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
     CGX_LAUNCH_CHECK();
   }
   sap       = sp;
-  sap.acc   = acc_own.data();
+  // one grid row (R = 1): the block's sums are already the owner's; the apply reads
+  // and re-zeroes them in place, no column collective
+  bool const col_reduce = R_ > 1;
+  sap.acc   = col_reduce ? acc_own.data() : sp.acc;
   int const nblk_push  = (int)std::min<int64_t>(pmode == kPushQueue ? sp.ntiles : sp.nunits, 256 * 2);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
@@ -1468,8 +1471,10 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
                                                   : k_pr_push<V, E, R, false>),
                              dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
         CGX_LAUNCH_CHECK();
-        ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
-        if (block_acc_bytes) HIP_CHECK(hipMemsetAsync(sp.acc, 0, block_acc_bytes, s));
+        if (col_reduce) {
+          ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
+          if (block_acc_bytes) HIP_CHECK(hipMemsetAsync(sp.acc, 0, block_acc_bytes, s));
+        }
         hipLaunchKernelGGL((enc ? k_pr_apply<V, E, R, true> : k_pr_apply<V, E, R, false>), dim3(nblk_apply),
                            dim3(kBlock), 0, s, sap);
         CGX_LAUNCH_CHECK();

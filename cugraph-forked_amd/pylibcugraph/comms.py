@@ -53,7 +53,17 @@ class CommOps(ctypes.Structure):
 
 
 def default_row_comm_size(world_size: int) -> int:
-    """C of the R x C grid: R = the largest divisor of P with R*R <= P (8 -> 2 x 4)."""
+    """C of the R x C grid.
+
+    Up to 8 ranks (one node, every GPU pair joined by its own xGMI link) the grid is
+    1 x P.  The x~ allgather then runs over all P-1 links at once and there is no
+    column reduce-scatter at all.  The reference's squarer grid (mg_utilities.cpp:60-66;
+    2 x 4 at 8 GPUs) trades that for less total volume, which pays on switched
+    networks.  On a full mesh the per-link time is what counts: V/P*4 B for the
+    allgather, plus V/P*8 B for a reduce-scatter whenever R > 1.
+    Beyond 8 ranks: R = the largest divisor of P with R*R <= P."""
+    if world_size <= 8:
+        return world_size
     r = 1
     for d in range(1, int(math.isqrt(world_size)) + 1):
         if world_size % d == 0:
