@@ -419,6 +419,129 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
   flush_counts(a.ctr, my_n, my_m);
 }
 
+// Bottom-up in two passes (identity order only, i.e. degree-renumbered graphs).
+//
+// Adjacency lists are sorted by id and ids descend by degree, so a vertex's first
+// neighbours are its hubs, and those are the likeliest to be in the frontier.
+//  * probe: one lane per vertex, 64 consecutive vertices per wave.  An unvisited
+//    vertex loads its first (up to) 4 neighbours at once and takes the first one in
+//    the frontier.  The wave's 64 visited/next bits are two whole words that no
+//    other wave touches, written without atomics.  Vertices of degree > 4 that miss
+//    go to a residual list.
+//  * residual: 16-lane groups scan the rest of those lists (from the 5th neighbour).
+// Both take the first hit in sorted order, i.e. the smallest-id frontier
+// neighbour, the same predecessor as the one-pass k_bottomup.  (The one-pass kernel
+// gives a low-degree vertex a 4..64-lane group, so a wave advances 1..16 vertices
+// per dependent load chain.)
+#ifndef CGX_BFS_PROBE
+#define CGX_BFS_PROBE 8  // RMAT-24 MTEPS: 1: 116K, 2: 129K, 4: 141K, 8: 146K, 16: 142K, 32: 136K
+#endif
+constexpr int kProbe = CGX_BFS_PROBE;
+
+template <typename V, typename E>
+__global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
+{
+  V const nd    = (V)(a.depth + 1);
+  int const lane = threadIdx.x & 63;
+  unsigned long long my_n = 0, my_m = 0;
+  int64_t const nchunks = (a.nv + 63) >> 6;
+  int64_t const stride  = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t c = blockIdx.x * (int64_t)(kBlock / 64) + (threadIdx.x >> 6); c < nchunks; c += stride) {
+    int64_t const v  = (c << 6) + lane;
+    bool const in    = v < a.nv;
+    uint32_t const vw = in ? a.vis[v >> 5] : 0xffffffffu;
+    bool const un    = in && !((vw >> (uint32_t(v) & 31u)) & 1u);
+    E beg = 0, end = 0;
+    if (un) {
+      beg = a.off[v];
+      end = a.off[v + 1];
+    }
+    int64_t const deg = (int64_t)(end - beg);
+    bool hit = false, more = false;
+    V par    = 0;
+    if (deg > 0) {
+      V u[kProbe];
+#pragma unroll
+      for (int t = 0; t < kProbe; ++t) u[t] = a.idx[beg + (t < deg ? t : 0)];
+      uint32_t fw[kProbe];  // all frontier words first: the loads issue back to back
+#pragma unroll
+      for (int t = 0; t < kProbe; ++t) fw[t] = a.fr[u[t] >> 5];
+      uint32_t hm = 0;
+#pragma unroll
+      for (int t = 0; t < kProbe; ++t) hm |= (t < deg ? (fw[t] >> (uint32_t(u[t]) & 31u)) & 1u : 0u) << t;
+#pragma unroll
+      for (int t = kProbe - 1; t >= 0; --t)  // the lowest hit wins: the smallest-id frontier neighbour
+        if ((hm >> t) & 1u) par = u[t];
+      hit  = hm != 0;
+      more = !hit && deg > kProbe;
+    }
+    if (hit) {
+      a.dist[v] = nd;
+      if (a.pred) a.pred[v] = par;
+      my_n += 1;
+      my_m += (unsigned long long)deg;
+    }
+    unsigned long long const hm = __ballot(hit);
+    if ((lane & 31) == 0) {
+      uint32_t const b = (uint32_t)(hm >> lane);  // this half-wave's word
+      if (b) {
+        a.vis[v >> 5] = vw | b;
+        a.nxt[v >> 5] = b;
+      }
+    }
+    unsigned long long const mm = __ballot(more);
+    if (mm) {
+      unsigned long long base = 0;
+      int const leader = __ffsll((long long)mm) - 1;
+      if (lane == leader) base = atomicAdd(&a.ctr->qlen[0], (unsigned long long)__popcll(mm));
+      base = __shfl(base, leader, 64);
+      if (more) res[base + __popcll(mm & ((1ull << lane) - 1ull))] = (V)v;
+    }
+  }
+  flush_counts(a.ctr, my_n, my_m);
+}
+
+template <typename V, typename E>
+__global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* res)
+{
+  constexpr int w = 16;
+  V const nd       = (V)(a.depth + 1);
+  int const tid    = threadIdx.x;
+  int const lane   = tid & (w - 1);
+  int const gbase  = (tid & 63) & ~(w - 1);
+  int64_t const n  = (int64_t)a.ctr->qlen[0];  // written by k_bu_probe (earlier launch)
+  int64_t const ng = (int64_t)gridDim.x * (kBlock / w);
+  unsigned long long my_n = 0, my_m = 0;
+  for (int64_t i = blockIdx.x * (int64_t)(kBlock / w) + tid / w; i < n; i += ng) {
+    V const v     = res[i];
+    E const beg0  = a.off[v];
+    E const end   = a.off[v + 1];
+    for (E base = beg0 + kProbe; base < end; base += w) {
+      E const e = base + lane;
+      bool hit  = false;
+      V u       = 0;
+      if (e < end) {
+        u   = a.idx[e];
+        hit = (a.fr[u >> 5] >> (uint32_t(u) & 31u)) & 1u;
+      }
+      unsigned long long const gm = (__ballot(hit) >> gbase) & 0xffffull;
+      if (gm) {
+        if (lane == __ffsll((long long)gm) - 1) {
+          uint32_t const bit = 1u << (uint32_t(v) & 31u);
+          a.dist[v] = nd;
+          if (a.pred) a.pred[v] = u;
+          atomicOr(a.nxt + (v >> 5), bit);
+          atomicOr(a.vis + (v >> 5), bit);
+          my_n += 1;
+          my_m += (unsigned long long)(end - beg0);
+        }
+        break;
+      }
+    }
+  }
+  flush_counts(a.ctr, my_n, my_m);
+}
+
 template <typename V>
 __global__ void k_bfs_init_sources(V* dist, V const* src, size_t ns, int64_t nv, int* bad)
 {
@@ -537,6 +660,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
                                               (unsigned long long)std::numeric_limits<V>::max());
     size_t levels = 0, bu_steps = 0;
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
+    bool const one_pass_bu = std::getenv("CGX_BFS_ONE_PASS_BU") != nullptr;  // A/B: the one-pass bottom-up
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
@@ -554,7 +678,14 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           have_bitmap = true;
         }
         HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));
-        hipLaunchKernelGGL((k_bottomup<V, E>), dim3(adj.num_items), dim3(kBlock), 0, s, a);
+        if (a.order == nullptr && !one_pass_bu) {  // probe + residual (identity order)
+          hipLaunchKernelGGL((k_bu_probe<V, E>), dim3(grid_for((nv + 63) / 64, kBlock / 64, 8192)), dim3(kBlock), 0,
+                             s, a, qb[0].data());
+          CGX_LAUNCH_CHECK();
+          hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(4096), dim3(kBlock), 0, s, a, qb[0].data());
+        } else {
+          hipLaunchKernelGGL((k_bottomup<V, E>), dim3(adj.num_items), dim3(kBlock), 0, s, a);
+        }
         CGX_LAUNCH_CHECK();
         read_ctr();
         std::swap(a.fr, a.nxt);
