@@ -661,6 +661,15 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     size_t levels = 0, bu_steps = 0;
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
     bool const one_pass_bu = std::getenv("CGX_BFS_ONE_PASS_BU") != nullptr;  // A/B: the one-pass bottom-up
+    // Grid sizes: every block ends with same-address atomics on the level counters,
+    // which serialise at the memory side (≈8 ns each): RMAT-24 MTEPS with the probe
+    // on 512 / 1024 / 2048 / 8192 / 32768 blocks: 166K / 173K / 168K / 148K / 101K
+    unsigned const residual_grid = std::getenv("CGX_BFS_RES_GRID") ? (unsigned)std::atoi(std::getenv("CGX_BFS_RES_GRID"))
+                                                                   : 1024u;
+    // (top-down segments capped at 1024 blocks each: 176.5K vs 148K MTEPS uncapped; 256-2048 within noise)
+    long long const td_cap = std::getenv("CGX_BFS_TD_CAP") ? std::atoll(std::getenv("CGX_BFS_TD_CAP")) : 1024;
+    unsigned const probe_grid = std::getenv("CGX_BFS_PROBE_GRID") ? (unsigned)std::atoi(std::getenv("CGX_BFS_PROBE_GRID"))
+                                                                  : 1024u;
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
@@ -679,10 +688,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         }
         HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));
         if (a.order == nullptr && !one_pass_bu) {  // probe + residual (identity order)
-          hipLaunchKernelGGL((k_bu_probe<V, E>), dim3(grid_for((nv + 63) / 64, kBlock / 64, 8192)), dim3(kBlock), 0,
-                             s, a, qb[0].data());
+          hipLaunchKernelGGL((k_bu_probe<V, E>), dim3(grid_for((nv + 63) / 64, kBlock / 64, probe_grid)), dim3(kBlock),
+                             0, s, a, qb[0].data());
           CGX_LAUNCH_CHECK();
-          hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(4096), dim3(kBlock), 0, s, a, qb[0].data());
+          hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, a, qb[0].data());
         } else {
           hipLaunchKernelGGL((k_bottomup<V, E>), dim3(adj.num_items), dim3(kBlock), 0, s, a);
         }
@@ -713,6 +722,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         long long nb_large = ncur[2] ? (long long)std::min<unsigned long long>(std::max<unsigned long long>(ncur[2] * 8, 256), 4096) : 0;
         long long nb_mid   = (long long)std::min<unsigned long long>((ncur[1] + 3) / 4, 4096);
         long long nb_small = (long long)std::min<unsigned long long>((ncur[0] + 63) / 64, 8192);
+        nb_large = std::min(nb_large, td_cap);
+        nb_mid   = std::min(nb_mid, td_cap);
+        nb_small = std::min(nb_small, td_cap);
         a.blk_mid_start    = nb_large;
         a.blk_small_start  = nb_large + nb_mid;
         long long grid     = nb_large + nb_mid + nb_small;
