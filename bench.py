@@ -18,6 +18,10 @@ Extra fields on the same JSON line:
                    the BFS path is available.
   louvain       -- configs[4]: Louvain time-to-solution, modularity and levels on
                    RMAT scale 23 + log2(N) (scale 26 at 8 GPUs), uniform weights.
+  bfs.cpu_baseline / louvain.cpu_baseline -- the reference's NetworkX CPU path
+                   (nx.single_source_shortest_path_length, nx louvain_communities)
+                   on bounded R-MAT samples (RMAT-16 / RMAT-14; NetworkX cannot
+                   hold the benchmark graphs), N=1 only.
 
 Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU):
 weak scaling, R-MAT scale 22 + log2(N) for PageRank (the headline value); the
@@ -234,6 +238,34 @@ def louvain_leg(p, args):
             "path": "sg" if args.world == 1 else f"mg{args.world} ({'RCCL' if args.comm == 'rccl' else 'torch'})"}
 
 
+def cpu_networkx_legs(args):
+    """the reference's NetworkX CPU path for BFS and Louvain, on bounded
+    R-MAT samples (same generator parameters, numpy twin), 1 core.  NetworkX's
+    dict-of-dicts graph cannot hold RMAT-23/24, so the sample scale is stated."""
+    import numpy as np
+    from oracle import graph as og
+    from oracle import rmat
+    from oracle.baseline import networkx_bfs, networkx_louvain
+    out = {}
+    sb = 16
+    s, d = rmat.rmat(sb, 16 << sb, seed=42)
+    s, d, _ = og.symmetrize_dedup(s, d, None)
+    root = int(s[0])
+    tb, t, e_cc = networkx_bfs(s, d, root)
+    out["bfs"] = {"value": (e_cc / t) / 1e6, "unit": "MTEPS", "cores": 1, "kind": "networkx",
+                  "sample": f"nx.single_source_shortest_path_length, networkx 3.4.2, RMAT-{sb} symmetric "
+                            f"({s.size} stored edges), 1 root; graph build {tb:.1f}s excluded"}
+    sl = 14
+    s, d = rmat.rmat(sl, 16 << sl, seed=42)
+    w = rmat.rmat_weights(s.size, seed=43).astype(np.float64)
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    tb, t, q = networkx_louvain(s, d, w)
+    out["louvain"] = {"value": t, "unit": "s", "cores": 1, "kind": "networkx", "modularity": q,
+                      "sample": f"nx.community.louvain_communities(seed=42) + modularity, networkx 3.4.2, "
+                                f"RMAT-{sl} symmetric uniform weights ({s.size} stored edges); build {tb:.1f}s excluded"}
+    return out
+
+
 def stream_copy_gbs(nbytes=4 << 30, reps=10):
     """Measured HBM ceiling: device-to-device copy of a 4 GiB buffer,
     read + write bytes / time, HIP events."""
@@ -420,6 +452,15 @@ def main():
                 f"Q={out['louvain']['modularity']:.6f} levels={out['louvain']['levels']}")
         except Exception as e:  # noqa: BLE001
             out["louvain"] = {"status": "failed", "error": repr(e)[:300]}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            nxb = cpu_networkx_legs(args)
+            if isinstance(out.get("bfs"), dict) and "mteps_harmonic_mean" in out["bfs"]:
+                out["bfs"]["cpu_baseline"] = nxb["bfs"]
+            if isinstance(out.get("louvain"), dict) and "time_s" in out["louvain"]:
+                out["louvain"]["cpu_baseline"] = nxb["louvain"]
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] networkx baselines unavailable: {e!r}")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

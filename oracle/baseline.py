@@ -65,3 +65,36 @@ def bfs_numpy(offsets, indices, source, max_levels=1 << 30):
     reached = dist >= 0
     edges = int((offsets[1:] - offsets[:-1])[reached].sum())
     return t, edges
+
+
+def networkx_bfs(src, dst, source):
+    """The reference's CPU path for BFS: ``nx.single_source_shortest_path_length``
+    on an undirected ``nx.Graph`` (pure Python, 1 core).  Returns
+    (build_seconds, bfs_seconds, undirected edges of the source's component)."""
+    import networkx as nx
+
+    t0 = time.perf_counter()
+    G = nx.Graph()
+    G.add_edges_from(zip(np.asarray(src).tolist(), np.asarray(dst).tolist()))
+    t1 = time.perf_counter()
+    lengths = nx.single_source_shortest_path_length(G, int(source))
+    t2 = time.perf_counter()
+    e_cc = sum(G.degree(v) for v in lengths) // 2
+    return t1 - t0, t2 - t1, e_cc
+
+
+def networkx_louvain(src, dst, weights, seed=42):
+    """The reference's CPU path for Louvain: ``nx.community.louvain_communities``
+    (resolution 1, the given seed) + ``nx.community.modularity``.
+    Returns (build_seconds, louvain_seconds, modularity)."""
+    import networkx as nx
+
+    t0 = time.perf_counter()
+    G = nx.Graph()
+    G.add_weighted_edges_from(zip(np.asarray(src).tolist(), np.asarray(dst).tolist(),
+                                  np.asarray(weights, dtype=np.float64).tolist()))
+    t1 = time.perf_counter()
+    comms = nx.community.louvain_communities(G, weight="weight", resolution=1.0, seed=seed)
+    t2 = time.perf_counter()
+    q = nx.community.modularity(G, comms, weight="weight")
+    return t1 - t0, t2 - t1, q
