@@ -147,6 +147,38 @@ struct level_ctr {
   unsigned long long pad;
 };
 
+// Level counters are single addresses: same-address atomics serialise at the memory
+// side (≈8 ns each, bfs.hip), so appends are reserved once per wave and sums are
+// added once per block, and the kernels that do so run on capped grids.
+inline unsigned capped(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 1024); }
+
+__device__ __forceinline__ long long wave_reserve(unsigned long long* tail, bool take)
+{
+  unsigned long long const mask = __ballot(take);
+  if (mask == 0) return -1;
+  int const lane   = threadIdx.x & 63;
+  int const leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(tail, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return take ? (long long)(base + __popcll(mask & ((1ull << lane) - 1ull))) : -1;
+}
+
+// block sum of v added to *dst (one atomic per block, none when zero); all threads call
+__device__ __forceinline__ void block_add(unsigned long long* dst, unsigned long long v)
+{
+  __shared__ unsigned long long sm[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (int w = 0; w < kBlock / 64; ++w) tot += sm[w];
+    if (tot) atomicAdd(dst, tot);
+  }
+}
+
 template <typename V>
 __global__ void k_init_sources(V const* src_global, size_t n, int64_t lo, int64_t hi, V* dist, uint32_t* queue,
                                unsigned long long* nq, int* flag)
@@ -219,9 +251,13 @@ __global__ void k_td_claim(unsigned long long const* cand, int64_t n, int64_t lo
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t v = (int64_t)(cand[i] >> 32) - lo;
     long long u = (long long)(uint32_t)cand[i];
-    if (dist[v] != INF) continue;
-    atomicMin(best + v, u);
-    if (atomicCAS(flag + v, 0, 1) == 0) next[atomicAdd(&ctr->next_n, 1ull)] = (uint32_t)v;
+    bool take = false;
+    if (dist[v] == INF) {
+      atomicMin(best + v, u);
+      take = atomicCAS(flag + v, 0, 1) == 0;
+    }
+    long long const slot = wave_reserve(&ctr->next_n, take);
+    if (take) next[slot] = (uint32_t)v;
   }
 }
 
@@ -237,7 +273,7 @@ __global__ void k_td_finalize(uint32_t const* next, int64_t n, V depth1, V* dist
     best[v] = std::numeric_limits<long long>::max();
     m += (unsigned long long)(off[v + 1] - off[v]);
   }
-  atomicAdd(&ctr->next_m, m);
+  block_add(&ctr->next_m, m);
 }
 
 __global__ void k_mark_bits(uint32_t const* q, int64_t n, uint32_t* bits)
@@ -254,22 +290,26 @@ __global__ void k_bottom_up(int64_t n_own, int64_t const* off, uint32_t const* i
   V const INF = std::numeric_limits<V>::max();
   unsigned long long m = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_own; v += (int64_t)gridDim.x * blockDim.x) {
-    if (dist[v] != INF) continue;
-    for (int64_t e = off[v]; e < off[v + 1]; ++e) {
-      int64_t u = idx[e];
-      int q     = mg_owner_of_global(u, voff, P);
-      int64_t l = u - voff[q];
-      if ((bitmap[q * words + (l >> 5)] >> (l & 31)) & 1u) {
-        dist[v] = depth1;
-        if (pred) pred[v] = (V)u;
-        flag[v] = 1;
-        next[atomicAdd(&ctr->next_n, 1ull)] = (uint32_t)v;
-        m += (unsigned long long)(off[v + 1] - off[v]);
-        break;
+    bool take = false;
+    if (dist[v] == INF) {
+      for (int64_t e = off[v]; e < off[v + 1]; ++e) {
+        int64_t u = idx[e];
+        int q     = mg_owner_of_global(u, voff, P);
+        int64_t l = u - voff[q];
+        if ((bitmap[q * words + (l >> 5)] >> (l & 31)) & 1u) {
+          dist[v] = depth1;
+          if (pred) pred[v] = (V)u;
+          flag[v] = 1;
+          take    = true;
+          m += (unsigned long long)(off[v + 1] - off[v]);
+          break;
+        }
       }
     }
+    long long const slot = wave_reserve(&ctr->next_n, take);
+    if (take) next[slot] = (uint32_t)v;
   }
-  atomicAdd(&ctr->next_m, m);
+  block_add(&ctr->next_m, m);
 }
 
 template <typename V>
@@ -391,7 +431,7 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       CGX_LAUNCH_CHECK();
       comm.allgather<uint32_t>(seg.data(), bitmap.data(), (size_t)rows.words, s);
       if (n_own)
-        hipLaunchKernelGGL(k_bottom_up<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
+        hipLaunchKernelGGL(k_bottom_up<V>, dim3(capped(n_own)), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
                            rows.idx.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), P, rows.words, depth1,
                            flag.data(), qb.data(), ctr.data());
       CGX_LAUNCH_CHECK();
@@ -436,13 +476,13 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       std::vector<size_t> rcnt;
       auto got = exchange<int64_t>(comm, reinterpret_cast<int64_t const*>(cu.data()), counts, rcnt, s);
       if (got.n)
-        hipLaunchKernelGGL(k_td_claim<V>, dim3(blocks(got.n)), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL(k_td_claim<V>, dim3(capped(got.n)), dim3(kBlock), 0, s,
                            reinterpret_cast<unsigned long long const*>(got.data()), (int64_t)got.n, lo, dist,
                            best.data(), flag.data(), qb.data(), ctr.data());
       CGX_LAUNCH_CHECK();
       auto hn = to_host(ctr.data(), 1, s)[0];
       if (hn.next_n)
-        hipLaunchKernelGGL(k_td_finalize<V>, dim3(blocks(hn.next_n)), dim3(kBlock), 0, s, qb.data(),
+        hipLaunchKernelGGL(k_td_finalize<V>, dim3(capped(hn.next_n)), dim3(kBlock), 0, s, qb.data(),
                            (int64_t)hn.next_n, depth1, dist, pred, best.data(), rows.off.data<int64_t>(), ctr.data());
       CGX_LAUNCH_CHECK();
     }

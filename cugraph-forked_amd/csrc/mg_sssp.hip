@@ -230,6 +230,19 @@ __global__ void k_candidates(uint32_t const* q, int64_t nq, unsigned long long c
   }
 }
 
+// appends to one tail: one atomic per wave (same-address atomics serialise, bfs.hip)
+__device__ __forceinline__ long long wave_reserve(unsigned long long* tail, bool take)
+{
+  unsigned long long const mask = __ballot(take);
+  if (mask == 0) return -1;
+  int const lane   = threadIdx.x & 63;
+  int const leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(tail, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return take ? (long long)(base + __popcll(mask & ((1ull << lane) - 1ull))) : -1;
+}
+
 template <typename W>
 __global__ void k_apply(uint32_t const* keys, W const* vals, int64_t n, int64_t lo, W* dist, int* stamp, int round,
                         uint32_t* changed, unsigned long long* nchanged)
@@ -237,8 +250,9 @@ __global__ void k_apply(uint32_t const* keys, W const* vals, int64_t n, int64_t 
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t const l = (int64_t)keys[i] - lo;
     W const nd      = vals[i];
-    if (nd < dist[l] && atomic_min_nonneg(dist + l, nd) > nd && atomicExch(stamp + l, round) != round)
-      changed[atomicAdd(nchanged, 1ull)] = (uint32_t)l;
+    bool const take = nd < dist[l] && atomic_min_nonneg(dist + l, nd) > nd && atomicExch(stamp + l, round) != round;
+    long long const slot = wave_reserve(nchanged, take);
+    if (take) changed[slot] = (uint32_t)l;
   }
 }
 
@@ -254,22 +268,25 @@ __global__ void k_split(uint32_t const* in, int64_t n, W const* dist, W const* r
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t const l = in[i];
     W const d        = dist[l];
+    bool to_near = false, to_far = false;
     if (from_far) {
       if (relaxed[l] == d) {
         infar[l] = 0;
-        continue;
-      }
-      if (d < thr) {
+      } else if (d < thr) {
         infar[l] = 0;
-        near[atomicAdd(nnear, 1ull)] = l;
+        to_near  = true;
       } else {
-        far[atomicAdd(nfar, 1ull)] = l;
+        to_far = true;
       }
     } else if (d < thr) {
-      near[atomicAdd(nnear, 1ull)] = l;
-    } else if (atomicExch(infar + l, 1) == 0) {
-      far[atomicAdd(nfar, 1ull)] = l;
+      to_near = true;
+    } else {
+      to_far = atomicExch(infar + l, 1) == 0;
     }
+    long long const sn = wave_reserve(nnear, to_near);
+    long long const sf = wave_reserve(nfar, to_far);
+    if (to_near) near[sn] = l;
+    if (to_far) far[sf] = l;
   }
 }
 
