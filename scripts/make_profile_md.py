@@ -1,0 +1,61 @@
+"""Write profiles/r01_bench.md from profiles/r01_bench_n1.json + r01_bench_kernel_stats.csv."""
+import csv
+import json
+import re
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+d = json.loads(open(f"profiles/{tag}_bench_n1.json").read())
+rows = list(csv.DictReader(open(f"profiles/{tag}_bench_kernel_stats.csv")))
+r = d["roofline"]
+
+
+def short(n):
+    n = n.replace("rocprim::ROCPRIM_400200_NS::detail::", "").replace("cgx::(anonymous namespace)::", "")
+    return n.replace("void ", "")[:90]
+
+
+push = next(x for x in rows if "k_pr_push" in x["Name"])
+app = next(x for x in rows if "k_pr_apply" in x["Name"])
+pa = (float(push["AverageNs"]) + float(app["AverageNs"])) / 1e3
+ev = r["avg_kernel_ms"] * 1e3
+out = [
+    f"# Profile {tag}: `bench.py` on one MI355X",
+    "",
+    f"Sources:",
+    f"- `profiles/{tag}_bench_n1.json`: the bench line from `python bench.py` (default legs).",
+    f"- `profiles/{tag}_bench_kernel_stats.csv`: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-traffic",
+    "  --no-cpu-baseline` (`scripts/gpu_profile_round.sh`). Graph construction is in the trace but in no timed region.",
+    "",
+    "## PageRank iteration (the roofline kernel pair)",
+    "",
+    "| kernel | launches | avg µs (rocprof) |",
+    "|---|---|---|",
+    f"| `{short(push['Name']).split('(')[0]}` | {push['Calls']} | {float(push['AverageNs']) / 1e3:.1f} |",
+    f"| `{short(app['Name']).split('(')[0]}` | {app['Calls']} | {float(app['AverageNs']) / 1e3:.1f} |",
+    "",
+    f"- rocprof push + apply = {pa:.1f} µs per iteration. The bench's HIP events around both launches (gap",
+    f"  included) give {ev:.1f} µs; the two agree within {abs(ev - pa) / pa * 100:.1f} %.",
+    f"- Algorithmic bytes per iteration: 4E + 16V = {r['algorithmic_bytes_per_launch'] / 1e6:.1f} MB, giving {r['achieved']:.0f} GB/s =",
+    f"  **{r['frac'] * 100:.1f} % of 8 TB/s**.",
+    f"- Measured HBM traffic per iteration (2×FETCH_SIZE + WRITE_SIZE, separate PMC passes) = {r['traffic'] / 1e6:.0f} MB,",
+    f"  i.e. {r['traffic'] / (r['avg_kernel_ms'] * 1e-3) / 1e12:.2f} TB/s actually moved. The measured stream-copy ceiling",
+    f"  (4 GiB device copy) is {r['stream_copy_gbs'] / 1e3:.2f} TB/s.",
+    "",
+    "## Other legs",
+    "",
+    f"- BFS RMAT-24: {d['bfs']['mteps_harmonic_mean']:.0f} MTEPS harmonic mean (Graph500 counting),",
+    f"  {d['bfs']['stored_edge_mteps_harmonic_mean']:.0f} stored-edge MTEPS, {d['bfs']['ms_mean']:.2f} ms per traversal.",
+    f"  NetworkX: {d['bfs'].get('cpu_baseline', {}).get('value', float('nan')):.2f} MTEPS ({d['bfs'].get('cpu_baseline', {}).get('sample', '')}).",
+    f"- Louvain RMAT-23: {d['louvain']['time_s']:.3f} s, Q {d['louvain']['modularity']:.4f}, {d['louvain']['levels']} levels.",
+    f"  NetworkX: {d['louvain'].get('cpu_baseline', {}).get('value', float('nan')):.2f} s ({d['louvain'].get('cpu_baseline', {}).get('sample', '')}).",
+    f"- PageRank CPU baseline: {d['cpu_baseline']['value']:.3g} edges/s ({d['cpu_baseline']['sample']}).",
+    "",
+    "## Top kernels of the whole run",
+    "",
+    "| kernel | calls | avg µs | % |",
+    "|---|---|---|---|",
+]
+for x in rows[:15]:
+    out.append(f"| `{short(x['Name'])}` | {x['Calls']} | {float(x['AverageNs']) / 1e3:.1f} | {x['Percentage'][:5]} |")
+open(f"profiles/{tag}_bench.md", "w").write("\n".join(out) + "\n")
