@@ -53,6 +53,14 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def release_caches(p):
+    """Between legs: torch's cached blocks and libcugraph_c's caching allocator."""
+    import torch
+    torch.cuda.synchronize()
+    p.trim_device_cache()
+    torch.cuda.empty_cache()
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -440,13 +448,13 @@ def main():
     if args.bfs:
         try:
             del r
-            torch.cuda.empty_cache()
+            release_caches(p)
             out["bfs"] = bfs_leg(p, args)
         except Exception as e:  # noqa: BLE001
             out["bfs"] = {"status": "failed", "error": repr(e)[:300]}
     if args.louvain:
         try:
-            torch.cuda.empty_cache()
+            release_caches(p)
             out["louvain"] = louvain_leg(p, args)
             log(f"[bench] louvain: RMAT-{out['louvain']['scale']} {out['louvain']['time_s']:.3f}s "
                 f"Q={out['louvain']['modularity']:.6f} levels={out['louvain']['levels']}")

@@ -19,9 +19,16 @@ from ._arrays import DeviceArray, DeviceView, copy_view_to_tensor, optional_view
 from . import generators  # noqa: E402,F401  (MI355X build extensions)
 from . import comms  # noqa: E402,F401  (multi-GPU communicator contexts)
 
-__all__ = ["ResourceHandle", "GraphProperties", "SGGraph", "MGGraph", "pagerank",
+__all__ = ["trim_device_cache", "ResourceHandle", "GraphProperties", "SGGraph", "MGGraph", "pagerank",
            "personalized_pagerank", "katz_centrality", "eigenvector_centrality", "hits", "bfs", "sssp",
            "louvain", "version"]
+
+
+def trim_device_cache():
+    """Return libcugraph_c's cached HBM blocks to the driver (ext.h
+    cugraph_amd_trim_device_cache); call it beside torch.cuda.empty_cache().
+    Returns the bytes released."""
+    return int(_lib.lib.cugraph_amd_trim_device_cache())
 
 
 def version():
