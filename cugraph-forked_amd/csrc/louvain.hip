@@ -27,6 +27,8 @@
 #include "prims.hpp"
 
 #include <rocprim/device/device_reduce_by_key.hpp>
+#include <rocprim/device/device_segmented_reduce.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <cfloat>
@@ -113,21 +115,6 @@ __global__ void k_row_offsets(uint32_t const* src, int64_t ne, int64_t nv, int64
   }
 }
 
-// vertex weights k[v] (row sums, in edge order) and self-loop weights
-__global__ void k_vertex_weights(int64_t const* off, uint32_t const* src, uint32_t const* dst, double const* w,
-                                 int64_t nv, uint32_t base, double* k, double* self, uint8_t* has_edges)
-{
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-    double s = 0, sl = 0;
-    for (int64_t e = off[v]; e < off[v + 1]; ++e) {
-      s += w[e];
-      if (dst[e] == (uint32_t)v + base) sl += w[e];
-    }
-    k[v]         = s;
-    self[v]      = sl;
-    has_edges[v] = off[v + 1] > off[v] ? 1 : 0;
-  }
-}
 
 __global__ void k_sweep_keys(uint32_t const* src, uint32_t const* dst, uint32_t const* c, int64_t ne, u64* keys)
 {
@@ -207,6 +194,21 @@ struct plain_f {
   __device__ double operator()(size_t i) const { return w[i]; }
 };
 
+// self-loop weight of edge e (its row is src[e] + base)
+struct self_w_f {
+  uint32_t const* s;
+  uint32_t const* d;
+  double const* w;
+  uint32_t base;
+  __device__ double operator()(int64_t e) const { return d[e] == s[e] + base ? w[e] : 0.0; }
+};
+
+__global__ void k_has_edges(int64_t const* off, int64_t n, uint8_t* has)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    has[v] = off[v + 1] > off[v] ? 1 : 0;
+}
+
 // contraction
 __global__ void k_pair_keys(uint32_t const* src, uint32_t const* dst, uint32_t const* lab, int64_t ne, u64* keys)
 {
@@ -282,6 +284,31 @@ struct louvain_state {
   dbuf<double> scal;       // 2 scalars
   explicit louvain_state(hipStream_t st) : s(st), scratch(1024, st), scal(2, st) {}
 };
+
+// k[v] = weight of row v, self[v] = its self-loop weight, has_edges[v]: segmented
+// reductions over the row offsets (rocPRIM hands segments to blocks), so a hub row
+// no longer runs as one thread's serial loop (20 ms per level at RMAT-23)
+void vertex_weights(louvain_state& S, level_graph const& g, int64_t const* off, double* k, double* self,
+                    uint8_t* has_edges)
+{
+  hipStream_t s    = S.s;
+  int64_t const nr = g.nrows;
+  if (nr == 0) return;
+  auto selfw = rocprim::make_transform_iterator(rocprim::make_counting_iterator<int64_t>(0),
+                                                self_w_f{g.src.data(), g.dst.data(), g.w.data(), (uint32_t)g.base});
+  size_t t1 = 0, t2 = 0;
+  HIP_CHECK(rocprim::segmented_reduce(nullptr, t1, g.w.data(), k, (unsigned)nr, off, off + 1,
+                                      rocprim::plus<double>(), 0.0, s));
+  HIP_CHECK(rocprim::segmented_reduce(nullptr, t2, selfw, self, (unsigned)nr, off, off + 1, rocprim::plus<double>(),
+                                      0.0, s));
+  buffer tmp(std::max<size_t>(std::max(t1, t2), 1), s);
+  HIP_CHECK(rocprim::segmented_reduce(tmp.data(), t1, g.w.data(), k, (unsigned)nr, off, off + 1,
+                                      rocprim::plus<double>(), 0.0, s));
+  HIP_CHECK(rocprim::segmented_reduce(tmp.data(), t2, selfw, self, (unsigned)nr, off, off + 1,
+                                      rocprim::plus<double>(), 0.0, s));
+  hipLaunchKernelGGL(k_has_edges, dim3(blocks(nr)), dim3(kBlock), 0, s, off, nr, has_edges);
+  CGX_LAUNCH_CHECK();
+}
 
 // Q = internal / m - gamma * sum_c a_c^2 / m^2 (compute_modularity,
 // common_methods.cuh:121-170).  Each rank sums its own edges and the a_c of the
@@ -478,9 +505,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     CGX_LAUNCH_CHECK();
     dbuf<double> k(nv, s), self(nv, s), a(nv, s);
     dbuf<uint8_t> has_edges(nv, s), present(nv, s);
-    hipLaunchKernelGGL(k_vertex_weights, dim3(blocks(nv)), dim3(kBlock), 0, s, off.data(), cur.src.data(),
-                       cur.dst.data(), cur.w.data(), nv, 0u, k.data(), self.data(), has_edges.data());
-    CGX_LAUNCH_CHECK();
+    vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
     HIP_CHECK(hipMemcpyAsync(a.data(), k.data(), nv * sizeof(double), hipMemcpyDeviceToDevice, s));
     fill<uint8_t>(present.data(), nv, 1, s);
     dbuf<uint32_t> clusters(nv, s), next(nv, s);
@@ -857,10 +882,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     dbuf<double> k(r1, s), self(r1, s), a(nv, s);
     dbuf<uint8_t> has_edges(r1, s), present(nv, s);
     if (nr)
-      hipLaunchKernelGGL(k_vertex_weights, dim3(blocks(nr)), dim3(kBlock), 0, s, off.data(), cur.src.data(),
-                         cur.dst.data(), cur.w.data(), nr, (uint32_t)cur.base, k.data(), self.data(),
-                         has_edges.data());
-    CGX_LAUNCH_CHECK();
+      vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
     allgatherv_dense<double>(comm, k.data(), voff, a.data(), s);
     fill<uint8_t>(present.data(), nv, 1, s);
     dbuf<uint32_t> clusters(nv, s), next(r1, s);
