@@ -610,8 +610,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     qb[c].resize(nv, s);
   }
   dbuf<bfs_ctr> ctr(1, s);
-  bfs_ctr* hctr = nullptr;
-  HIP_CHECK(hipHostMalloc((void**)&hctr, sizeof(bfs_ctr), hipHostMallocDefault));
+  bfs_ctr* hctr = h.pinned_as<bfs_ctr>();
 
   bfs_args<V, E> a{};
   a.off   = adj.offsets.data<E>();
@@ -755,10 +754,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     h.last_bfs_levels    = levels;
     h.last_bfs_bottom_up = bu_steps;
   } catch (...) {
-    (void)hipHostFree(hctr);
     throw;
   }
-  HIP_CHECK(hipHostFree(hctr));
   if (pred) {
     hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF);
     CGX_LAUNCH_CHECK();

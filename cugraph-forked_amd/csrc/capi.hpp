@@ -33,6 +33,33 @@ struct handle_t {
   size_t last_bfs_levels     = 0;
   size_t last_bfs_bottom_up  = 0;
   size_t last_louvain_levels = 0;
+  // Host-pinned scratch for the per-level / per-chunk device state reads and a pool
+  // of profiling events, both kept for the handle's lifetime: hipHostMalloc +
+  // hipHostFree per call measured ~250 us of host stall per BFS traversal.
+  void* pinned = nullptr;
+  std::vector<hipEvent_t> events;
+  template <typename T>
+  T* pinned_as()
+  {
+    static_assert(sizeof(T) <= kPinnedBytes, "pinned scratch too small");
+    if (!pinned) HIP_CHECK(hipHostMalloc(&pinned, kPinnedBytes, hipHostMallocDefault));
+    return static_cast<T*>(pinned);
+  }
+  hipEvent_t event(size_t i)  // the i-th pooled event (created on first use)
+  {
+    while (events.size() <= i) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreate(&e));
+      events.push_back(e);
+    }
+    return events[i];
+  }
+  static constexpr size_t kPinnedBytes = 4096;
+  ~handle_t()
+  {
+    if (pinned) (void)hipHostFree(pinned);
+    for (auto e : events) (void)hipEventDestroy(e);
+  }
 };
 
 struct array_view_t {  // reference c_api/array.hpp:30-35

@@ -1067,18 +1067,16 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   size_t launched = 0;
   auto kernel  = g.weighted ? k_pr_iter<V, E, R, true> : k_pr_iter<V, E, R, false>;
   pr_state* hpin = nullptr;
-  HIP_CHECK(hipHostMalloc((void**)&hpin, sizeof(pr_state), hipHostMallocDefault));
+  hpin = h.pinned_as<pr_state>();
   try {
     while (true) {
       for (int i = 0; i < chunk; ++i) {
         a.x_in  = bufs[launched & 1];
         a.x_out = bufs[(launched + 1) & 1];
         if (h.profiling) {
-          hipEvent_t e0, e1;
-          HIP_CHECK(hipEventCreate(&e0));
-          HIP_CHECK(hipEventCreate(&e1));
+          hipEvent_t const e0 = h.event(ev.size());  // pooled on the handle
           ev.push_back(e0);
-          ev.push_back(e1);
+          ev.push_back(h.event(ev.size()));
           HIP_CHECK(hipEventRecord(e0, s));
         }
         if (push) {
@@ -1098,11 +1096,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       if (hst.done) break;
     }
   } catch (...) {
-    (void)hipHostFree(hpin);
-    for (auto e : ev) (void)hipEventDestroy(e);
     throw;
   }
-  HIP_CHECK(hipHostFree(hpin));
   h.last_iterations = (size_t)hst.iter;
   if (h.profiling) {
     double tot = 0;
@@ -1112,7 +1107,6 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       HIP_CHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
       tot += ms;
     }
-    for (auto e : ev) HIP_CHECK(hipEventDestroy(e));
     h.last_hot_ms       = tot;
     h.last_hot_launches = k;
   }
@@ -1451,16 +1445,14 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   std::vector<hipEvent_t> ev;
   pr_state hst{};
   pr_state* hpin = nullptr;
-  HIP_CHECK(hipHostMalloc((void**)&hpin, sizeof(pr_state), hipHostMallocDefault));
+  hpin = h.pinned_as<pr_state>();
   try {
     while (true) {
       for (int i = 0; i < chunk; ++i) {
         if (h.profiling) {
-          hipEvent_t e0, e1;
-          HIP_CHECK(hipEventCreate(&e0));
-          HIP_CHECK(hipEventCreate(&e1));
+          hipEvent_t const e0 = h.event(ev.size());  // pooled on the handle
           ev.push_back(e0);
-          ev.push_back(e1);
+          ev.push_back(h.event(ev.size()));
           HIP_CHECK(hipEventRecord(e0, s));
         }
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
@@ -1489,11 +1481,8 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       if (hst.done) break;
     }
   } catch (...) {
-    (void)hipHostFree(hpin);
-    for (auto e : ev) (void)hipEventDestroy(e);
     throw;
   }
-  HIP_CHECK(hipHostFree(hpin));
   h.last_iterations = (size_t)hst.iter;
   if (h.profiling) {
     double tot = 0;
@@ -1503,7 +1492,6 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       HIP_CHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
       tot += ms;
     }
-    for (auto e : ev) HIP_CHECK(hipEventDestroy(e));
     h.last_hot_ms       = tot;
     h.last_hot_launches = k;
   }

@@ -295,7 +295,7 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
     fill<int>(infar.data(), nv, 0, s);
     dbuf<sssp_ctr> ctr(1, s);
     sssp_ctr* hc = nullptr;
-    HIP_CHECK(hipHostMalloc((void**)&hc, sizeof(sssp_ctr), hipHostMallocDefault));
+    hc = h.pinned_as<sssp_ctr>();
     try {
       auto read_ctr = [&]() {
         HIP_CHECK(hipMemcpyAsync(hc, ctr.data(), sizeof(sssp_ctr), hipMemcpyDeviceToHost, s));
@@ -373,10 +373,8 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
       }
       h.last_iterations = rounds;
     } catch (...) {
-      (void)hipHostFree(hc);
       throw;
     }
-    HIP_CHECK(hipHostFree(hc));
   }
   if (want_pred) {
     V* pred = res.predecessors->buf.data<V>();
