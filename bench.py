@@ -8,10 +8,11 @@ unweighted, fp32 PageRank, alpha 0.85, epsilon 1e-6.  A "step" is one complete
 value = stored edges x PageRank iterations x steps / timed seconds (whole job).
 
 Extra fields on the same JSON line:
-  roofline      -- the PageRank iteration kernel: algorithmic bytes/iteration
-                   (4E + 16V) / average kernel duration from HIP events recorded
-                   around every launch on the library's stream during the timed
-                   region; peak 8 TB/s (MI355X_MICROARCH.md).
+  roofline      -- the PageRank iteration kernels: algorithmic bytes/iteration
+                   (4E + 16V) / average iteration time from HIP events recorded
+                   around each 16-iteration chunk on the library's stream during
+                   the timed region (divided by the iterations run); peak 8 TB/s
+                   (MI355X_MICROARCH.md).
   cpu_baseline  -- NetworkX's PageRank loop (scipy CSR, fp64, 1 core;
                    oracle/baseline.py) for a few iterations on the SAME graph.
   bfs           -- configs[2]: RMAT scale-24 BFS MTEPS (Graph500 counting), when
@@ -409,7 +410,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_pr_push + k_pr_apply (one PageRank iteration, HIP events around both)" if world == 1 else
+            "kernel": ("k_pr_push_q + k_pr_apply (one PageRank iteration): HIP events around each 16-iteration chunk on the "
+                       "library stream / iterations run (inter-kernel gaps and post-convergence no-op launches included)" if world == 1 else
                        "one MG PageRank iteration per rank (row allgather + push + column reduce-scatter + apply + "
                        "allreduce, HIP events around all); bytes = this rank's 1/N share"),
             "achieved": r["achieved"],

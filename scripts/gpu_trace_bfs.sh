@@ -10,7 +10,7 @@ ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name
 idx = [i for i, k in enumerate(ks) if "k_bfs_init_sources" in k[2]][-1]
 t0 = ks[idx][0]
 for s, e, n in ks[idx:]:
-    nm = n.split("(")[0].replace("void ", "").replace("cgx::(anonymous namespace)::", "")[:40]
+    nm = n.replace("void ", "").replace("cgx::(anonymous namespace)::", "").split("(")[0][:40]
     print(f"{(s - t0) / 1e3:9.1f} us  dur {(e - s) / 1e3:8.1f} us  {nm}")
 PY
 exit $rc
