@@ -1441,17 +1441,17 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   int const chunk = 8;
   std::vector<hipEvent_t> ev;
   pr_state hst{};
-  pr_state* hpin = nullptr;
-  hpin = h.pinned_as<pr_state>();
-  try {
+  pr_state* hpin = h.pinned_as<pr_state>();
+  {
+    // (collectives run even in the no-op iterations after convergence: 8 per check;
+    // one pair of pooled events per chunk, as on one GPU)
     while (true) {
+      if (h.profiling) {
+        ev.push_back(h.event(ev.size()));
+        ev.push_back(h.event(ev.size()));
+        HIP_CHECK(hipEventRecord(ev[ev.size() - 2], s));
+      }
       for (int i = 0; i < chunk; ++i) {
-        if (h.profiling) {
-          hipEvent_t const e0 = h.event(ev.size());  // pooled on the handle
-          ev.push_back(e0);
-          ev.push_back(h.event(ev.size()));
-          HIP_CHECK(hipEventRecord(e0, s));
-        }
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
         if (nblk_push)
           hipLaunchKernelGGL((pmode == kPushQueue ? (g.weighted ? k_pr_push_q<V, E, R, true> : k_pr_push_q<V, E, R, false>)
@@ -1470,27 +1470,24 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
         ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
         hipLaunchKernelGGL((k_mg_finish_guarded<V, E, R>), dim3(1), dim3(64), 0, s, a, true);
         CGX_LAUNCH_CHECK();
-        if (h.profiling) HIP_CHECK(hipEventRecord(ev.back(), s));
       }
+      if (h.profiling) HIP_CHECK(hipEventRecord(ev.back(), s));
       HIP_CHECK(hipMemcpyAsync(hpin, st.data(), sizeof(pr_state), hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
       hst = *hpin;
       if (hst.done) break;
     }
-  } catch (...) {
-    throw;
   }
   h.last_iterations = (size_t)hst.iter;
   if (h.profiling) {
     double tot = 0;
-    size_t k   = std::min<size_t>((size_t)hst.iter, ev.size() / 2);
-    for (size_t i = 0; i < k; ++i) {
+    for (size_t i = 0; i + 1 < ev.size(); i += 2) {
       float ms = 0;
-      HIP_CHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+      HIP_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
       tot += ms;
     }
     h.last_hot_ms       = tot;
-    h.last_hot_launches = k;
+    h.last_hot_launches = std::max<size_t>((size_t)hst.iter, 1);
   }
   if (hst.done == 2) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
 }
