@@ -295,9 +295,12 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 // k_pr_apply then turns the sums into pr'/x~' per vertex (streaming) and resets the
 // accumulators.  Per iteration HBM traffic: 4E (entries) [+4E weights] + x~ lines
 // + 8V acc read + 8V acc reset + 16V vertex state.
-constexpr int kWinBits     = 13;
+#ifndef CGX_WIN_BITS
+#define CGX_WIN_BITS 12  // RMAT-22 ms/iteration: 11 bits 0.212, 12 bits 0.204, 13 bits 0.217, 14 bits 0.347
+#endif
+constexpr int kWinBits     = CGX_WIN_BITS;  // destination window: 2^12 x 8 B = 32 KB of LDS accumulators
 constexpr int kWin         = 1 << kWinBits;
-constexpr int kSrcBits     = 32 - kWinBits;  // 19
+constexpr int kSrcBits     = 32 - kWinBits;  // 20 source-offset bits per entry
 constexpr int kXcds        = 8;   // MI355X XCDs (workgroups are dealt to them round-robin)
 #ifndef CGX_XCD_SEGS
 #define CGX_XCD_SEGS 1
@@ -308,8 +311,14 @@ constexpr int kXcds        = 8;   // MI355X XCDs (workgroups are dealt to them r
 // blocks running at once share one or two slices) 0.27; no segments 0.221.  The
 // x~ misses these save cost less than the extra flushes and partial units.
 constexpr int kXcdSegs     = CGX_XCD_SEGS;
-constexpr int kPushThreads = 1024;
-constexpr int kPerThread   = 8;  // entries per thread per unit
+#ifndef CGX_PUSH_THREADS
+#define CGX_PUSH_THREADS 1024
+#endif
+constexpr int kPushThreads = CGX_PUSH_THREADS;
+#ifndef CGX_PER_THREAD
+#define CGX_PER_THREAD 8
+#endif
+constexpr int kPerThread   = CGX_PER_THREAD;  // entries per thread per unit
 constexpr int kPushUnit    = kPerThread * kPushThreads;
 #ifndef CGX_TILE_UNITS
 #define CGX_TILE_UNITS 8  // 8: 0.221, 16: 0.222, 32: 0.229, 64: 0.241 ms/iteration (RMAT-22)
