@@ -170,6 +170,8 @@ def traffic_leg(args):
         tot = 0.0
         for kern in ("k_pr_push", "k_pr_apply"):
             vals = [float(x["Counter_Value"]) for x in rows if kern in x["Kernel_Name"]]
+            if not vals and kern == "k_pr_apply":
+                continue  # fused apply (default): the push kernel does it
             if not vals:
                 return None, f"no {kern} launches under rocprofv3"
             live = [v for v in vals if v > 0.01 * max(vals)]

@@ -347,6 +347,13 @@ struct push_args {
   int64_t const* tiles;     // first unit of every (segment, window) tile, ntiles + 1 entries
   int64_t ntiles;
   unsigned int* tile_ctr;   // queue head (k_pr_apply resets it)
+  int32_t const* tile_win;  // window of every tile
+  // fused apply (k_pr_push_q<..., true>): the block finishing a window's last tile
+  // applies the window; the last window reduces the iteration
+  uint32_t const* win_tiles;
+  unsigned int* win_done;
+  unsigned int* tile_ctr_next;  // the other queue head (next iteration's), reset by the last window
+  int64_t nwin;
 };
 
 template <typename T>
@@ -551,11 +558,83 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_enc(push_args<V, E, R>
 // branch-free (masked lanes load x~[base] and add 0; the next unit of the tile is
 // always prefetched, the last re-reading itself), so the only waits are "gathers
 // done" and "prefetch done".
-template <typename V, typename E, typename R, bool WEIGHTED>
+// Sum over a kPushThreads block; result valid in thread 0.  `sm` >= kPushThreads / 64.
+__device__ __forceinline__ double block_sum_push(double v, double* sm)
+{
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = 0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < kPushThreads / 64; ++i) r += sm[i];
+  return r;
+}
+
+// Fused apply of window `win` (k_pr_apply's work for its kWin vertices) by the
+// block that finished the window's last tile.  Every tile's flush atomics have
+// completed (s_waitcnt vmcnt(0) before the window counter's increment), and the
+// sums are read with agent-scope atomic loads, coherent with those atomics.  The
+// window's (diff, dangling) partial goes to partials[2 win] (write-through); the
+// last window reduces the partials in window order -- deterministic -- and updates
+// the iteration state, then resets the next iteration's queue head.
+template <typename V, typename E, typename R>
+__device__ void apply_window(push_args<V, E, R> const& sa, int64_t win)
+{
+  __shared__ double sm[kPushThreads / 64];
+  __shared__ int s_last;
+  auto const& a     = sa.a;
+  double const base = a.st->base;
+  double const pf   = a.st->pers_factor;
+  double my_diff = 0, my_dang = 0;
+  int64_t const v0 = win * kWin;
+  int64_t const v1 = v0 + kWin < a.nv ? v0 + kWin : a.nv;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += kPushThreads) {
+    unsigned long long f = __hip_atomic_load(sa.acc + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f) __hip_atomic_store(sa.acc + v, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
+  }
+  double const bd = block_sum_push(my_diff, sm);
+  double const bg = block_sum_push(my_dang, sm);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(sa.win_done + win, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.partials[2 * win], bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.partials[2 * win + 1], bg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(&a.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last     = (t == (unsigned)sa.nwin - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double d = 0, g = 0;
+  for (int64_t w = threadIdx.x; w < sa.nwin; w += kPushThreads) {
+    d += __hip_atomic_load(&a.partials[2 * w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g += __hip_atomic_load(&a.partials[2 * w + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  d = block_sum_push(d, sm);
+  g = block_sum_push(g, sm);
+  if (threadIdx.x == 0) {
+    update_state<V, E, R>(a, d, g, true);
+    // no block takes tiles from the next head during this launch
+    __hip_atomic_store(sa.tile_ctr_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The push (default): persistent blocks take tiles -- runs of at most kTileUnits
+// units of one (source segment, window) -- from a queue in unit order.  A tile's
+// units are summed into the LDS window and flushed once.  The queue balances the
+// unequal cost of units (hub-source units gather from few lines, tail units from
+// many), which a static split cannot (0.221 vs 0.227 ms/iteration).  The unit body is
+// branch-free (masked lanes load x~[base] and add 0; the next unit of the tile is
+// always prefetched, the last re-reading itself), so the only waits are "gathers
+// done" and "prefetch done".  FUSED: the apply runs per window inside this kernel
+// (apply_window) instead of as k_pr_apply.
+template <typename V, typename E, typename R, bool WEIGHTED, bool FUSED = false>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push_q(push_args<V, E, R> sa)
 {
   __shared__ unsigned long long acc[kWin];
   __shared__ int s_tile;
+  __shared__ int s_fin;
   if (sa.a.st->done) return;
   int const tid = threadIdx.x;
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
@@ -568,53 +647,66 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_q(push_args<V, E, R> s
     int64_t const t = s_tile;
     if (t >= sa.ntiles) break;  // uniform
     int64_t const ua = sa.tiles[t], ub = sa.tiles[t + 1];
-    int64_t const win = units[ua].win;
-    int64_t k0   = units[ua].k0;
-    int n        = (int)(units[ua].k1 - k0);
-    int64_t base = units[ua].base;
-    uint32_t ent[kPerThread];
-    R w[kPerThread];
+    int64_t const win = sa.tile_win[t];
+    if (ua < ub) {  // uniform; empty tiles stand for windows without entries
+      int64_t k0   = units[ua].k0;
+      int n        = (int)(units[ua].k1 - k0);
+      int64_t base = units[ua].base;
+      uint32_t ent[kPerThread];
+      R w[kPerThread];
 #pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent (and ew) are padded by a unit
-      if constexpr (WEIGHTED) w[j] = nt_load(sa.ew + k0 + j * kPushThreads + tid);
+      for (int j = 0; j < kPerThread; ++j) {
+        ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent (and ew) are padded by a unit
+        if constexpr (WEIGHTED) w[j] = nt_load(sa.ew + k0 + j * kPushThreads + tid);
+      }
+      for (int64_t un = ua; un < ub; ++un) {
+        R const* const xb = x + base;
+        R xv[kPerThread];
+#pragma unroll
+        for (int j = 0; j < kPerThread; ++j) {
+          bool const ok = j * kPushThreads + tid < n;
+          xv[j]         = xb[ok ? (ent[j] >> kWinBits) : 0u];
+          xv[j]         = ok ? xv[j] : R(0);
+        }
+        int64_t const nx  = un + 1 < ub ? un + 1 : un;
+        int64_t const k0n = units[nx].k0;
+        int const nn      = (int)(units[nx].k1 - k0n);
+        int64_t const bsn = units[nx].base;
+        uint32_t ent_n[kPerThread];
+        R w_n[kPerThread];
+#pragma unroll
+        for (int j = 0; j < kPerThread; ++j) {
+          ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
+          if constexpr (WEIGHTED) w_n[j] = nt_load(sa.ew + k0n + j * kPushThreads + tid);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
+#pragma unroll
+        for (int j = 0; j < kPerThread; ++j) {
+          double v = (double)xv[j];
+          if constexpr (WEIGHTED) v *= (double)w[j];
+          atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
+        }
+#pragma unroll
+        for (int j = 0; j < kPerThread; ++j) {
+          ent[j] = ent_n[j];
+          if constexpr (WEIGHTED) w[j] = w_n[j];
+        }
+        n    = nn;
+        base = bsn;
+      }
+      flush_window<V, E, R>(sa, acc, win);  // ends with a barrier: s_tile may be rewritten
     }
-    for (int64_t un = ua; un < ub; ++un) {
-      R const* const xb = x + base;
-      R xv[kPerThread];
-#pragma unroll
-      for (int j = 0; j < kPerThread; ++j) {
-        bool const ok = j * kPushThreads + tid < n;
-        xv[j]         = xb[ok ? (ent[j] >> kWinBits) : 0u];
-        xv[j]         = ok ? xv[j] : R(0);
+    if constexpr (FUSED) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's flush atomics are performed
+      __syncthreads();
+      if (tid == 0) {
+        unsigned d = __hip_atomic_fetch_add(sa.win_done + win, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_fin      = (d + 1 == sa.win_tiles[win]);
       }
-      int64_t const nx  = un + 1 < ub ? un + 1 : un;
-      int64_t const k0n = units[nx].k0;
-      int const nn      = (int)(units[nx].k1 - k0n);
-      int64_t const bsn = units[nx].base;
-      uint32_t ent_n[kPerThread];
-      R w_n[kPerThread];
-#pragma unroll
-      for (int j = 0; j < kPerThread; ++j) {
-        ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
-        if constexpr (WEIGHTED) w_n[j] = nt_load(sa.ew + k0n + j * kPushThreads + tid);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
-#pragma unroll
-      for (int j = 0; j < kPerThread; ++j) {
-        double v = (double)xv[j];
-        if constexpr (WEIGHTED) v *= (double)w[j];
-        atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
-      }
-#pragma unroll
-      for (int j = 0; j < kPerThread; ++j) {
-        ent[j] = ent_n[j];
-        if constexpr (WEIGHTED) w[j] = w_n[j];
-      }
-      n    = nn;
-      base = bsn;
+      __syncthreads();
+      if (s_fin) apply_window<V, E, R>(sa, win);  // uniform
+      __syncthreads();  // s_tile / s_fin are rewritten next
     }
-    flush_window<V, E, R>(sa, acc, win);  // ends with a barrier: s_tile may be rewritten
   }
 }
 
@@ -818,18 +910,41 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     auto hu = to_host(pp.units.data<push_unit>(), nunits, s);
     std::vector<int64_t> tiles;
     // hub windows hold millions of entries: a tile is at most kTileUnits units
+    std::vector<int32_t> twin;
+    std::vector<uint32_t> wt(nwin, 0u);
     for (int64_t u = 0; u < nunits; ++u)
-      if (u == 0 || hu[u].win != hu[u - 1].win || hu[u].seg != hu[u - 1].seg || u - tiles.back() >= kTileUnits)
+      if (u == 0 || hu[u].win != hu[u - 1].win || hu[u].seg != hu[u - 1].seg || u - tiles.back() >= kTileUnits) {
         tiles.push_back(u);
+        twin.push_back(hu[u].win);
+        ++wt[hu[u].win];
+      }
     tiles.push_back(nunits);
+    // every window gets at least one (possibly empty) tile, so the fused apply
+    // of k_pr_push_q reaches every vertex
+    for (int64_t w = 0; w < nwin; ++w)
+      if (!wt[w]) {
+        tiles.push_back(nunits);
+        twin.push_back((int32_t)w);
+        wt[w] = 1;
+      }
     pp.ntiles = (int64_t)tiles.size() - 1;
     pp.tiles.set_stream(s);
     pp.tiles.resize(tiles.size() * sizeof(int64_t));
     to_device(pp.tiles.data<int64_t>(), tiles.data(), tiles.size(), s);
+    pp.tile_win.set_stream(s);
+    pp.tile_win.resize(twin.size() * sizeof(int32_t));
+    to_device(pp.tile_win.data<int32_t>(), twin.data(), twin.size(), s);
+    pp.win_tiles.set_stream(s);
+    pp.win_tiles.resize(wt.size() * sizeof(uint32_t));
+    to_device(pp.win_tiles.data<uint32_t>(), wt.data(), wt.size(), s);
   }
+  pp.nwin = nwin;
+  pp.win_done.set_stream(s);
+  pp.win_done.resize(std::max<int64_t>(nwin, 1) * sizeof(uint32_t));
+  HIP_CHECK(hipMemsetAsync(pp.win_done.data(), 0, std::max<int64_t>(nwin, 1) * sizeof(uint32_t), s));
   pp.tile_ctr.set_stream(s);
-  pp.tile_ctr.resize(sizeof(unsigned int));
-  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, sizeof(unsigned int), s));
+  pp.tile_ctr.resize(2 * sizeof(unsigned int));
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, 2 * sizeof(unsigned int), s));
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -918,7 +1033,23 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.tiles    = pp.tiles.data<int64_t>();
   sa.ntiles   = pp.ntiles;
   sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
-  if (sa.tile_ctr) HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, sizeof(unsigned int), s));
+  sa.tile_win = pp.tile_win.data<int32_t>();
+  sa.win_tiles = pp.win_tiles.data<uint32_t>();
+  sa.win_done  = pp.win_done.data<unsigned int>();
+  sa.nwin      = pp.nwin;
+  sa.tile_ctr_next = sa.tile_ctr ? sa.tile_ctr + 1 : nullptr;
+  if (sa.tile_ctr) HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, 2 * sizeof(unsigned int), s));
+  if (sa.win_done) HIP_CHECK(hipMemsetAsync(sa.win_done, 0, std::max<int64_t>(pp.nwin, 1) * sizeof(unsigned int), s));
+}
+
+// Fused apply (k_pr_push_q<..., FUSED>) for single-GPU queue runs, opt-in with
+// CGX_PR_FUSED=1.  Same results, but slower on RMAT-22 (0.211 vs 0.205 ms/iteration,
+// same-box A/B): the per-tile drain, barriers and window-counter atomic cost more
+// than the separate k_pr_apply launch (~25 us) they remove.
+inline bool fused_apply_enabled()
+{
+  char const* e = std::getenv("CGX_PR_FUSED");
+  return e && std::string(e) == "1";
 }
 
 template <typename V, typename E, typename R>
@@ -1009,7 +1140,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   // iteration state
   int const nblk_iter = (int)adj.num_items;
   int const nblk_init = (int)grid_for(nv, kBlock, 1024);
-  dbuf<double> partials(2 * std::max({nblk_iter, nblk_init, 2048}), s);
+  dbuf<double> partials(2 * std::max<int64_t>({nblk_iter, nblk_init, 2048, (nv + kWin - 1) / kWin}), s);
   dbuf<pr_state> st(1, s);
   HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(pr_state), s));
   dbuf<R> xa(nv, s), xb(nv, s);
@@ -1068,6 +1199,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     nblk_push  = (int)std::min<int64_t>(pmode == kPushQueue ? sa.ntiles : sa.nunits, 256 * 2);
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
+  bool const fused = push && pmode == kPushQueue && nblk_push > 0 && fused_apply_enabled();
+  auto fkernel     = g.weighted ? k_pr_push_q<V, E, R, true, true> : k_pr_push_q<V, E, R, false, true>;
   // Chunked enqueue: 16 iterations per host check (RMAT-22 converges in 16).
   // Profiling records one pair of pooled HIP events around each chunk -- an event
   // between every two iterations cost a ~10 us queue gap per iteration -- and
@@ -1091,8 +1224,14 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       a.x_out = bufs[(launched + 1) & 1];
       if (push) {
         sa.a = a;
-        if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
-        hipLaunchKernelGGL(akernel, dim3(nblk_apply), dim3(kBlock), 0, s, sa);
+        if (fused) {  // queue heads alternate: the launch resets the one the next uses
+          sa.tile_ctr      = adj.pr.tile_ctr.data<unsigned int>() + (launched & 1);
+          sa.tile_ctr_next = adj.pr.tile_ctr.data<unsigned int>() + ((launched + 1) & 1);
+          hipLaunchKernelGGL(fkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
+        } else {
+          if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
+          hipLaunchKernelGGL(akernel, dim3(nblk_apply), dim3(kBlock), 0, s, sa);
+        }
       } else {
         hipLaunchKernelGGL(kernel, dim3(nblk_iter), dim3(kBlock), 0, s, a);
       }

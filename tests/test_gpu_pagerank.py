@@ -187,3 +187,21 @@ def test_encoded_push_bitwise_equals_plain(scale, monkeypatch):
     r_enc = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
     assert h.last_iterations() == it_plain
     assert np.array_equal(r_enc, r_plain)
+
+
+@pytest.mark.parametrize("scale,weighted", [(12, False), (20, False), (16, True)])
+def test_fused_apply_equals_split(scale, weighted, monkeypatch):
+    """The opt-in fused apply (pagerank.hip apply_window inside k_pr_push_q,
+    CGX_PR_FUSED=1) updates every vertex from the same fixed-point sums as
+    k_pr_apply: same ranks bit for bit (only the L1-difference summation order
+    differs, so the iteration count is compared too)."""
+    s, d, w = rmat_graph(scale, weighted, True)
+    h, G = make_graph(s, d, w, transposed=True, renumber=True, symmetric=True)
+    r_split = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    it_split = h.last_iterations()
+    monkeypatch.setenv("CGX_PR_FUSED", "1")
+    r_fused = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    assert h.last_iterations() == it_split
+    assert np.array_equal(r_fused, r_split)
+    r_again = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    assert np.array_equal(r_again, r_fused)
