@@ -218,6 +218,22 @@ __device__ __forceinline__ uint32_t encode_fixed(float x);
 // ENC: x~' is stored as its fixed-point word (encode_fixed) instead of the fp32
 // value -- the form the unweighted push kernel gathers
 template <typename V, typename E, typename R, bool ENC = false>
+__device__ __forceinline__ void vertex_update_from(pr_args<V, E, R> const& a, V v, double s, R old, R ow, double base,
+                                                   double pf, double& my_diff, double& my_dang)
+{
+  double n = base + a.alpha * s;
+  if (a.pers) n += pf * (double)a.pers[v];
+  R nr     = (R)n;
+  a.pr[v]  = nr;
+  my_diff += fabs((double)nr - (double)old);
+  R xv = R(0);
+  if (ow == R(0)) my_dang += (double)nr;
+  else xv = (R)((double)nr / (double)ow);
+  if constexpr (ENC) reinterpret_cast<uint32_t*>(a.x_out)[v] = encode_fixed(xv);
+  else a.x_out[v] = xv;
+}
+
+template <typename V, typename E, typename R, bool ENC = false>
 __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, double s, double base, double pf,
                                               double& my_diff, double& my_dang)
 {
@@ -322,6 +338,9 @@ constexpr int kPerThread   = CGX_PER_THREAD;  // entries per thread per unit
 constexpr int kPushUnit    = kPerThread * kPushThreads;
 #ifndef CGX_TILE_UNITS
 #define CGX_TILE_UNITS 8  // 8: 0.221, 16: 0.222, 32: 0.229, 64: 0.241 ms/iteration (RMAT-22)
+#endif
+#ifndef CGX_APPLY_BATCH
+#define CGX_APPLY_BATCH 4
 #endif
 constexpr int kTileUnits   = CGX_TILE_UNITS;  // units per queue tile at most (one LDS flush per tile)
 constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
@@ -719,7 +738,28 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
   double const base = a.st->base;
   double const pf   = a.st->pers_factor;
   double my_diff = 0, my_dang = 0;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < a.nv; v += (int64_t)gridDim.x * blockDim.x) {
+  int64_t const stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t v            = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // kApplyBatch vertices per thread with all loads issued before the first store
+  // (pr and outw may alias as far as the compiler knows, which serialises the plain loop)
+  constexpr int kApplyBatch = CGX_APPLY_BATCH;
+  for (; v + (kApplyBatch - 1) * stride < a.nv; v += kApplyBatch * stride) {
+    unsigned long long f[kApplyBatch];
+    R old[kApplyBatch], ow[kApplyBatch];
+#pragma unroll
+    for (int j = 0; j < kApplyBatch; ++j) {
+      f[j]   = sa.acc[v + j * stride];
+      old[j] = a.pr[v + j * stride];
+      ow[j]  = a.outw[v + j * stride];
+    }
+#pragma unroll
+    for (int j = 0; j < kApplyBatch; ++j) {
+      if (f[j]) sa.acc[v + j * stride] = 0ull;
+      vertex_update_from<V, E, R, ENC>(a, (V)(v + j * stride), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j],
+                                       base, pf, my_diff, my_dang);
+    }
+  }
+  for (; v < a.nv; v += stride) {
     unsigned long long f = sa.acc[v];
     if (f) sa.acc[v] = 0ull;
     vertex_update<V, E, R, ENC>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
