@@ -669,11 +669,19 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     long long const td_cap = std::getenv("CGX_BFS_TD_CAP") ? std::atoll(std::getenv("CGX_BFS_TD_CAP")) : 1024;
     unsigned const probe_grid = std::getenv("CGX_BFS_PROBE_GRID") ? (unsigned)std::atoi(std::getenv("CGX_BFS_PROBE_GRID"))
                                                                   : 1024u;
+    // Direction switch thresholds (Beamer's form).  Our bottom-up is cheap per edge
+    // (hub-first adjacency, early exit), so it pays to stay top-down longer and
+    // bottom-up longer than Beamer's alpha 14 / beta 24.  RMAT-24 harmonic-mean MTEPS
+    // (alpha, beta): (4, 24) 135K; (14, 24) 211K; (14, 64) 218K; (40, 24) 224K;
+    // (40, 64) 226K; (80, 64) 223K; (80, 128) 225K; (150, 64) 209K.
+    // Env overrides are measurement only.
+    double const alpha_do = std::getenv("CGX_BFS_ALPHA") ? std::atof(std::getenv("CGX_BFS_ALPHA")) : 40.0;
+    double const beta_do  = std::getenv("CGX_BFS_BETA") ? std::atof(std::getenv("CGX_BFS_BETA")) : 64.0;
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
-        if (!bottom_up && (double)m_f > (double)m_u / 14.0) bottom_up = true;
-        else if (bottom_up && (double)n_f < (double)nv / 24.0) bottom_up = false;
+        if (!bottom_up && (double)m_f > (double)m_u / alpha_do) bottom_up = true;
+        else if (bottom_up && (double)n_f < (double)nv / beta_do) bottom_up = false;
       }
       a.depth = depth;
       zero_ctr();
