@@ -223,10 +223,12 @@ __global__ void k_has_edges(int64_t const* off, int64_t n, uint8_t* has)
 }
 
 // contraction
-__global__ void k_pair_keys(uint32_t const* src, uint32_t const* dst, uint32_t const* lab, int64_t ne, u64* keys)
+// compact pair key label(u) << cb | label(v) (cb = label bits; see k_sweep_keys)
+__global__ void k_pair_keys(uint32_t const* src, uint32_t const* dst, uint32_t const* lab, int64_t ne, int cb,
+                            u64* keys)
 {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
-    keys[e] = ((u64)lab[src[e]] << 32) | (u64)lab[dst[e]];
+    keys[e] = ((u64)lab[src[e]] << cb) | (u64)lab[dst[e]];
 }
 
 __global__ void k_mark_used(uint32_t const* lab, int64_t nv, uint32_t* used)
@@ -276,17 +278,20 @@ __global__ void k_new_ids(uint32_t const* nmap, int64_t n, uint32_t* new_of_labe
     new_of_label[nmap[i]] = (uint32_t)i;
 }
 
-__global__ void k_relabel_pairs(u64 const* keys, int64_t n, uint32_t const* nl, u64* out)
+// (l(u) << 32 | l(v)) -> compact (new(l(u)) << cb | new(l(v)))
+__global__ void k_relabel_pairs(u64 const* keys, int64_t n, uint32_t const* nl, int cb, u64* out)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = ((u64)nl[(uint32_t)(keys[i] >> 32)] << 32) | (u64)nl[(uint32_t)keys[i]];
+    out[i] = ((u64)nl[(uint32_t)(keys[i] >> 32)] << cb) | (u64)nl[(uint32_t)keys[i]];
 }
 
-__global__ void k_split_pairs(u64 const* keys, int64_t n, uint32_t* s, uint32_t* d)
+// key = s << cb | d (cb = 32 for the plain form)
+__global__ void k_split_pairs(u64 const* keys, int64_t n, uint32_t* s, uint32_t* d, int cb)
 {
+  u64 const mask = cb >= 64 ? ~0ull : (1ull << cb) - 1;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    s[i] = (uint32_t)(keys[i] >> 32);
-    d[i] = (uint32_t)keys[i];
+    s[i] = (uint32_t)(keys[i] >> cb);
+    d[i] = (uint32_t)(keys[i] & mask);
   }
 }
 
@@ -436,13 +441,15 @@ level_graph contract(louvain_state& S, level_graph const& g, uint32_t* labels)
   dbuf<double> w2(std::max<int64_t>(ne, 1), s), cw(std::max<int64_t>(ne, 1), s);
   int64_t nce = 0;
   if (ne) {
-    hipLaunchKernelGGL(k_pair_keys, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), labels, ne,
+    int const cb = bits_for((unsigned long long)std::max<int64_t>(nv - 1, 0));
+    hipLaunchKernelGGL(k_pair_keys, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), labels, ne, cb,
                        keys.data());
     CGX_LAUNCH_CHECK();
-    radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0,
-                                  32 + bits_for(nv - 1), s);
+    radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0, 2 * cb, s);
     nce = reduce_by_key(keys2.data(), w2.data(), (size_t)ne, keys.data(), cw.data(), rocprim::plus<double>(),
                         rocprim::equal_to<u64>(), s);
+    hipLaunchKernelGGL(k_expand_keys, dim3(blocks(nce)), dim3(kBlock), 0, s, keys.data(), nce, cb);
+    CGX_LAUNCH_CHECK();
   }
   // used labels (ascending) and their coarse out-degrees
   dbuf<uint32_t> used(nv + 1, s), pos(nv + 1, s), deg(nv, s);
@@ -472,13 +479,13 @@ level_graph contract(louvain_state& S, level_graph const& g, uint32_t* labels)
   out.dst.resize(std::max<int64_t>(nce, 1), s);
   out.w.resize(std::max<int64_t>(nce, 1), s);
   if (nce) {
-    hipLaunchKernelGGL(k_relabel_pairs, dim3(blocks(nce)), dim3(kBlock), 0, s, keys.data(), nce, nl.data(),
+    int const cb2 = bits_for((unsigned long long)std::max<int64_t>(nu - 1, 0));
+    hipLaunchKernelGGL(k_relabel_pairs, dim3(blocks(nce)), dim3(kBlock), 0, s, keys.data(), nce, nl.data(), cb2,
                        keys2.data());
     CGX_LAUNCH_CHECK();
-    radix_sort_pairs<u64, double>(keys2.data(), keys.data(), cw.data(), out.w.data(), (size_t)nce, 0,
-                                  32 + bits_for(nu - 1), s);
+    radix_sort_pairs<u64, double>(keys2.data(), keys.data(), cw.data(), out.w.data(), (size_t)nce, 0, 2 * cb2, s);
     hipLaunchKernelGGL(k_split_pairs, dim3(blocks(nce)), dim3(kBlock), 0, s, keys.data(), nce, out.src.data(),
-                       out.dst.data());
+                       out.dst.data(), cb2);
     CGX_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(k_gather_u32, dim3(blocks(nv)), dim3(kBlock), 0, s, nl.data(), labels, nv);
@@ -768,7 +775,7 @@ level_graph mg_level0(handle_t& h, graph_t& g)
     radix_sort_pairs<u64, double>(k1.data(), k2.data(), w1.data(), out.w.data(), (size_t)m, 0,
                                   32 + bits_for(std::max<int64_t>(out.nrows - 1, 0)), s);
     hipLaunchKernelGGL(k_split_pairs, dim3(blocks(m)), dim3(kBlock), 0, s, k2.data(), m, out.src.data(),
-                       out.dst.data());
+                       out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
   }
   return out;
@@ -860,7 +867,7 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, s
     radix_sort_pairs<u64, double>(mk2.data(), mk.data(), mw.data(), out.w.data(), (size_t)nm, 0,
                                   32 + bits_for(std::max<int64_t>(nu - 1, 0)), s);
     hipLaunchKernelGGL(k_split_pairs, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, out.src.data(),
-                       out.dst.data());
+                       out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(k_gather_u32, dim3(blocks(nv)), dim3(kBlock), 0, s, nl.data(), lab, nv);
