@@ -199,7 +199,7 @@ __global__ void k_init_sources(V const* src_global, size_t n, int64_t lo, int64_
 template <typename V>
 __global__ void k_td_candidates(uint32_t const* frontier, int64_t nf, unsigned long long const* pre, int64_t m,
                                 int64_t const* off, uint32_t const* idx, int64_t lo, int64_t hi, V const* dist,
-                                unsigned long long* out)
+                                int gb, unsigned long long* out)
 {
   V const INF = std::numeric_limits<V>::max();
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
@@ -213,7 +213,9 @@ __global__ void k_td_candidates(uint32_t const* frontier, int64_t nf, unsigned l
     int64_t e     = off[u] + (t - (int64_t)pre[a]);
     uint32_t v    = idx[e];
     bool visited  = (int64_t)v >= lo && (int64_t)v < hi && dist[(int64_t)v - lo] != INF;  // own: known locally
-    out[t]        = visited ? ~0ull : (((unsigned long long)v << 32) | (unsigned long long)(uint32_t)(lo + u));
+    // compact key v << gb | parent (gb = global id bits): the sort runs over 2 gb bits;
+    // the sentinel ~0 still sorts last (v = parent = 2^gb - 1 would be a visited self loop)
+    out[t]        = visited ? ~0ull : (((unsigned long long)v << gb) | (unsigned long long)(uint32_t)(lo + u));
   }
 }
 
@@ -240,8 +242,19 @@ __global__ void k_split_points(unsigned long long const* keys, int64_t n, int64_
 }
 
 struct same_v {
-  __host__ __device__ bool operator()(unsigned long long a, unsigned long long b) const { return (a >> 32) == (b >> 32); }
+  int gb;  // candidate keys are v << gb | parent
+  __host__ __device__ bool operator()(unsigned long long a, unsigned long long b) const { return (a >> gb) == (b >> gb); }
 };
+
+// compact candidate keys -> v << 32 | parent (the sentinel ~0 stays ~0)
+__global__ void k_expand_cand(unsigned long long* k, int64_t n, int gb)
+{
+  unsigned long long const mask = (1ull << gb) - 1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    unsigned long long const x = k[i];
+    if (x != ~0ull) k[i] = ((x >> gb) << 32) | (x & mask);
+  }
+}
 
 template <typename V>
 __global__ void k_td_claim(unsigned long long const* cand, int64_t n, int64_t lo, V const* dist, long long* best,
@@ -417,6 +430,7 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   V depth    = 0;
   bool bottom_up = false;
   size_t levels = 0, bu_steps = 0;
+  int const gb = bits_for((unsigned long long)std::max<int64_t>(g.num_vertices - 1, 0));  // candidate key bits
   while (nf > 0 && depth < limit) {
     if (dir_opt) {
       if (!bottom_up && m_f > m_u / 14.0) bottom_up = true;
@@ -454,15 +468,19 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       if (mcand) {
         hipLaunchKernelGGL(k_td_candidates<V>, dim3(blocks(mcand)), dim3(kBlock), 0, s, qa.data(), nf_own,
                            pre.data(), mcand, rows.off.data<int64_t>(), rows.idx.data<uint32_t>(), lo, hi, dist,
-                           cand.data());
+                           gb, cand.data());
         CGX_LAUNCH_CHECK();
-        radix_sort_keys<unsigned long long>(cand.data(), cs.data(), mcand, 0, 64, s);
+        radix_sort_keys<unsigned long long>(cand.data(), cs.data(), mcand, 0, 2 * gb, s);
         dbuf<size_t> cnt(1, s);
         size_t tmp = 0;
-        HIP_CHECK(rocprim::unique(nullptr, tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v(), s));
+        HIP_CHECK(rocprim::unique(nullptr, tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v{gb}, s));
         buffer t(tmp, s);
-        HIP_CHECK(rocprim::unique(t.data(), tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v(), s));
+        HIP_CHECK(rocprim::unique(t.data(), tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v{gb}, s));
         nu = (int64_t)to_host_scalar(cnt.data(), s);
+        if (nu) {
+          hipLaunchKernelGGL(k_expand_cand, dim3(blocks(nu)), dim3(kBlock), 0, s, cu.data(), nu, gb);
+          CGX_LAUNCH_CHECK();
+        }
       }
       // per-owner split points (the sentinel ~0 run, if any, sorts last and is dropped)
       std::vector<size_t> counts(P, 0);
