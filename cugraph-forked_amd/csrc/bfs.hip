@@ -492,12 +492,10 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
       my_m += (unsigned long long)deg;
     }
     unsigned long long const hm = __ballot(hit);
-    if ((lane & 31) == 0) {
+    if ((lane & 31) == 0 && in) {
       uint32_t const b = (uint32_t)(hm >> lane);  // this half-wave's word
-      if (b) {
-        a.vis[v >> 5] = vw | b;
-        a.nxt[v >> 5] = b;
-      }
+      if (b) a.vis[v >> 5] = vw | b;
+      a.nxt[v >> 5] = b;  // every word of nxt is written here: no memset before the probe
     }
     unsigned long long const mm = __ballot(more);
     if (mm) {
@@ -707,8 +705,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           CGX_LAUNCH_CHECK();
           have_bitmap = true;
         }
-        HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));
-        if (a.order == nullptr && !one_pass_bu) {  // probe + residual (identity order)
+        bool const probe_path = a.order == nullptr && !one_pass_bu;
+        if (!probe_path) HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));  // the probe writes every word
+        if (probe_path) {  // probe + residual (identity order)
           hipLaunchKernelGGL((k_bu_probe<V, E>), dim3(grid_for((nv + 63) / 64, kBlock / 64, probe_grid)), dim3(kBlock),
                              0, s, a, qb[0].data());
           CGX_LAUNCH_CHECK();
