@@ -1,37 +1,43 @@
 #!/usr/bin/env python3
-"""Benchmark: PageRank edges/s (+ BFS MTEPS) on Graph500 R-MAT, MI355X.
+"""Benchmark: PageRank edges/s + BFS MTEPS on Graph500 R-MAT scale 24, MI355X.
 
 BASELINE.json metric: "PageRank edges/sec + BFS MTEPS on RMAT-24 at 1/2/4/8 MI355X".
-Workload at N=1 (configs[1]): RMAT scale-22, symmetrised + deduplicated,
-unweighted, fp32 PageRank, alpha 0.85, epsilon 1e-6.  A "step" is one complete
-``cugraph_pagerank`` call (power iteration to convergence) on the resident graph.
-value = stored edges x PageRank iterations x steps / timed seconds (whole job).
+Headline (``value``): PageRank on RMAT scale-24 -- symmetrised + deduplicated,
+unweighted, fp32, alpha 0.85, epsilon 1e-6 -- on the resident graph.  A "step" is
+one complete ``cugraph_pagerank`` call (power iteration to convergence).
+value = stored edges x PageRank iterations x steps / timed seconds (whole job; the
+same graph at every N, so ``scaling`` is "strong").
 
 Extra fields on the same JSON line:
-  roofline      -- the PageRank iteration kernels: algorithmic bytes/iteration
-                   (4E + 16V) / average iteration time from HIP events recorded
-                   around each 16-iteration chunk on the library's stream during
-                   the timed region (divided by the iterations run); peak 8 TB/s
-                   (MI355X_MICROARCH.md).
-  cpu_baseline  -- NetworkX's PageRank loop (scipy CSR, fp64, 1 core;
-                   oracle/baseline.py) for a few iterations on the SAME graph.
-  bfs           -- configs[2]: RMAT scale-24 BFS MTEPS (Graph500 counting), when
-                   the BFS path is available.
-  louvain       -- configs[4]: Louvain time-to-solution, modularity and levels on
-                   RMAT scale 23 + log2(N) (scale 26 at 8 GPUs), uniform weights.
-  bfs.cpu_baseline / louvain.cpu_baseline -- the reference's NetworkX CPU path
-                   (nx.single_source_shortest_path_length, nx louvain_communities)
-                   on bounded R-MAT samples (RMAT-16 / RMAT-14; NetworkX cannot
-                   hold the benchmark graphs), N=1 only.
+  roofline         -- the PageRank iteration: algorithmic bytes/iteration 4E + 16V
+                       / average iteration time from HIP events
+                      recorded on the library's stream around each chunk of
+                      iterations in the timed region; peak 8 TB/s; traffic = HBM
+                      bytes per iteration from rocprofv3 PMC passes; copy_ceiling =
+                      a measured 16-B-per-lane copy kernel (ext.h).
+  cpu_baseline     -- (N=1) NetworkX's PageRank loop restated on scipy (the port of
+                      nx.pagerank's _pagerank_scipy, fp64, 1 core) on the SAME
+                      RMAT-24 graph for a few iterations; plus the compiled C
+                      restatement of the reference CPU reference (1 thread and
+                      OpenMP), nx.pagerank itself on the largest sample that stays
+                      bounded, and the host's core count.
+  pagerank_rmat22  -- (N=1) configs[1]: the same measurement on RMAT-22.
+  pagerank_rmat26  -- (N=8) configs[3]: RMAT-26 on the 2D partition.
+  pagerank_alt_grid-- (N>1) the headline graph on the other R x C grid (1 x P).
+  bfs              -- configs[2]: RMAT-24 BFS, Graph500 MTEPS (harmonic mean over
+                      8 roots), its roofline (4E_cc + 16V_cc per traversal) and PMC
+                      traffic, and CPU baselines (NetworkX on a bounded sample,
+                      compiled C restatement on the same graph).
+  louvain          -- configs[4]: Louvain time-to-solution on RMAT 23 + log2(N)
+                      (RMAT-26 at 8 GPUs), uniform weights.
 
-Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU):
-weak scaling, R-MAT scale 22 + log2(N) for PageRank (the headline value); the
-BFS leg stays on RMAT-24 at every N as BASELINE.json names it.  Every rank generates
-and deduplicates the same edge list, keeps its 1/N slice, and the MG graph is
-built collectively (cugraph_mg_graph_create: hash owners, degree renumbering, 2D
-R x C edge blocks); PageRank and BFS then run over RCCL communicators created
-inside libcugraph_c (pylibcugraph.comms.init_rccl).  torch.distributed (gloo)
-is only used for the RCCL unique id, the timing barrier and the max over ranks.
+Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU): every
+rank generates the same edge list, keeps its 1/N slice, and the MG graph is built
+collectively (cugraph_mg_graph_create: hash owners, degree renumbering, 2D R x C
+edge blocks, R x C = the reference's grid by default); PageRank and BFS run over
+RCCL communicators created inside libcugraph_c (pylibcugraph.comms.init_rccl).
+torch.distributed (gloo) carries only the RCCL unique id, the timing barrier and
+the max over ranks.
 """
 from __future__ import annotations
 
@@ -52,6 +58,13 @@ sys.path.insert(0, os.path.join(ROOT, "cugraph-forked_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BFS_KERNELS = ("k_topdown", "k_bu_probe", "k_bu_residual", "k_bottomup", "k_mark_queues", "k_bitmap_to_queues",
+               "k_bfs_init_sources", "k_finish_pred", "k_sources_to_bitmap", "k_bfs_")
+PR_KERNELS = ("k_pr_push", "k_pr_apply")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
 
 
 def release_caches(p):
@@ -62,10 +75,60 @@ def release_caches(p):
     torch.cuda.empty_cache()
 
 
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+def barrier(args):
+    if args.world > 1:
+        import torch.distributed as dist
+        dist.barrier()
 
 
+def _allreduce(args, v, op):
+    if args.world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    x = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(x, op=op)
+    return float(x[0])
+
+
+def max_over_ranks(args, t):
+    import torch.distributed as dist
+    return _allreduce(args, t, dist.ReduceOp.MAX) if args.world > 1 else t
+
+
+def sum_over_ranks(args, v):
+    import torch.distributed as dist
+    return _allreduce(args, v, dist.ReduceOp.SUM) if args.world > 1 else v
+
+
+def host_info(threads):
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "model": model, "threads_used": threads}
+
+
+def omp_threads():
+    """Threads for the OpenMP baseline: the process's CPU share (16 on a one-GPU box:
+    OMP_NUM_THREADS is set there), never more than the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, env if env > 0 else 16))
+
+
+# ----------------------------------------------------------------------------- graphs
 def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want_roots=0, mg=None):
     """Device R-MAT -> symmetrise + dedup (cugraph.Graph preprocessing) -> graph.
     mg = (rank, world): every rank makes the same edge list and passes its slice to
@@ -91,96 +154,192 @@ def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want
         if want_roots:
             deg = torch.bincount(s.to(torch.int64), minlength=1 << scale)  # degree by external id
         lo, hi = rank * E // world, (rank + 1) * E // world
-        sl = slice(lo, hi)
-        g = p.MGGraph(h, props, s[sl].contiguous(), d[sl].contiguous(), None if w is None else w[sl].contiguous(),
-                      store_transposed=transposed, num_edges=E)
+        g = p.MGGraph(h, props, s[lo:hi].contiguous(), d[lo:hi].contiguous(),
+                      None if w is None else w[lo:hi].contiguous(), store_transposed=transposed, num_edges=E)
     del s, d, w
     torch.cuda.synchronize()
     return g, roots, deg
 
 
-def pagerank_leg(p, args):
+# ----------------------------------------------------------------------------- PageRank
+def pagerank_leg(p, args, scale, steps, warmup, ctx=None):
     import torch
-    h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
+    h = p.ResourceHandle(ctx.ptr if ctx else None)
+    barrier(args)
     t0 = time.perf_counter()
-    g, _, _ = build_rmat_graph(p, h, args.scale, mg=args.mg)
-    build_s = time.perf_counter() - t0
+    g, _, _ = build_rmat_graph(p, h, scale, mg=args.mg)
+    build_s = max_over_ranks(args, time.perf_counter() - t0)
     V, E = g.number_of_vertices(), g.number_of_edges()
-    log(f"[bench] RMAT-{args.scale}: V={V} E={E} (build {build_s:.2f}s)")
-    for _ in range(args.warmup):
+    log(f"[bench] pagerank RMAT-{scale}: V={V} E={E} (build {build_s:.2f}s)")
+    for _ in range(warmup):
         p.pagerank(h, g, None, None, None, None, args.alpha, args.epsilon, 500, False)
     torch.cuda.synchronize()
-    times, iters, kms, klaunch = [], [], 0.0, 0
+    iters, kms, klaunch = [], 0.0, 0
     h.set_profiling(True)
     barrier(args)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         p.pagerank(h, g, None, None, None, None, args.alpha, args.epsilon, 500, False)
         iters.append(h.last_iterations())
         kms += h.last_hot_kernel_ms()
         klaunch += h.last_hot_kernel_launches()
     torch.cuda.synchronize()
     barrier(args)
-    t = time.perf_counter() - t0
+    t = max_over_ranks(args, time.perf_counter() - t0)
     h.set_profiling(False)
-    it_total = sum(iters)
-    value = E * it_total / t
-    # algorithmic bytes of one rank's share: 4E/N + 16V/N
+    value = E * sum(iters) / t
+    # algorithmic bytes of one rank's share: (4E + 16V) / N
     bytes_per_iter = (4 * E + 16 * V) / args.world
     avg_ms = kms / max(klaunch, 1)
     achieved = bytes_per_iter / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    log(f"[bench] pagerank RMAT-{scale}: {value:.4g} edges/s, iters {iters}, {avg_ms:.4f} ms/iter, "
+        f"{achieved:.1f} GB/s algorithmic")
     return dict(h=h, g=g, V=V, E=E, t=t, iters=iters, value=value, avg_ms=avg_ms, achieved=achieved,
-                bytes_per_iter=bytes_per_iter, build_s=build_s)
+                bytes_per_iter=bytes_per_iter, build_s=build_s, scale=scale, steps=steps)
 
 
-def cpu_baseline_leg(p, r, args):
-    from oracle.baseline import pagerank_scipy_iterations
-    off, idx, _ = r["g"].adjacency(r["h"], transposed=True)
-    off, idx = off.cpu().numpy(), idx.cpu().numpy()
-    t, eps = pagerank_scipy_iterations(off, idx, r["V"], iterations=args.cpu_iters)
-    return {"value": eps, "unit": "edges/s", "cores": 1, "kind": "port",
-            "sample": f"{args.cpu_iters} NetworkX-style scipy power iterations (fp64, 1 thread) on the same "
-                      f"RMAT-{args.scale} graph ({t:.1f}s); graph build excluded as on the GPU"}
+def pagerank_summary(r, args, grid=None):
+    """The JSON object of one PageRank leg (secondary legs)."""
+    return {"scale": r["scale"], "vertices": r["V"], "edges": r["E"], "value": r["value"], "unit": "edges/s",
+            "ms_per_step": r["t"] / r["steps"] * 1e3, "iterations": r["iters"],
+            "graph_build_s": round(r["build_s"], 3), "grid": grid,
+            "roofline": {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": r["achieved"] / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": r["bytes_per_iter"],
+                         "avg_kernel_ms": r["avg_ms"]}}
 
 
-def traffic_leg(args):
-    """HBM bytes per PageRank iteration from PMC counters: a child process runs the
-    PageRank leg under ``rocprofv3 --pmc`` once per counter (FETCH_SIZE and
-    WRITE_SIZE cannot share a pass), MI355X_MICROARCH.md "HBM": bytes = 2 x
-    FETCH_SIZE (gfx950 tallies 128-B requests at 64 B) + WRITE_SIZE, both in KiB.
-    Launches after convergence (no-ops) are skipped."""
+# ----------------------------------------------------------------------------- PMC traffic
+def pmc_pass(ctr, child_args, kernels):
+    """One rocprofv3 --pmc pass over a child bench process; returns
+    {kernel-prefix: [values per launch]} in KiB (MI355X_MICROARCH.md: FETCH_SIZE /
+    WRITE_SIZE, one counter per pass since they cannot share one)."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
-        return None, "rocprofv3 not found"
-    per_iter = {}
+        raise RuntimeError("rocprofv3 not found")
     env = dict(os.environ, TMPDIR="/tmp")
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__)] + child_args
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                           timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(f"rocprofv3 {ctr} rc={r.returncode}: {r.stderr.decode()[-300:]}")
+        rows = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            rows += list(csv.DictReader(open(f)))
+    out = {k: [] for k in kernels}
+    for x in rows:
+        for k in kernels:
+            if k in x["Kernel_Name"]:
+                out[k].append(float(x["Counter_Value"]))
+                break
+    return out
+
+
+def pagerank_traffic(args):
+    """HBM bytes per PageRank iteration (k_pr_push + k_pr_apply): 2 x FETCH_SIZE
+    (gfx950 tallies 128-B requests at 64 B) + WRITE_SIZE, KiB -> bytes.  Launches
+    after convergence (no-ops) are skipped."""
+    per = {}
+    child = ["--traffic-child", "pagerank", "--scale", str(args.scale)]
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        with tempfile.TemporaryDirectory(dir="/tmp") as d:
-            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
-                   sys.executable, os.path.abspath(__file__), "--traffic-child", "--scale", str(args.scale),
-                   "--steps", "1", "--warmup", "0", "--no-bfs", "--no-cpu-baseline"]
-            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                               timeout=300)
-            if r.returncode != 0:
-                return None, f"rocprofv3 {ctr} rc={r.returncode}: {r.stderr.decode()[-300:]}"
-            rows = []
-            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-                rows += list(csv.DictReader(open(f)))
+        vals = pmc_pass(ctr, child, PR_KERNELS)
         tot = 0.0
-        for kern in ("k_pr_push", "k_pr_apply"):
-            vals = [float(x["Counter_Value"]) for x in rows if kern in x["Kernel_Name"]]
-            if not vals and kern == "k_pr_apply":
-                continue  # fused apply (default): the push kernel does it
-            if not vals:
-                return None, f"no {kern} launches under rocprofv3"
-            live = [v for v in vals if v > 0.01 * max(vals)]
+        for k, v in vals.items():
+            if not v:
+                if k == "k_pr_apply":
+                    continue
+                raise RuntimeError(f"no {k} launches under rocprofv3")
+            live = [x for x in v if x > 0.01 * max(v)]
             tot += sum(live) / len(live)
-        per_iter[ctr] = tot
-    return (2.0 * per_iter["FETCH_SIZE"] + per_iter["WRITE_SIZE"]) * 1024.0, per_iter
+        per[ctr] = tot
+    return (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0, per
 
 
-def bfs_leg(p, args):
+def bfs_traffic(args, traversals):
+    """HBM bytes per BFS traversal (all BFS kernels of the child's traversals)."""
+    per = {}
+    child = ["--traffic-child", "bfs", "--bfs-scale", str(args.bfs_scale), "--bfs-roots", str(args.bfs_roots)]
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        vals = pmc_pass(ctr, child, BFS_KERNELS)
+        per[ctr] = sum(sum(v) for v in vals.values()) / traversals
+    return (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0, per
+
+
+# ----------------------------------------------------------------------------- CPU baselines
+def pagerank_cpu_baseline(p, r, args):
+    """SURVEY.md §8d.  Primary: NetworkX's PageRank loop (_pagerank_scipy restated on
+    scipy, fp64, 1 core) on the same graph, a few iterations.  Secondary: the compiled
+    C restatement of the reference's CPU reference (1 thread, OpenMP) and nx.pagerank
+    itself on a bounded sample."""
+    import numpy as np
+    from oracle.baseline import networkx_pagerank, pagerank_scipy_iterations
+    off, idx, _ = r["g"].adjacency(r["h"], transposed=True)
+    off, idx = off.cpu().numpy().astype(np.int64), idx.cpu().numpy()
+    V, E = r["V"], r["E"]
+    t, eps = pagerank_scipy_iterations(off, idx, V, iterations=args.cpu_iters)
+    T = omp_threads()
+    out = {"value": eps, "unit": "edges/s", "cores": 1, "kind": "port",
+           "sample": f"{args.cpu_iters} NetworkX-style scipy power iterations (nx.pagerank's _pagerank_scipy loop, "
+                     f"fp64, 1 thread) on the same RMAT-{r['scale']} graph ({t:.1f}s); graph build excluded as on "
+                     "the GPU",
+           "host": host_info(T)}
+    try:
+        from oracle import cpu_native
+        t1, _ = cpu_native.pagerank(off, idx, args.cpu_iters, args.alpha, threads=1)
+        tn, _ = cpu_native.pagerank(off, idx, args.cpu_iters, args.alpha, threads=T)
+        out["compiled"] = {
+            "kind": "port", "source": "oracle/cpu_baseline.c (pagerank_test.cpp:43-130 restated, fp32)",
+            "single_thread": {"value": E * args.cpu_iters / t1, "unit": "edges/s", "cores": 1},
+            "openmp": {"value": E * args.cpu_iters / tn, "unit": "edges/s", "cores": T},
+            "sample": f"{args.cpu_iters} iterations on the same RMAT-{r['scale']} graph"}
+    except Exception as e:  # noqa: BLE001
+        out["compiled"] = {"error": repr(e)[:200]}
+    del off, idx
+    try:
+        sc = args.nx_pagerank_scale
+        tb, tp, ne, it = networkx_pagerank(sc, args.alpha, args.epsilon)
+        out["networkx"] = {"value": ne * it / tp, "unit": "edges/s", "cores": 1, "kind": "networkx",
+                           "seconds": tp, "iterations": it,
+                           "sample": f"nx.pagerank (networkx 3.4.2, tol=epsilon/N as nx defines it) to convergence "
+                                     f"on RMAT-{sc} symmetric ({ne} stored edges, the largest sample kept within "
+                                     f"the bench's time budget); nx.Graph build {tb:.1f}s excluded"}
+    except Exception as e:  # noqa: BLE001
+        out["networkx"] = {"error": repr(e)[:200]}
+    return out
+
+
+def networkx_cpu_legs(args):
+    """The reference's NetworkX CPU path for BFS and Louvain on bounded R-MAT samples
+    (same generator parameters, numpy twin), 1 core; NetworkX cannot hold the
+    benchmark graphs, so the sample scale is stated."""
+    import numpy as np
+    from oracle import graph as og
+    from oracle import rmat
+    from oracle.baseline import networkx_bfs, networkx_louvain
+    out = {}
+    sb = 16
+    s, d = rmat.rmat(sb, 16 << sb, seed=42)
+    s, d, _ = og.symmetrize_dedup(s, d, None)
+    root = int(s[0])
+    tb, t, e_cc = networkx_bfs(s, d, root)
+    out["bfs"] = {"value": (e_cc / t) / 1e6, "unit": "MTEPS", "cores": 1, "kind": "networkx",
+                  "sample": f"nx.single_source_shortest_path_length, networkx 3.4.2, RMAT-{sb} symmetric "
+                            f"({s.size} stored edges), 1 root; graph build {tb:.1f}s excluded"}
+    sl = 14
+    s, d = rmat.rmat(sl, 16 << sl, seed=42)
+    w = rmat.rmat_weights(s.size, seed=43).astype(np.float64)
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    tb, t, q = networkx_louvain(s, d, w)
+    out["louvain"] = {"value": t, "unit": "s", "cores": 1, "kind": "networkx", "modularity": q,
+                      "sample": f"nx.community.louvain_communities(seed=42) + modularity, networkx 3.4.2, "
+                                f"RMAT-{sl} symmetric uniform weights ({s.size} stored edges); build {tb:.1f}s excluded"}
+    return out
+
+
+# ----------------------------------------------------------------------------- BFS
+def bfs_leg(p, args, child=False):
     import torch
     h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
     scale = args.bfs_scale
@@ -189,10 +348,14 @@ def bfs_leg(p, args):
     if deg is None:  # SG: degrees from the CSR (internal order == result order)
         off, _, _ = g.adjacency(h, transposed=False)
         deg_int = (off[1:] - off[:-1]).to(torch.int64)
-    rates, stored, levels, bu, times = [], [], [], [], []
+    rates, stored, levels, bu, times, bytes_alg = [], [], [], [], [], []
+    number_map = None
     for r in roots:
         mine = [int(r)] if args.rank == 0 else []
         src = torch.tensor(mine, dtype=torch.int32, device="cuda")
+        if child:  # PMC pass: exactly one traversal per root
+            p.bfs(h, g, src.clone(), True, 0, True, False)
+            continue
         p.bfs(h, g, src.clone(), True, 0, True, False)  # warm
         torch.cuda.synchronize()
         barrier(args)
@@ -205,23 +368,59 @@ def bfs_leg(p, args):
         # Graph500 TEPS: undirected edges of the source's component = stored directed edges / 2
         if deg is None:
             e_cc = int(deg_int[reached].sum().item())
+            v_cc = int(reached.sum().item())
         else:
             e_cc = int(sum_over_ranks(args, float(deg[verts[reached].to(torch.int64)].sum().item())))
+            v_cc = int(sum_over_ranks(args, float(reached.sum().item())))
+        if number_map is None and deg is None:
+            number_map = verts.cpu().numpy()  # internal id -> external id (SG)
         times.append(t)
         levels.append(h.last_bfs_levels())
         bu.append(h.last_bfs_bottom_up_steps())
         rates.append((e_cc / 2) / t / 1e6)
         stored.append(e_cc / t / 1e6)
+        bytes_alg.append(4 * e_cc + 16 * v_cc)
+    if child:
+        return None
     hm = len(rates) / sum(1.0 / m for m in rates)
     hm_stored = len(stored) / sum(1.0 / m for m in stored)
-    return {"scale": scale, "vertices": V, "edges": E, "roots": len(rates),
-            "mteps_harmonic_mean": hm, "mteps_min": min(rates), "mteps_max": max(rates),
-            "stored_edge_mteps_harmonic_mean": hm_stored,
-            "ms_mean": 1e3 * sum(times) / len(times), "levels": levels, "bottom_up_steps": bu,
-            "direction_optimizing": True, "n_gpus": args.world,
-            "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)"}
+    achieved = sum(bytes_alg) / sum(times) / 1e9 / args.world
+    out = {"scale": scale, "vertices": V, "edges": E, "roots": len(rates),
+           "mteps_harmonic_mean": hm, "mteps_min": min(rates), "mteps_max": max(rates),
+           "stored_edge_mteps_harmonic_mean": hm_stored,
+           "ms_mean": 1e3 * sum(times) / len(times), "levels": levels, "bottom_up_steps": bu,
+           "direction_optimizing": True, "n_gpus": args.world,
+           "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)",
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "algorithmic_bytes_per_launch": sum(bytes_alg) / len(bytes_alg) / args.world,
+                        "kernel": "one traversal (all levels, host wall time between synchronisations); "
+                                  "bytes = 4 E_cc + 16 V_cc (SURVEY.md §8d), per rank at N > 1; a direction-"
+                                  "optimising traversal may read fewer bytes than that"}}
+    if args.rank == 0 and args.world == 1 and not args.no_cpu_baseline:
+        try:
+            import numpy as np
+            from oracle import cpu_native
+            off, idx, _ = g.adjacency(h, transposed=False)
+            off, idx = off.cpu().numpy().astype(np.int64), idx.cpu().numpy()
+            # the first bench root, in internal ids
+            root_int = int(np.nonzero(number_map == roots[0])[0][0])
+            T = omp_threads()
+            t1, d1, _ = cpu_native.bfs(off, idx, root_int, threads=1)
+            tn, _, _ = cpu_native.bfs(off, idx, root_int, threads=T)
+            e_cc = int((off[1:] - off[:-1])[d1 != np.iinfo(np.int32).max].sum())
+            out["cpu_baseline_compiled"] = {
+                "kind": "port", "source": "oracle/cpu_baseline.c (bfs_test.cpp:41-79 restated)",
+                "single_thread": {"value": (e_cc / 2) / t1 / 1e6, "unit": "MTEPS", "cores": 1},
+                "openmp": {"value": (e_cc / 2) / tn / 1e6, "unit": "MTEPS", "cores": T},
+                "sample": f"one traversal from the first bench root on the same RMAT-{scale} graph (top-down)",
+                "host": host_info(T)}
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline_compiled"] = {"error": repr(e)[:200]}
+    return out
 
 
+# ----------------------------------------------------------------------------- Louvain
 def louvain_leg(p, args):
     """configs[4]: Louvain time-to-solution on a symmetrised R-MAT graph with uniform
     [0, 1) fp32 weights (seed 42, cugraph_funcs.py:56-58), max_level 100,
@@ -249,77 +448,16 @@ def louvain_leg(p, args):
             "path": "sg" if args.world == 1 else f"mg{args.world} ({'RCCL' if args.comm == 'rccl' else 'torch'})"}
 
 
-def cpu_networkx_legs(args):
-    """the reference's NetworkX CPU path for BFS and Louvain, on bounded
-    R-MAT samples (same generator parameters, numpy twin), 1 core.  NetworkX's
-    dict-of-dicts graph cannot hold RMAT-23/24, so the sample scale is stated."""
-    import numpy as np
-    from oracle import graph as og
-    from oracle import rmat
-    from oracle.baseline import networkx_bfs, networkx_louvain
-    out = {}
-    sb = 16
-    s, d = rmat.rmat(sb, 16 << sb, seed=42)
-    s, d, _ = og.symmetrize_dedup(s, d, None)
-    root = int(s[0])
-    tb, t, e_cc = networkx_bfs(s, d, root)
-    out["bfs"] = {"value": (e_cc / t) / 1e6, "unit": "MTEPS", "cores": 1, "kind": "networkx",
-                  "sample": f"nx.single_source_shortest_path_length, networkx 3.4.2, RMAT-{sb} symmetric "
-                            f"({s.size} stored edges), 1 root; graph build {tb:.1f}s excluded"}
-    sl = 14
-    s, d = rmat.rmat(sl, 16 << sl, seed=42)
-    w = rmat.rmat_weights(s.size, seed=43).astype(np.float64)
-    s, d, w = og.symmetrize_dedup(s, d, w)
-    tb, t, q = networkx_louvain(s, d, w)
-    out["louvain"] = {"value": t, "unit": "s", "cores": 1, "kind": "networkx", "modularity": q,
-                      "sample": f"nx.community.louvain_communities(seed=42) + modularity, networkx 3.4.2, "
-                                f"RMAT-{sl} symmetric uniform weights ({s.size} stored edges); build {tb:.1f}s excluded"}
-    return out
+# ----------------------------------------------------------------------------- main
+def make_ctx(p, args, C):
+    if args.comm == "rccl":
+        return p.comms.init_rccl(C)
+    return p.comms.init_torch(C)
 
 
-def stream_copy_gbs(nbytes=4 << 30, reps=10):
-    """Measured HBM ceiling: device-to-device copy of a 4 GiB buffer,
-    read + write bytes / time, HIP events."""
-    import torch
-    a = torch.empty(nbytes // 4, dtype=torch.int32, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
-
-
-def barrier(args):
-    if args.world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-
-
-def max_over_ranks(args, t):
-    if args.world == 1:
-        return t
-    import torch
-    import torch.distributed as dist
-    x = torch.tensor([t], dtype=torch.float64)
-    dist.all_reduce(x, op=dist.ReduceOp.MAX)
-    return float(x[0])
-
-
-def sum_over_ranks(args, v):
-    if args.world == 1:
-        return v
-    import torch
-    import torch.distributed as dist
-    x = torch.tensor([v], dtype=torch.float64)
-    dist.all_reduce(x)
-    return float(x[0])
+def grid_name(args, C):
+    return (f"2D {args.world // C}x{C} (rows x cols), "
+            f"{'RCCL' if args.comm == 'rccl' else 'torch.distributed/gloo'}")
 
 
 def main():
@@ -327,33 +465,35 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scale", type=int, default=None)
+    ap.add_argument("--scale", type=int, default=24, help="headline PageRank scale (BASELINE: RMAT-24 at every N)")
     ap.add_argument("--alpha", type=float, default=0.85)
     ap.add_argument("--epsilon", type=float, default=1e-6)
-    ap.add_argument("--cpu-iters", type=int, default=5)
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--nx-pagerank-scale", type=int, default=17)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bfs", dest="bfs", action="store_true", default=True)
     ap.add_argument("--no-bfs", dest="bfs", action="store_false")
-    ap.add_argument("--bfs-scale", type=int, default=None)
+    ap.add_argument("--bfs-scale", type=int, default=24)
+    ap.add_argument("--bfs-roots", type=int, default=8)
     ap.add_argument("--louvain", dest="louvain", action="store_true", default=True)
     ap.add_argument("--no-louvain", dest="louvain", action="store_false")
     ap.add_argument("--louvain-scale", type=int, default=None, help="default 23 + log2(N): RMAT-26 at 8 GPUs")
-    ap.add_argument("--row-comm-size", type=int, default=None, help="C of the R x C grid (default: R <= C)")
+    ap.add_argument("--secondary", dest="secondary", action="store_true", default=True,
+                    help="secondary PageRank legs: RMAT-22 at N=1, RMAT-26 at N=8, the other grid at N>1")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false")
+    ap.add_argument("--row-comm-size", type=int, default=None,
+                    help="C of the R x C grid (default: the reference's rule, mg_utilities.cpp:60-63 -- the "
+                         "largest divisor of N <= sqrt(N): 2 at N=8, R=4)")
     ap.add_argument("--comm", choices=["rccl", "torch"], default="rccl",
                     help="MG collectives: RCCL inside libcugraph_c (default), or torch.distributed callbacks "
                          "(code-path rehearsal with several ranks on one GPU; not a performance number)")
-    ap.add_argument("--bfs-roots", type=int, default=8)
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
-    ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--traffic-child", choices=["pagerank", "bfs"], default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     grow = int(round(math.log2(max(world, 1))))
-    if args.scale is None:
-        args.scale = 22 + grow
-    if args.bfs_scale is None:
-        args.bfs_scale = 24  # BASELINE: BFS on RMAT-24 at 1/2/4/8 GPUs (fixed graph)
     if args.louvain_scale is None:
         args.louvain_scale = 23 + grow  # BASELINE configs[4]: RMAT-26 Louvain on 8 GPUs
     args.world, args.rank = world, rank
@@ -363,29 +503,24 @@ def main():
     import pylibcugraph as p
 
     args.ctx = None
+    C = None
     if world > 1:
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group("gloo")  # bootstrap + timing only; the data path is RCCL
-        if args.comm == "rccl":
-            args.ctx = p.comms.init_rccl(args.row_comm_size)
-        else:
-            args.ctx = p.comms.init_torch(args.row_comm_size)
+        C = args.row_comm_size or p.comms.default_row_comm_size(world)
+        args.ctx = make_ctx(p, args, C)
     torch.cuda.init()
 
-    r = pagerank_leg(p, args)
-    if args.traffic_child:
+    if args.traffic_child == "pagerank":
+        pagerank_leg(p, args, args.scale, 1, 0)
         return
-    r["t"] = max_over_ranks(args, r["t"])
-    r["value"] = r["E"] * sum(r["iters"]) / r["t"]
-    log(f"[bench] pagerank: {r['value']:.4g} edges/s, iters {r['iters']}, kernel {r['avg_ms']:.4f} ms/iter, "
-        f"{r['achieved']:.1f} GB/s algorithmic")
-    grid = None
-    if world > 1:
-        C = args.ctx.row_comm_size
-        grid = f"2D {world // C}x{C} (rows x cols), {'RCCL' if args.comm == 'rccl' else 'torch.distributed/gloo'}"
+    if args.traffic_child == "bfs":
+        bfs_leg(p, args, child=True)
+        return
 
+    r = pagerank_leg(p, args, args.scale, args.steps, args.warmup, args.ctx)
     out = {
         "metric": "PageRank edges/sec + BFS MTEPS on RMAT-24 at 1/2/4/8 MI355X",
         "value": r["value"],
@@ -395,7 +530,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": r["t"] / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: device Graph500 R-MAT (a=.57 b=c=.19, ef 16, seed 42, scrambled), symmetrised+dedup",
@@ -408,12 +543,13 @@ def main():
             "edges": r["E"],
             "iterations_per_step": r["iters"][0] if r["iters"] else 0,
             "graph_build_s": round(r["build_s"], 3),
-            "parallelism": "sg" if world == 1 else f"mg{world}: {grid}",
+            "parallelism": "sg" if world == 1 else f"mg{world}: {grid_name(args, C)}",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_pr_push_q + k_pr_apply (one PageRank iteration): HIP events around each 16-iteration chunk on the "
-                       "library stream / iterations run (inter-kernel gaps and post-convergence no-op launches included)" if world == 1 else
+            "kernel": ("k_pr_push_q + k_pr_apply (one PageRank iteration): HIP events on the library stream around "
+                       "each chunk of iterations in the timed region / iterations run (inter-kernel gaps "
+                       "included)" if world == 1 else
                        "one MG PageRank iteration per rank (row allgather + push + column reduce-scatter + apply + "
                        "allreduce, HIP events around all); bytes = this rank's 1/N share"),
             "achieved": r["achieved"],
@@ -426,39 +562,75 @@ def main():
         },
     }
     if world > 1:  # MG comm bytes per rank and iteration (x~ allgather + u64 sums reduce-scatter)
-        C = args.ctx.row_comm_size
         Rr = world // C
         out["roofline"]["comm_bytes_per_rank_iter"] = ((C - 1) * r["V"] / world * 4 + (Rr - 1) * r["V"] / world * 8)
     try:
-        out["roofline"]["stream_copy_gbs"] = stream_copy_gbs()
+        out["roofline"]["copy_ceiling_gbs"] = r["h"].measure_copy_bandwidth(4 << 30, 10)
     except Exception as e:  # noqa: BLE001
-        out["roofline"]["stream_copy_gbs"] = f"unavailable: {e!r}"[:200]
+        out["roofline"]["copy_ceiling_gbs"] = f"unavailable: {e!r}"[:200]
     # (no nested profiler: a bench already running under rocprofv3 skips the traffic passes)
     under_prof = any(k.startswith("ROCPROF_") for k in os.environ)
-    if rank == 0 and world == 1 and not args.no_traffic and not under_prof:
+    do_traffic = rank == 0 and world == 1 and not args.no_traffic and not under_prof
+    if do_traffic:
         try:
-            tb, detail = traffic_leg(args)
+            tb, detail = pagerank_traffic(args)
             out["roofline"]["traffic"] = tb
             out["roofline"]["traffic_note"] = (
-                "HBM bytes per iteration (k_pr_push + k_pr_apply) = 2 x FETCH_SIZE + WRITE_SIZE from separate "
-                f"rocprofv3 --pmc passes: {detail}" if tb else f"unavailable: {detail}")
+                "HBM bytes per iteration (k_pr_push + k_pr_apply) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from separate "
+                f"rocprofv3 --pmc passes: {detail}")
         except Exception as e:  # noqa: BLE001
             out["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline_leg(p, r, args)
+            out["cpu_baseline"] = pagerank_cpu_baseline(p, r, args)
         except Exception as e:  # noqa: BLE001
-            out["cpu_baseline"] = {"error": repr(e)}
+            out["cpu_baseline"] = {"error": repr(e)[:300]}
+    del r
+    release_caches(p)
+
+    if args.secondary:
+        try:
+            if world == 1:
+                r2 = pagerank_leg(p, args, 22, args.steps, args.warmup)
+                out["pagerank_rmat22"] = pagerank_summary(r2, args, "sg")
+                del r2
+            else:
+                alt = p.comms.flat_row_comm_size(world) if C != p.comms.flat_row_comm_size(world) \
+                    else p.comms.default_row_comm_size(world)
+                if alt != C:
+                    ctx2 = make_ctx(p, args, alt)
+                    r2 = pagerank_leg(p, args, args.scale, args.steps, args.warmup, ctx2)
+                    out["pagerank_alt_grid"] = pagerank_summary(r2, args, grid_name(args, alt))
+                    del r2
+                    release_caches(p)
+                    barrier(args)
+                    ctx2.free()
+                if world == 8:
+                    r2 = pagerank_leg(p, args, 26, max(1, args.steps // 2), 1, args.ctx)
+                    out["pagerank_rmat26"] = pagerank_summary(r2, args, grid_name(args, C))
+                    del r2
+        except Exception as e:  # noqa: BLE001
+            out["secondary_error"] = repr(e)[:300]
+        release_caches(p)
     if args.bfs:
         try:
-            del r
-            release_caches(p)
             out["bfs"] = bfs_leg(p, args)
+            log(f"[bench] bfs RMAT-{args.bfs_scale}: {out['bfs']['mteps_harmonic_mean']:.1f} MTEPS, "
+                f"{out['bfs']['ms_mean']:.3f} ms/traversal")
+            if do_traffic:
+                try:
+                    tb, detail = bfs_traffic(args, args.bfs_roots)
+                    out["bfs"]["roofline"]["traffic"] = tb
+                    out["bfs"]["roofline"]["traffic_note"] = (
+                        "HBM bytes per traversal (every BFS kernel) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from "
+                        f"separate rocprofv3 --pmc passes over one traversal per root: {detail}")
+                except Exception as e:  # noqa: BLE001
+                    out["bfs"]["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]
         except Exception as e:  # noqa: BLE001
             out["bfs"] = {"status": "failed", "error": repr(e)[:300]}
+        release_caches(p)
     if args.louvain:
         try:
-            release_caches(p)
             out["louvain"] = louvain_leg(p, args)
             log(f"[bench] louvain: RMAT-{out['louvain']['scale']} {out['louvain']['time_s']:.3f}s "
                 f"Q={out['louvain']['modularity']:.6f} levels={out['louvain']['levels']}")
@@ -466,7 +638,7 @@ def main():
             out["louvain"] = {"status": "failed", "error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            nxb = cpu_networkx_legs(args)
+            nxb = networkx_cpu_legs(args)
             if isinstance(out.get("bfs"), dict) and "mteps_harmonic_mean" in out["bfs"]:
                 out["bfs"]["cpu_baseline"] = nxb["bfs"]
             if isinstance(out.get("louvain"), dict) and "time_s" in out["louvain"]:
@@ -478,7 +650,6 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-        r = None
         args.ctx.free()
         dist.destroy_process_group()
 

@@ -99,6 +99,21 @@ void device_free(void* p, hipStream_t s)
   c.cached += cls;
 }
 
+void* device_forget(void* p, hipStream_t s)
+{
+  if (!p) return nullptr;
+  cache_t& c = cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return nullptr;  // not ours
+    c.live.erase(it);
+  }
+  // pending work on the block's stream finishes before the caller may hipFree it
+  if (hipStreamSynchronize(s) != hipSuccess) (void)hipGetLastError();
+  return p;
+}
+
 size_t device_cache_trim()
 {
   cache_t& c = cache();

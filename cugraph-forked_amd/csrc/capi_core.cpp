@@ -9,6 +9,7 @@
 
 #include <cugraph_amd/ext.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -142,6 +143,20 @@ extern "C" void cugraph_type_erased_device_array_free(cugraph_type_erased_device
   delete a;  // freed on the null stream (common.hpp buffer::release)
 }
 
+// reference array.h:95 (declared under `#if 0` there, array.cpp:111-122: RMM buffers
+// cannot give up their memory).  Blocks of the caching allocator can: the block
+// leaves the allocator's books (never cached, never reused), its stream is
+// synchronised, and the caller owns the pointer and frees it with hipFree.
+extern "C" void* cugraph_type_erased_device_array_release(cugraph_type_erased_device_array_t* p)
+{
+  auto* a = reinterpret_cast<device_array_t*>(p);
+  if (!a) return nullptr;
+  hipStream_t const s = a->buf.stream();
+  void* raw           = a->buf.detach();
+  delete a;
+  return raw ? cgx::device_forget(raw, s) : nullptr;
+}
+
 extern "C" cugraph_type_erased_device_array_view_t* cugraph_type_erased_device_array_view(
   cugraph_type_erased_device_array_t* array)
 {
@@ -268,6 +283,21 @@ extern "C" cugraph_error_code_t cugraph_type_erased_host_array_create(const cugr
 extern "C" void cugraph_type_erased_host_array_free(cugraph_type_erased_host_array_t* p)
 {
   delete reinterpret_cast<host_array_t*>(p);
+}
+
+// reference array.h:212 (also `#if 0` there, array.cpp:210-217).  The bytes move to
+// a malloc'd block the caller frees with free(); an empty array gives NULL.
+extern "C" void* cugraph_type_erased_host_array_release(cugraph_type_erased_host_array_t* p)
+{
+  auto* a = reinterpret_cast<host_array_t*>(p);
+  if (!a) return nullptr;
+  void* raw = nullptr;
+  if (!a->data.empty()) {
+    raw = std::malloc(a->data.size());
+    if (raw) std::memcpy(raw, a->data.data(), a->data.size());
+  }
+  delete a;
+  return raw;
 }
 
 extern "C" cugraph_type_erased_host_array_view_t* cugraph_type_erased_host_array_view(

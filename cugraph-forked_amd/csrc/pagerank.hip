@@ -44,6 +44,7 @@ struct pr_state {
   double base;         // unvarying part of the current iteration
   double pers_factor;  // alpha*dangling + 1 - alpha (personalised runs)
   double diff;         // L1 difference of the last iteration
+  double prev_diff;    // ... and of the one before (host chunk sizing)
   double dangling;     // dangling mass after the last iteration
   unsigned int ticket;
   int iter;
@@ -73,6 +74,22 @@ struct pr_args {
   double* mg_sums;  // multi-GPU: (diff, dangling) of this rank, allreduced before k_mg_finish
 };
 
+// Iterations to enqueue before the host next reads the state.  The L1 difference
+// of the power iteration falls geometrically (ratio ~ alpha times the second
+// eigenvalue), so the count still needed is predicted from the last two
+// differences, plus one for rounding; the first check comes after 8.  Launches
+// after convergence return at once, so an overshoot costs an empty launch and an
+// undershoot one more host round trip.  Not tied to any one graph.
+inline int next_chunk(pr_state const& st, double eps, int max_iter)
+{
+  int const left = std::max(1, max_iter - st.iter);
+  if (st.iter < 2 || !(st.diff > 0.0) || !(st.prev_diff > 0.0) || !(eps > 0.0)) return std::min(8, left);
+  double const r = std::min(0.995, std::max(1e-3, st.diff / st.prev_diff));
+  double const n = std::ceil(std::log(eps / st.diff) / std::log(r)) + 1.0;
+  int const k    = n < 1.0 ? 1 : n > 64.0 ? 64 : (int)n;
+  return std::min(k, left);
+}
+
 namespace {
 
 // next iteration's base, convergence flag and iteration count from the global
@@ -83,6 +100,7 @@ __device__ void update_state(pr_args<V, E, R> const& a, double d, double g, bool
   pr_state* st    = a.st;
   int it          = st->iter + (count_iter ? 1 : 0);
   st->iter        = it;
+  if (count_iter) st->prev_diff = st->diff;
   st->diff        = d;
   st->dangling    = g;
   double pf       = g * a.alpha + (1.0 - a.alpha);
@@ -1241,12 +1259,11 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   }
   bool const fused = push && pmode == kPushQueue && nblk_push > 0 && fused_apply_enabled();
   auto fkernel     = g.weighted ? k_pr_push_q<V, E, R, true, true> : k_pr_push_q<V, E, R, false, true>;
-  // Chunked enqueue: 16 iterations per host check (RMAT-22 converges in 16).
-  // Profiling records one pair of pooled HIP events around each chunk -- an event
+  // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
+  // predicted remainder.  Profiling records one pair of pooled HIP events around each chunk -- an event
   // between every two iterations cost a ~10 us queue gap per iteration -- and
   // reports chunk time / iterations run, so the no-op launches after convergence
   // in the last chunk count against the kernels.
-  int const chunk = 16;
   std::vector<hipEvent_t> ev;
   pr_state hst{};
   R* bufs[2]    = {xa.data(), xb.data()};
@@ -1259,6 +1276,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       ev.push_back(h.event(ev.size()));
       HIP_CHECK(hipEventRecord(ev[ev.size() - 2], s));
     }
+    int const chunk = next_chunk(hst, eps, a.max_iter);
     for (int i = 0; i < chunk; ++i) {
       a.x_in  = bufs[launched & 1];
       a.x_out = bufs[(launched + 1) & 1];
@@ -1626,12 +1644,11 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
 
-  int const chunk = 8;
   std::vector<hipEvent_t> ev;
   pr_state hst{};
   pr_state* hpin = h.pinned_as<pr_state>();
   {
-    // (collectives run even in the no-op iterations after convergence: 8 per check;
+    // (collectives run even in the no-op iterations after convergence: next_chunk;
     // one pair of pooled events per chunk, as on one GPU)
     while (true) {
       if (h.profiling) {
@@ -1639,6 +1656,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
         ev.push_back(h.event(ev.size()));
         HIP_CHECK(hipEventRecord(ev[ev.size() - 2], s));
       }
+      int const chunk = next_chunk(hst, eps, a.max_iter);
       for (int i = 0; i < chunk; ++i) {
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
         if (nblk_push)

@@ -74,6 +74,13 @@ class ResourceHandle:
     def last_louvain_levels(self):
         return _lib.lib.cugraph_amd_last_louvain_levels(self.c_resource_handle_ptr)
 
+    def measure_copy_bandwidth(self, nbytes=4 << 30, reps=10):
+        """HBM ceiling: 16-B-per-lane copy kernel on this handle's stream, GB/s (read + write)."""
+        r = _lib.lib.cugraph_amd_measure_copy_bandwidth(self.c_resource_handle_ptr, int(nbytes), int(reps))
+        if r < 0:
+            raise RuntimeError("cugraph_amd_measure_copy_bandwidth failed")
+        return r
+
     def __del__(self, _sd=_lib.SHUTDOWN, _free=_lib.lib.cugraph_free_resource_handle):
         p = getattr(self, "c_resource_handle_ptr", None)
         if p and not _sd[0]:

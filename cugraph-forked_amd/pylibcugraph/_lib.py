@@ -140,6 +140,8 @@ _proto("cugraph_amd_last_bfs_bottom_up_steps", c_size_t, P)
 _proto("cugraph_amd_last_louvain_levels", c_size_t, P)
 _proto("cugraph_amd_trim_device_cache", c_size_t)
 _proto("cugraph_amd_version", ctypes.c_char_p)
+_proto("cugraph_amd_measure_copy_bandwidth", c_double, P, c_size_t, c_int)
+_proto("cugraph_type_erased_device_array_release", P, P)
 # multi-GPU communicator contexts (include/cugraph_amd/comm.h)
 _proto("cugraph_amd_comm_unique_id_size", c_size_t)
 _proto("cugraph_amd_comm_get_unique_id", c_int, P, PP)

@@ -53,22 +53,22 @@ class CommOps(ctypes.Structure):
 
 
 def default_row_comm_size(world_size: int) -> int:
-    """C of the R x C grid.
+    """C of the R x C grid: the reference's rule (mg_utilities.cpp:60-63), the largest
+    divisor of P that is <= sqrt(P) -- 2 at 8 GPUs (R = 4), 2 at 4, 1 at 2.
 
-    Up to 8 ranks (one node, every GPU pair joined by its own xGMI link) the grid is
-    1 x P.  The x~ allgather then runs over all P-1 links at once and there is no
-    column reduce-scatter at all.  The reference's squarer grid (mg_utilities.cpp:60-66;
-    2 x 4 at 8 GPUs) trades that for less total volume, which pays on switched
-    networks.  On a full mesh the per-link time is what counts: V/P*4 B for the
-    allgather, plus V/P*8 B for a reduce-scatter whenever R > 1.
-    Beyond 8 ranks: R = the largest divisor of P with R*R <= P."""
-    if world_size <= 8:
-        return world_size
-    r = 1
-    for d in range(1, int(math.isqrt(world_size)) + 1):
-        if world_size % d == 0:
-            r = d
-    return world_size // r
+    ``row_comm_size=P`` (1 x P) is the alternative for one fully connected node: the
+    x~ allgather then runs over all P-1 xGMI links and the column reduce-scatter of
+    the fixed-point sums disappears.  bench.py times both grids at
+    N > 1 so the choice rests on a measurement of the driver's node."""
+    c = max(1, int(math.isqrt(world_size)))
+    while world_size % c:
+        c -= 1
+    return c
+
+
+def flat_row_comm_size(world_size: int) -> int:
+    """1 x P: every rank in one row."""
+    return world_size
 
 
 def grid_groups(world_size: int, row_comm_size: int):

@@ -106,6 +106,11 @@ cugraph_type_erased_device_array_view_t* cugraph_amd_heirarchical_clustering_res
  * equivalent is releasing its RMM pool. */
 size_t cugraph_amd_trim_device_cache(void);
 
+/* Measured HBM ceiling: a 16-B-per-lane grid-stride copy of `bytes` (nontemporal
+ * loads and stores), `reps` launches timed with HIP events on the handle's stream.
+ * Returns (read + write bytes) / time in GB/s, or a negative value on error. */
+double cugraph_amd_measure_copy_bandwidth(const cugraph_resource_handle_t* handle, size_t bytes, int reps);
+
 /* Library build string, e.g. "cugraph-forked_amd gfx950 <date>". */
 const char* cugraph_amd_version(void);
 

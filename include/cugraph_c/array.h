@@ -1,8 +1,9 @@
 /*
  * libcugraph_c type-erased arrays -- MI355X build.
  * ABI-compatible with the reference cpp/include/cugraph_c/array.h:25-326.
- * Device arrays live in HBM (hipMallocAsync on the handle's stream); views
- * wrap caller memory and never own it.
+ * Device arrays live in HBM, allocated on the handle's stream from
+ * libcugraph_c's stream-ordered caching allocator (csrc/alloc.cpp); views wrap
+ * caller memory and never own it.
  */
 #pragma once
 #include <cugraph_c/resource_handle.h>
@@ -33,6 +34,11 @@ cugraph_error_code_t cugraph_type_erased_device_array_create_from_view(
 
 /* reference array.h:78 */
 void cugraph_type_erased_device_array_free(cugraph_type_erased_device_array_t* p);
+
+/* reference array.h:95 (compiled out there with `#if 0`; implemented here).
+ * Gives up ownership: the array handle is freed, its stream synchronised, and the
+ * returned device pointer belongs to the caller, who frees it with hipFree. */
+void* cugraph_type_erased_device_array_release(cugraph_type_erased_device_array_t* p);
 
 /* reference array.h:97 -- view of an owning array (lives as long as the array) */
 cugraph_type_erased_device_array_view_t* cugraph_type_erased_device_array_view(
@@ -72,6 +78,11 @@ cugraph_error_code_t cugraph_type_erased_host_array_create(const cugraph_resourc
 
 /* reference array.h:183 */
 void cugraph_type_erased_host_array_free(cugraph_type_erased_host_array_t* p);
+
+/* reference array.h:212 (compiled out there with `#if 0`; implemented here).
+ * The array handle is freed and its bytes returned in a malloc'd block the caller
+ * frees with free(); NULL for an empty array. */
+void* cugraph_type_erased_host_array_release(cugraph_type_erased_host_array_t* p);
 
 /* reference array.h:202 */
 cugraph_type_erased_host_array_view_t* cugraph_type_erased_host_array_view(

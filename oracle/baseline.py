@@ -98,3 +98,43 @@ def networkx_louvain(src, dst, weights, seed=42):
     t2 = time.perf_counter()
     q = nx.community.modularity(G, comms, weight="weight")
     return t1 - t0, t2 - t1, q
+
+
+def networkx_pagerank(scale, alpha=0.85, epsilon=1e-6, seed=42):
+    """The reference's CPU path for PageRank itself: ``nx.pagerank`` on an
+    undirected ``nx.Graph`` of the symmetrised R-MAT graph of `scale` (numpy twin of
+    the device generator), to convergence.  NetworkX stops on L1 < N * tol
+    (networkx/algorithms/link_analysis/pagerank_alg.py, _pagerank_scipy), so tol =
+    epsilon / N gives the reference's L1 < epsilon rule.  The iteration count is
+    that of the same loop (pagerank_scipy_iterations' body) run to the same rule.
+    Returns (build_seconds, pagerank_seconds, stored_edges, iterations)."""
+    import networkx as nx
+    import scipy.sparse as sp
+
+    from oracle import graph as og
+    from oracle import rmat
+
+    s, d = rmat.rmat(scale, 16 << scale, seed=seed)
+    s, d, _ = og.symmetrize_dedup(s, d, None)
+    t0 = time.perf_counter()
+    G = nx.Graph()
+    G.add_edges_from(zip(s.tolist(), d.tolist()))
+    t1 = time.perf_counter()
+    N = G.number_of_nodes()
+    nx.pagerank(G, alpha=alpha, tol=epsilon / N, max_iter=500)
+    t2 = time.perf_counter()
+    # iterations of the same power loop to the same stopping rule
+    ids, inv = np.unique(np.concatenate([s, d]), return_inverse=True)
+    si, di = inv[: s.size], inv[s.size:]
+    V = ids.size
+    outdeg = np.bincount(si, minlength=V).astype(np.float64)
+    AT = sp.csr_matrix((1.0 / outdeg[si], (di, si)), shape=(V, V))
+    x = np.full(V, 1.0 / V)
+    it = 0
+    while it < 500:
+        xl = x
+        x = alpha * (AT @ xl) + (1 - alpha) / V  # no dangling vertices in a symmetric edge-list graph
+        it += 1
+        if np.abs(x - xl).sum() < N * (epsilon / N):
+            break
+    return t1 - t0, t2 - t1, int(s.size), it

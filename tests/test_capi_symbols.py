@@ -32,7 +32,8 @@ def test_headers_declare_reference_entry_points():
                  "cugraph_pagerank", "cugraph_personalized_pagerank", "cugraph_bfs", "cugraph_sssp",
                  "cugraph_louvain", "cugraph_centrality_result_get_values", "cugraph_paths_result_get_distances",
                  "cugraph_heirarchical_clustering_result_get_modularity", "cugraph_error_message",
-                 "cugraph_type_erased_device_array_view_copy_to_host"]:
+                 "cugraph_type_erased_device_array_view_copy_to_host",
+                 "cugraph_type_erased_device_array_release", "cugraph_type_erased_host_array_release"]:
         assert must in names
 
 

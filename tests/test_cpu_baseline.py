@@ -1,0 +1,58 @@
+"""The compiled CPU restatement (oracle/cpu_baseline.c, bench.py's secondary CPU
+baseline) agrees with the numpy oracle: PageRank iterates converge to the
+oracle's ranks and BFS distances are exact, single-threaded and with OpenMP."""
+import numpy as np
+import pytest
+
+from conftest import dataset_path
+from oracle import bfs as obfs
+from oracle import graph as og
+from oracle import pagerank as opr
+from oracle import rmat
+
+cpu = pytest.importorskip("oracle.cpu_native")
+
+
+def _built():
+    try:
+        cpu.lib()
+        return True
+    except FileNotFoundError:
+        return False
+
+
+pytestmark = pytest.mark.skipif(not _built(), reason="make -C oracle not run")
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_pagerank_matches_oracle(threads):
+    s, d, _ = og.read_csv(dataset_path("karate.csv"))
+    s, d, _ = og.symmetrize_dedup(s, d, None)
+    g = og.create_graph(s, d, None, store_transposed=True, renumber=False)
+    _, pr = cpu.pagerank(g.offsets, g.indices, 100, alpha=0.85, threads=threads)
+    ref = opr.pagerank(g.num_vertices, s, d, None, 0.85, 1e-10, 500)
+    assert np.allclose(pr, ref, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_bfs_matches_oracle(threads):
+    s, d = rmat.rmat(11, 16 << 11, seed=42)
+    s, d, _ = og.symmetrize_dedup(s, d, None)
+    g = og.create_graph(s, d, None, renumber=True)
+    src = 0
+    _, dist, pred = cpu.bfs(g.offsets, g.indices, src, threads=threads)
+    rd, _ = obfs.bfs(g.num_vertices, g.offsets, g.indices, [src])
+    assert np.array_equal(dist, rd)
+    reached = (dist != np.iinfo(np.int32).max) & (np.arange(dist.size) != src)
+    # every predecessor is a neighbour one level up (bfs_test.cpp:210-230 rule)
+    assert np.all(dist[pred[reached]] == dist[reached] - 1)
+
+
+def test_pagerank_f64_equals_numpy_oracle():
+    s, d = rmat.rmat(12, 16 << 12, seed=42)
+    s, d, _ = og.symmetrize_dedup(s, d, None)
+    g = og.create_graph(s, d, None, store_transposed=True, renumber=True)
+    ref, it_ref = opr.pagerank_from_graph(g, alpha=0.85, epsilon=1e-6, max_iterations=500, return_iterations=True)
+    pr, it = cpu.pagerank_f64(g.offsets, g.indices, 0.85, 1e-6, 500, threads=4)
+    assert it == it_ref
+    assert np.max(np.abs(pr - ref) / ref) < 1e-12

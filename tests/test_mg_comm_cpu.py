@@ -25,7 +25,8 @@ def test_grid_helpers():
     sys.path.insert(0, PKG)
     pytest.importorskip("torch")
     from pylibcugraph.comms import default_row_comm_size, grid_groups
-    assert [default_row_comm_size(p) for p in (1, 2, 4, 8, 6, 16, 32)] == [1, 2, 4, 8, 6, 4, 8]
+    # the reference's rule, mg_utilities.cpp:60-63: largest divisor <= sqrt(P)
+    assert [default_row_comm_size(p) for p in (1, 2, 4, 8, 6, 16, 32)] == [1, 1, 2, 2, 2, 4, 4]
     rows, cols = grid_groups(8, 4)
     assert rows == [[0, 1, 2, 3], [4, 5, 6, 7]]
     assert cols == [[0, 4], [1, 5], [2, 6], [3, 7]]
