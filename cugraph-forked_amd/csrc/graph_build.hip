@@ -53,17 +53,21 @@ __global__ void k_dense_by_search(V* ids, size_t n, V const* sorted, size_t nv, 
   }
 }
 
-template <typename V>
-__global__ void k_count32(V const* major, size_t n, int* deg)
+// offsets[v] = first i with sorted[i] >= v (v in [0, nv]): the CSR offsets of a
+// sorted major array, i.e. degrees as run lengths -- no per-edge atomics (hub ids
+// made same-address atomicAdd counting the graph build's hot spot)
+template <typename V, typename E>
+__global__ void k_lower_bounds(V const* sorted, size_t n, int64_t nv, E* out)
 {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    atomicAdd(deg + major[i], 1);
-}
-template <typename V>
-__global__ void k_count64(V const* major, size_t n, unsigned long long* deg)
-{
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    atomicAdd(deg + major[i], 1ull);
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v <= nv; v += (int64_t)gridDim.x * blockDim.x) {
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+      size_t mid = (lo + hi) >> 1;
+      if ((int64_t)sorted[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    out[v] = static_cast<E>(lo);
+  }
 }
 
 template <typename V>
@@ -98,12 +102,19 @@ __global__ void k_inverse_perm(V const* order, size_t n, V* inv)
     inv[order[i]] = static_cast<V>(i);
 }
 
-// expand offsets into the major id of every edge
+// the major id of every edge: last row with offsets[row] <= e (one thread per
+// edge, so a hub row is not one thread's loop)
 template <typename V, typename E>
-__global__ void k_expand_majors(E const* offsets, int64_t nv, V* majors)
+__global__ void k_expand_majors(E const* offsets, int64_t nv, int64_t ne, V* majors)
 {
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-    for (E e = offsets[v]; e < offsets[v + 1]; ++e) majors[e] = static_cast<V>(v);
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nv - 1;
+    while (lo < hi) {
+      int64_t mid = (lo + hi + 1) >> 1;
+      if ((int64_t)offsets[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    majors[e] = static_cast<V>(lo);
   }
 }
 
@@ -159,12 +170,6 @@ __global__ void k_atomic_weight_sums(V const* idx, W const* w, size_t ne, double
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < ne; e += (size_t)gridDim.x * blockDim.x)
     atomicAdd(acc + idx[e], (double)w[e]);
 }
-template <typename V>
-__global__ void k_atomic_counts(V const* idx, size_t ne, unsigned long long* acc)
-{
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < ne; e += (size_t)gridDim.x * blockDim.x)
-    atomicAdd(acc + idx[e], 1ull);
-}
 
 template <typename V>
 __global__ void k_ext_to_int(V* ids, size_t n, V const* sorted_ext, V const* internal, size_t nv, int* bad)
@@ -200,24 +205,31 @@ __global__ void k_int_to_ext(V* ids, size_t n, V const* nmap, int64_t nv)
 }
 
 // ---------------------------------------------------------------- helpers
+// CSR offsets [nv + 1] of a SORTED major array
 template <typename V, typename E>
-void degrees_of(V const* majors, size_t n, int64_t nv, E* deg, hipStream_t s)
+void offsets_of_sorted(V const* sorted, size_t n, int64_t nv, E* off, hipStream_t s)
 {
-  if constexpr (sizeof(E) == 4) {
-    fill<int>(reinterpret_cast<int*>(deg), nv, 0, s);
-    if (n) {
-      hipLaunchKernelGGL(k_count32<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, majors, n,
-                         reinterpret_cast<int*>(deg));
-      CGX_LAUNCH_CHECK();
-    }
+  hipLaunchKernelGGL((k_lower_bounds<V, E>), dim3(grid_for(nv + 1, kBlock, 8192)), dim3(kBlock), 0, s, sorted, n, nv,
+                     off);
+  CGX_LAUNCH_CHECK();
+}
+
+// degree of every id in [0, nv) among n unsorted majors: radix sort of the ids
+// over the bits in use, then run lengths (a sort streams ~4 passes of 8 B per
+// edge; counting with atomics serialised on the hub ids at 20-55 ms on RMAT-24)
+template <typename V, typename E, typename D>
+void degrees_of(V const* majors, size_t n, int64_t nv, D* deg, hipStream_t s)
+{
+  dbuf<E> off(nv + 1, s);
+  if (n) {
+    dbuf<V> sorted(n, s);
+    radix_sort_keys<V>(majors, sorted.data(), n, 0, bits_for((unsigned long long)std::max<int64_t>(nv - 1, 0)), s);
+    offsets_of_sorted<V, E>(sorted.data(), n, nv, off.data(), s);
   } else {
-    fill<unsigned long long>(reinterpret_cast<unsigned long long*>(deg), nv, 0ull, s);
-    if (n) {
-      hipLaunchKernelGGL(k_count64<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, majors, n,
-                         reinterpret_cast<unsigned long long*>(deg));
-      CGX_LAUNCH_CHECK();
-    }
+    fill<E>(off.data(), nv + 1, E(0), s);
   }
+  hipLaunchKernelGGL((k_degrees<E, D>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off.data(), nv, deg);
+  CGX_LAUNCH_CHECK();
 }
 
 // sort (major, minor[, w]) by (major, minor) and compress into adj
@@ -250,11 +262,9 @@ void compress(hipStream_t s, int64_t nv, V const* majors, V const* minors, W con
     CGX_LAUNCH_CHECK();
   }
   key_sorted.b.release();
-  dbuf<E> deg(nv + 1, s);
-  degrees_of<V, E>(smaj.data(), n, nv + 1, deg.data(), s);
   adj.offsets.set_stream(s);
   adj.offsets.resize((nv + 1) * sizeof(E));
-  exclusive_scan<E, E>(deg.data(), adj.offsets.data<E>(), nv + 1, s);
+  offsets_of_sorted<V, E>(smaj.data(), n, nv, adj.offsets.data<E>(), s);
   adj.sched_valid = false;
 }
 
@@ -327,7 +337,7 @@ void build_impl(handle_t& h, graph_t& g, array_view_t const& src, array_view_t c
     }
     // 3. major degrees, 4. stable descending sort by degree
     dbuf<E> deg(nv, s), deg_sorted(nv, s);
-    degrees_of<V, E>(majors, n, nv, deg.data(), s);
+    degrees_of<V, E, E>(majors, n, nv, deg.data(), s);
     dbuf<V> ids(nv, s), order(nv, s);
     iota<V>(ids.data(), nv, V(0), s);
     radix_sort_pairs<E, V>(deg.data(), deg_sorted.data(), ids.data(), order.data(), nv, 0,
@@ -373,9 +383,9 @@ void transpose_impl(handle_t& h, graph_t& g, bool to_transposed)
   int64_t nv             = g.num_vertices;
   size_t n               = (size_t)g.num_edges;
   dbuf<V> majors(n, s);
-  if (nv) {
-    hipLaunchKernelGGL((k_expand_majors<V, E>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s,
-                       from.offsets.data<E>(), nv, majors.data());
+  if (nv && n) {
+    hipLaunchKernelGGL((k_expand_majors<V, E>), dim3(grid_for(n, kBlock, 16384)), dim3(kBlock), 0, s,
+                       from.offsets.data<E>(), nv, (int64_t)n, majors.data());
     CGX_LAUNCH_CHECK();
   }
   auto adj = std::make_shared<adjacency_t>();
@@ -505,14 +515,7 @@ void outw_impl(handle_t& h, graph_t& g)
       }
       convert<W, double>(out, acc.data(), nv, s);
     } else {
-      dbuf<unsigned long long> acc(nv, s);
-      fill<unsigned long long>(acc.data(), nv, 0ull, s);
-      if (ne) {
-        hipLaunchKernelGGL(k_atomic_counts<V>, dim3(grid_for(ne, kBlock, 8192)), dim3(kBlock), 0, s, idx, ne,
-                           acc.data());
-        CGX_LAUNCH_CHECK();
-      }
-      convert<W, unsigned long long>(out, acc.data(), nv, s);
+      degrees_of<V, int64_t, W>(idx, ne, nv, out, s);
     }
   }
   HIP_CHECK(hipStreamSynchronize(s));

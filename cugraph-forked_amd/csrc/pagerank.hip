@@ -910,7 +910,10 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   dbuf<uint64_t> keys_out(ne, s);
   dbuf<uint32_t> vals_out(ne, s);
   seg_bounds sb{};
-  {  // source segments of equal entry counts (one per XCD)
+  if (kXcdSegs == 1) {  // one segment: no per-source counting pass
+    sb.lo[0] = 0;
+    sb.lo[kXcdSegs] = n_cols;
+  } else {  // source segments of equal entry counts (one per XCD)
     dbuf<unsigned long long> cnt(n_cols + 1, s), pre(n_cols + 1, s);
     fill<unsigned long long>(cnt.data(), n_cols + 1, 0ull, s);
     hipLaunchKernelGGL(k_src_counts<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, ne, cnt.data());
