@@ -97,20 +97,17 @@ struct err_t {
 struct pr_push_t {
   bool built = false;
   bool ok    = false;  // ids and edge positions fit the 32-bit packing
-  buffer ent;          // uint32[E]: (source - segment base) << 12 | (destination - window base)
-  buffer ew;           // weight_t[E] for weighted graphs
-  buffer units;        // push_unit[nunits]
+  int win_bits = 12;   // destination window = 2^win_bits consecutive rows
+  buffer ent;          // uint32[E + unit]: (source - unit's first source) << win_bits | (row - window base)
+  buffer ew;           // weight_t[E + unit] for weighted graphs
+  buffer units;        // push_unit[nunits], in (window, source) order
   int64_t nunits = 0;
-  std::vector<int64_t> seg_start;  // first unit of every source segment (+ end)
-  buffer acc;          // u64[nacc] fixed-point sums, zero between iterations
+  buffer acc;          // u64[nacc] fixed-point sums by row, zero between iterations
   int64_t nacc = 0;
-  buffer tiles;        // int64[ntiles + 1]: first unit of every (source segment, window) tile
-  int64_t ntiles = 0;  // windows without entries get one empty tile each (at the end)
-  buffer tile_win;     // int32[ntiles]: window of every tile
-  buffer win_tiles;    // uint32[nwin]: tiles per window
-  buffer win_done;     // uint32[nwin]: tiles finished this iteration (fused apply; zero between iterations)
+  buffer tiles;        // int64[ntiles + 1]: first unit of every tile (<= 8 units of one window)
+  int64_t ntiles = 0;
   int64_t nwin = 0;
-  buffer tile_ctr;     // uint32[2]: tile queue heads (alternate iterations); zero between iterations
+  buffer tile_ctr;     // uint32: tile queue head; zero between iterations
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

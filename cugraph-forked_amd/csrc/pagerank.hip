@@ -231,11 +231,7 @@ __device__ __forceinline__ double row_partial_block(pr_args<V, E, R> const& a, E
   return (s0 + s1) + (s2 + s3);
 }
 
-__device__ __forceinline__ uint32_t encode_fixed(float x);
-
-// ENC: x~' is stored as its fixed-point word (encode_fixed) instead of the fp32
-// value -- the form the unweighted push kernel gathers
-template <typename V, typename E, typename R, bool ENC = false>
+template <typename V, typename E, typename R>
 __device__ __forceinline__ void vertex_update_from(pr_args<V, E, R> const& a, V v, double s, R old, R ow, double base,
                                                    double pf, double& my_diff, double& my_dang)
 {
@@ -247,11 +243,10 @@ __device__ __forceinline__ void vertex_update_from(pr_args<V, E, R> const& a, V 
   R xv = R(0);
   if (ow == R(0)) my_dang += (double)nr;
   else xv = (R)((double)nr / (double)ow);
-  if constexpr (ENC) reinterpret_cast<uint32_t*>(a.x_out)[v] = encode_fixed(xv);
-  else a.x_out[v] = xv;
+  a.x_out[v] = xv;
 }
 
-template <typename V, typename E, typename R, bool ENC = false>
+template <typename V, typename E, typename R>
 __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, double s, double base, double pf,
                                               double& my_diff, double& my_dang)
 {
@@ -265,8 +260,7 @@ __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, do
   R xv = R(0);
   if (ow == R(0)) my_dang += (double)nr;
   else xv = (R)((double)nr / (double)ow);
-  if constexpr (ENC) reinterpret_cast<uint32_t*>(a.x_out)[v] = encode_fixed(xv);
-  else a.x_out[v] = xv;
+  a.x_out[v] = xv;
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -313,62 +307,57 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 // form below reads x~ in SOURCE order instead, so consecutive entries share cache
 // lines, and scatters into LDS, which is per-CU and scales with the CUs:
 //
-//  * destinations are cut into windows of kWin ids (kWin u64 accumulators = 64 KB
-//    of LDS per block);
-//  * push entries are the CSC edges re-sorted by (window, source) and packed in
-//    32 bits: (source - segment base) << kWinBits | (destination - window base),
-//    a segment being the sources of one window inside one 2^kSrcBits-aligned block;
-//  * units of <= kPushUnit entries never cross a segment, and blocks take
-//    contiguous runs of units, so a block flushes its LDS window to the global
-//    accumulator (integer atomics) only when the window changes -- once or twice;
+//  * destinations are cut into windows of 2^WB consecutive ids (2^WB u64
+//    accumulators = 32 KB (WB 12) or 64 KB (WB 13) of LDS per block; two blocks per CU);
+//  * push entries are the CSC edges sorted by (window, source) and packed in 32
+//    bits: (source - unit's first source) << WB | (destination - window base);
+//  * a unit is <= kPushUnit entries of one window whose sources span less than
+//    2^(32 - WB); a tile is a run of <= kTileUnits units of one window;
+//  * persistent blocks take tiles from a queue in unit order, sum a tile into the
+//    LDS window and flush it to the global accumulators (integer atomics) once;
 //  * sums are 64-bit fixed point (scale 2^62; every destination's sum is at most
 //    the total rank mass 1 since x~[u] w(u, v) summed over v is pr[u]).  Integer
 //    addition is associative: the result is bitwise deterministic whatever the
 //    order of the atomics.
 //
+// Ids descend by degree, so a window of low-degree destinations draws its sources
+// mostly from the hubs (few x~ lines); measured alternative: windows dealt runs of
+// 64 ids round robin (every window a sample of all degrees, equal sizes, blocks
+// sweeping the sources in lockstep) gathered 2.3x the L1->L2 requests and ran
+// 1.45x slower on RMAT-24.  The gathers that miss L2 are what this kernel waits
+// on: RMAT-24, 4K windows, ~0.09 distinct x~ lines of 128 B per entry.
+//
 // k_pr_apply then turns the sums into pr'/x~' per vertex (streaming) and resets the
 // accumulators.  Per iteration HBM traffic: 4E (entries) [+4E weights] + x~ lines
 // + 8V acc read + 8V acc reset + 16V vertex state.
-#ifndef CGX_WIN_BITS
-#define CGX_WIN_BITS 12  // RMAT-22 ms/iteration: 11 bits 0.212, 12 bits 0.204, 13 bits 0.217, 14 bits 0.347
-#endif
-constexpr int kWinBits     = CGX_WIN_BITS;  // destination window: 2^12 x 8 B = 32 KB of LDS accumulators
-constexpr int kWin         = 1 << kWinBits;
-constexpr int kSrcBits     = 32 - kWinBits;  // 20 source-offset bits per entry
-constexpr int kXcds        = 8;   // MI355X XCDs (workgroups are dealt to them round-robin)
-#ifndef CGX_XCD_SEGS
-#define CGX_XCD_SEGS 1
-#endif
-// Source segments of equal entry counts (1 = none).  Measured on RMAT-22, ms per
-// iteration: 8 segments pinned to the 8 XCDs (static kernel, each XCD's x~ slice
-// fits its L2) 0.367; 8 segments taken segment-major from the tile queue (the
-// blocks running at once share one or two slices) 0.27; no segments 0.221.  The
-// x~ misses these save cost less than the extra flushes and partial units.
-constexpr int kXcdSegs     = CGX_XCD_SEGS;
-#ifndef CGX_PUSH_THREADS
-#define CGX_PUSH_THREADS 1024
-#endif
-constexpr int kPushThreads = CGX_PUSH_THREADS;
-#ifndef CGX_PER_THREAD
-#define CGX_PER_THREAD 8
-#endif
-constexpr int kPerThread   = CGX_PER_THREAD;  // entries per thread per unit
+constexpr int kPushThreads = 1024;
+constexpr int kPerThread   = 8;  // entries per thread per unit
 constexpr int kPushUnit    = kPerThread * kPushThreads;
-#ifndef CGX_TILE_UNITS
-#define CGX_TILE_UNITS 8  // 8: 0.221, 16: 0.222, 32: 0.229, 64: 0.241 ms/iteration (RMAT-22)
-#endif
+constexpr int kTileUnits   = 8;  // RMAT-22: 8: 0.221, 16: 0.222, 32: 0.229, 64: 0.241 ms/iteration
+constexpr int kPushBlocks  = 512;  // persistent grid: two 1024-thread blocks per CU, 256 CUs
 #ifndef CGX_APPLY_BATCH
 #define CGX_APPLY_BATCH 4
 #endif
-constexpr int kTileUnits   = CGX_TILE_UNITS;  // units per queue tile at most (one LDS flush per tile)
 constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
 constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 
+// Window bits: 13 (8K destinations, 64 KB of LDS) from 2^22 destinations up,
+// where the x~ lines a window re-reads dominate (RMAT-24: 0.065 instead of 0.091
+// distinct lines per entry); 12 below (RMAT-22 measured 0.204 vs 0.217
+// ms/iteration for 4K vs 8K).  CGX_PR_WIN_BITS overrides (12 or 13).
+inline int push_win_bits(int64_t n_rows)
+{
+  if (char const* e = std::getenv("CGX_PR_WIN_BITS")) {
+    int b = std::atoi(e);
+    if (b == 12 || b == 13) return b;
+  }
+  return n_rows >= (int64_t(1) << 22) ? 13 : 12;
+}
+
 struct push_unit {
   int64_t k0, k1;  // entries [k0, k1)
-  int64_t base;    // source id of offset 0
-  int32_t win;     // destination window
-  int32_t seg;     // source segment (XCD) of the unit
+  int64_t base;    // source id of offset 0 (the unit's first source)
+  int64_t win;     // window
 };
 
 template <typename V, typename E, typename R>
@@ -378,19 +367,10 @@ struct push_args {
   R const* ew;  // entry weights (weighted graphs)
   push_unit const* units;
   int64_t nunits;
-  int64_t seg_start[kXcdSegs + 1];  // first unit of every source segment
-  unsigned long long* acc;  // [nwin * kWin] fixed-point sums, zero between iterations
-  int ablate;  // measurement only (CGX_PR_ABLATE): 1 no gathers, 2 no LDS atomics, 4 no push, 8 no flush
-  int64_t const* tiles;     // first unit of every (segment, window) tile, ntiles + 1 entries
+  unsigned long long* acc;  // [n_rows] fixed-point sums, zero between iterations
+  int64_t const* tiles;     // first unit of every tile, ntiles + 1 entries
   int64_t ntiles;
   unsigned int* tile_ctr;   // queue head (k_pr_apply resets it)
-  int32_t const* tile_win;  // window of every tile
-  // fused apply (k_pr_push_q<..., true>): the block finishing a window's last tile
-  // applies the window; the last window reduces the iteration
-  uint32_t const* win_tiles;
-  unsigned int* win_done;
-  unsigned int* tile_ctr_next;  // the other queue head (next iteration's), reset by the last window
-  int64_t nwin;
 };
 
 template <typename T>
@@ -404,41 +384,15 @@ __device__ __forceinline__ unsigned long long to_fixed(double v)
   return (unsigned long long)__double2ll_rn(v * kFixScale);
 }
 
-// Encoded x~ for unweighted fp32 graphs: a 32-bit word {shift:8, mantissa:24}
-// with to_fixed((double)x) == mantissa << shift exactly.  For x >= 2^-39 the
-// fixed-point value is the fp32 mantissa shifted left by e - 88 (e = biased
-// exponent); below that it is < 2^24 and is stored with shift 0.  The push kernel
-// then turns a gathered word into its 64-bit contribution with three integer
-// instructions (and, shift, 64-bit shift) instead of the fp64 conversion chain,
-// and the sums are the same bits as the fp64 form.  Requires 0 <= x < 2 (x~ <= 1).
-__device__ __forceinline__ uint32_t encode_fixed(float x)
-{
-  unsigned long long const f = to_fixed((double)x);
-  if (f < (1ull << 24)) return (uint32_t)f;
-  int const sh = 40 - __clzll((long long)f);  // top bit p = 63 - clz; shift = p - 23
-  return (uint32_t)(f >> sh) | ((uint32_t)sh << 24);
-}
-
-__device__ __forceinline__ unsigned long long decode_fixed(uint32_t w)
-{
-  return (unsigned long long)(w & 0xffffffu) << (w >> 24);
-}
-
-template <typename R>
-__global__ void k_encode_x(R* x, int64_t n)
-{
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
-    reinterpret_cast<uint32_t*>(x)[v] = encode_fixed((float)x[v]);
-}
-
-template <typename V, typename E, typename R>
+// add the LDS window to the global accumulators and clear it
+template <int WB, typename V, typename E, typename R>
 __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win)
 {
   __syncthreads();
-  unsigned long long* g = sa.acc + win * kWin;
-  for (int i = threadIdx.x; i < kWin; i += kPushThreads) {
+  unsigned long long* g = sa.acc + (win << WB);
+  for (int i = threadIdx.x; i < (1 << WB); i += kPushThreads) {
     unsigned long long v = acc[i];
-    if (v && !(sa.ablate & 8)) {
+    if (v) {
       atomicAdd(g + i, v);
       acc[i] = 0ull;
     }
@@ -446,232 +400,18 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
   __syncthreads();
 }
 
-template <typename V, typename E, typename R, bool WEIGHTED>
-__global__ __launch_bounds__(kPushThreads) void k_pr_push(push_args<V, E, R> sa)
-{
-  __shared__ unsigned long long acc[kWin];
-  auto const& a = sa.a;
-  if (a.st->done || (sa.ablate & 4)) return;
-  int const tid = threadIdx.x;
-  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
-  // contiguous runs of units (window-major order; measured faster than an
-  // XCD-blocked or segment-major schedule, which multiply the window flushes)
-  // XCD-aware: workgroup b runs on XCD b % 8, and the XCD's workgroups share the
-  // units of one source segment -- whose x~ slice then stays in that XCD's L2
-  int64_t u0, u1;
-  if (kXcdSegs == kXcds && gridDim.x % kXcds == 0) {
-    int const seg    = blockIdx.x % kXcds;
-    int64_t const nbx = gridDim.x / kXcds;
-    // rotate the XCDs' starting windows apart so they do not flush one window at once
-    int64_t const lb = (blockIdx.x / kXcds + seg * nbx / kXcds) % nbx;
-    int64_t const a0 = sa.seg_start[seg], cnt = sa.seg_start[seg + 1] - a0;
-    u0 = a0 + lb * cnt / nbx;
-    u1 = a0 + (lb + 1) * cnt / nbx;
-  } else {
-    u0 = blockIdx.x * sa.nunits / gridDim.x;
-    u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
-  }
-  int64_t cur      = u0 < u1 ? sa.units[u0].win : -1;
-  __syncthreads();
-  uint32_t ent[kPerThread];
-  R w[kPerThread];
-  push_unit pu{};
-  auto load_unit = [&](int64_t un, push_unit& p, uint32_t* e, R* ww) {
-    p = sa.units[un];
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      int64_t k = p.k0 + j * kPushThreads + tid;
-      e[j]      = k < p.k1 ? nt_load(sa.ent + k) : 0u;
-      if constexpr (WEIGHTED) ww[j] = k < p.k1 ? nt_load(sa.ew + k) : R(0);
-    }
-  };
-  if (u0 < u1) load_unit(u0, pu, ent, w);
-  for (int64_t un = u0; un < u1; ++un) {
-    uint32_t ent_n[kPerThread];
-    R w_n[kPerThread];
-    push_unit pu_n{};
-    if (un + 1 < u1) load_unit(un + 1, pu_n, ent_n, w_n);
-    if (pu.win != cur) {
-      flush_window<V, E, R>(sa, acc, cur);
-      cur = pu.win;
-    }
-    R x[kPerThread];
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      bool const ok = pu.k0 + j * kPushThreads + tid < pu.k1;
-      if (sa.ablate & 1) x[j] = ok ? R(1e-9) : R(0);
-      else x[j] = ok ? a.x_in[pu.base + (int64_t)(ent[j] >> kWinBits)] : R(0);
-    }
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      if (x[j] != R(0) && !(sa.ablate & 2)) {
-        double v = (double)x[j];
-        if constexpr (WEIGHTED) v *= (double)w[j];
-        atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
-      }
-    }
-    pu = pu_n;
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      ent[j] = ent_n[j];
-      if constexpr (WEIGHTED) w[j] = w_n[j];
-    }
-  }
-  if (cur >= 0) flush_window<V, E, R>(sa, acc, cur);
-}
-
-// Unweighted fp32 push over encoded x~ (the benchmark path).  Same schedule and
-// sums as k_pr_push, leaner inner loop (~8 VALU per edge instead of ~25, from the
-// SQ_INSTS_VALU counter): unit descriptors come through scalar loads, entry and
-// x~ addresses are 32-bit offsets from scalar bases, the contribution is
-// decode_fixed of the gathered word, and only partial units pay for lane masks.
-// The x~ gathers of a unit are issued before the next unit's entry loads, so the
-// wait for the gathers does not include the HBM latency of the prefetch.
-template <typename V, typename E, typename R>
-__global__ __launch_bounds__(kPushThreads) void k_pr_push_enc(push_args<V, E, R> sa)
-{
-  __shared__ unsigned long long acc[kWin];
-  if (sa.a.st->done) return;
-  int const tid = threadIdx.x;
-  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
-  int64_t const u0 = blockIdx.x * sa.nunits / gridDim.x;
-  int64_t const u1 = (blockIdx.x + 1) * sa.nunits / gridDim.x;
-  if (u0 >= u1) return;  // uniform
-  using cunit_t            = __attribute__((address_space(4))) push_unit const;
-  cunit_t* const units     = (cunit_t*)sa.units;  // read-only here: scalar loads
-  uint32_t const* const xe = reinterpret_cast<uint32_t const*>(sa.a.x_in);
-  int64_t cur              = units[u0].win;
-  __syncthreads();
-  uint32_t ent[kPerThread];
-  int64_t k0   = units[u0].k0;
-  int n        = (int)(units[u0].k1 - k0);
-  int64_t base = units[u0].base;
-  int win      = units[u0].win;
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent is padded
-  // Branch-free body: every lane loads (masked lanes read x~[base] and add 0), and
-  // the next unit's entries are always fetched (the last unit re-reads itself), so
-  // the waits the compiler places are "gathers done" (vmcnt = the 8 prefetches still
-  // in flight) and "prefetch done" -- not a full drain before every gather, which
-  // any per-lane branch around a load produces.
-  for (int64_t un = u0; un < u1; ++un) {
-    if (win != cur) {
-      flush_window<V, E, R>(sa, acc, cur);
-      cur = win;
-    }
-    uint32_t const* xb = xe + base;
-    uint32_t xw[kPerThread];
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      bool const ok = j * kPushThreads + tid < n;
-      xw[j]         = xb[ok ? (ent[j] >> kWinBits) : 0u];
-      xw[j]         = ok ? xw[j] : 0u;
-    }
-    int64_t const nx  = un + 1 < u1 ? un + 1 : un;
-    int64_t const k0n = units[nx].k0;
-    int const nn      = (int)(units[nx].k1 - k0n);
-    int64_t const bsn = units[nx].base;
-    int const winn    = units[nx].win;
-    uint32_t ent_n[kPerThread];
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
-    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) atomicAdd(&acc[ent[j] & (kWin - 1)], decode_fixed(xw[j]));
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) ent[j] = ent_n[j];
-    n    = nn;
-    base = bsn;
-    win  = winn;
-  }
-  flush_window<V, E, R>(sa, acc, cur);
-}
-
-// The push (default): persistent blocks take tiles -- runs of at most kTileUnits
-// units of one (source segment, window) -- from a queue in unit order.  A tile's
-// units are summed into the LDS window and flushed once.  The queue balances the
-// unequal cost of units (hub-source units gather from few lines, tail units from
-// many), which a static split cannot (0.221 vs 0.227 ms/iteration).  The unit body is
+// The push: persistent blocks take tiles from the queue.  The unit body is
 // branch-free (masked lanes load x~[base] and add 0; the next unit of the tile is
-// always prefetched, the last re-reading itself), so the only waits are "gathers
-// done" and "prefetch done".
-// Sum over a kPushThreads block; result valid in thread 0.  `sm` >= kPushThreads / 64.
-__device__ __forceinline__ double block_sum_push(double v, double* sm)
+// always prefetched, the last re-reading itself -- ent and ew are padded by a
+// unit), so the only waits are "gathers done" and "prefetch done".  A queue
+// balances the unequal cost of units (hub-source units gather from few lines,
+// tail units from many): 0.221 vs 0.227 ms/iteration for a static split (RMAT-22).
+template <int WB, typename V, typename E, typename R, bool WEIGHTED>
+__device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
 {
-  v = wave_sum(v);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double r = 0;
-  if (threadIdx.x == 0)
-    for (int i = 0; i < kPushThreads / 64; ++i) r += sm[i];
-  return r;
-}
-
-// Fused apply of window `win` (k_pr_apply's work for its kWin vertices) by the
-// block that finished the window's last tile.  Every tile's flush atomics have
-// completed (s_waitcnt vmcnt(0) before the window counter's increment), and the
-// sums are read with agent-scope atomic loads, coherent with those atomics.  The
-// window's (diff, dangling) partial goes to partials[2 win] (write-through); the
-// last window reduces the partials in window order -- deterministic -- and updates
-// the iteration state, then resets the next iteration's queue head.
-template <typename V, typename E, typename R>
-__device__ void apply_window(push_args<V, E, R> const& sa, int64_t win)
-{
-  __shared__ double sm[kPushThreads / 64];
-  __shared__ int s_last;
-  auto const& a     = sa.a;
-  double const base = a.st->base;
-  double const pf   = a.st->pers_factor;
-  double my_diff = 0, my_dang = 0;
-  int64_t const v0 = win * kWin;
-  int64_t const v1 = v0 + kWin < a.nv ? v0 + kWin : a.nv;
-  for (int64_t v = v0 + threadIdx.x; v < v1; v += kPushThreads) {
-    unsigned long long f = __hip_atomic_load(sa.acc + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f) __hip_atomic_store(sa.acc + v, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
-  }
-  double const bd = block_sum_push(my_diff, sm);
-  double const bg = block_sum_push(my_dang, sm);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(sa.win_done + win, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.partials[2 * win], bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.partials[2 * win + 1], bg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned t = __hip_atomic_fetch_add(&a.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last     = (t == (unsigned)sa.nwin - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  double d = 0, g = 0;
-  for (int64_t w = threadIdx.x; w < sa.nwin; w += kPushThreads) {
-    d += __hip_atomic_load(&a.partials[2 * w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g += __hip_atomic_load(&a.partials[2 * w + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  d = block_sum_push(d, sm);
-  g = block_sum_push(g, sm);
-  if (threadIdx.x == 0) {
-    update_state<V, E, R>(a, d, g, true);
-    // no block takes tiles from the next head during this launch
-    __hip_atomic_store(sa.tile_ctr_next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// The push (default): persistent blocks take tiles -- runs of at most kTileUnits
-// units of one (source segment, window) -- from a queue in unit order.  A tile's
-// units are summed into the LDS window and flushed once.  The queue balances the
-// unequal cost of units (hub-source units gather from few lines, tail units from
-// many), which a static split cannot (0.221 vs 0.227 ms/iteration).  The unit body is
-// branch-free (masked lanes load x~[base] and add 0; the next unit of the tile is
-// always prefetched, the last re-reading itself), so the only waits are "gathers
-// done" and "prefetch done".  FUSED: the apply runs per window inside this kernel
-// (apply_window) instead of as k_pr_apply.
-template <typename V, typename E, typename R, bool WEIGHTED, bool FUSED = false>
-__global__ __launch_bounds__(kPushThreads) void k_pr_push_q(push_args<V, E, R> sa)
-{
+  constexpr int kWin = 1 << WB;
   __shared__ unsigned long long acc[kWin];
-  __shared__ int s_tile;
-  __shared__ int s_fin;
+  __shared__ int64_t s_tile;
   if (sa.a.st->done) return;
   int const tid = threadIdx.x;
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
@@ -679,75 +419,79 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_q(push_args<V, E, R> s
   cunit_t* const units = (cunit_t*)sa.units;  // read-only here: scalar loads
   R const* const x     = sa.a.x_in;
   while (true) {
-    if (tid == 0) s_tile = (int)atomicAdd(sa.tile_ctr, 1u);
+    if (tid == 0) s_tile = (int64_t)atomicAdd(sa.tile_ctr, 1u);
     __syncthreads();
     int64_t const t = s_tile;
+    __syncthreads();  // every thread has read s_tile before thread 0 takes the next tile
     if (t >= sa.ntiles) break;  // uniform
     int64_t const ua = sa.tiles[t], ub = sa.tiles[t + 1];
-    int64_t const win = sa.tile_win[t];
-    if (ua < ub) {  // uniform; empty tiles stand for windows without entries
-      int64_t k0   = units[ua].k0;
-      int n        = (int)(units[ua].k1 - k0);
-      int64_t base = units[ua].base;
-      uint32_t ent[kPerThread];
-      R w[kPerThread];
+    int64_t const win = units[ua].win;
+    int64_t k0   = units[ua].k0;
+    int n        = (int)(units[ua].k1 - k0);
+    int64_t base = units[ua].base;
+    uint32_t ent[kPerThread];
+    R w[kPerThread];
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+      ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);
+      if constexpr (WEIGHTED) w[j] = nt_load(sa.ew + k0 + j * kPushThreads + tid);
+    }
+    for (int64_t un = ua; un < ub; ++un) {
+      R const* const xb = x + base;
+      R xv[kPerThread];
 #pragma unroll
       for (int j = 0; j < kPerThread; ++j) {
-        ent[j] = nt_load(sa.ent + k0 + j * kPushThreads + tid);  // ent (and ew) are padded by a unit
-        if constexpr (WEIGHTED) w[j] = nt_load(sa.ew + k0 + j * kPushThreads + tid);
+        bool const ok = j * kPushThreads + tid < n;
+        xv[j]         = xb[ok ? (ent[j] >> WB) : 0u];
+        xv[j]         = ok ? xv[j] : R(0);
       }
-      for (int64_t un = ua; un < ub; ++un) {
-        R const* const xb = x + base;
-        R xv[kPerThread];
+      int64_t const nx  = un + 1 < ub ? un + 1 : un;
+      int64_t const k0n = units[nx].k0;
+      int const nn      = (int)(units[nx].k1 - k0n);
+      int64_t const bsn = units[nx].base;
+      uint32_t ent_n[kPerThread];
+      R w_n[kPerThread];
 #pragma unroll
-        for (int j = 0; j < kPerThread; ++j) {
-          bool const ok = j * kPushThreads + tid < n;
-          xv[j]         = xb[ok ? (ent[j] >> kWinBits) : 0u];
-          xv[j]         = ok ? xv[j] : R(0);
-        }
-        int64_t const nx  = un + 1 < ub ? un + 1 : un;
-        int64_t const k0n = units[nx].k0;
-        int const nn      = (int)(units[nx].k1 - k0n);
-        int64_t const bsn = units[nx].base;
-        uint32_t ent_n[kPerThread];
-        R w_n[kPerThread];
-#pragma unroll
-        for (int j = 0; j < kPerThread; ++j) {
-          ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
-          if constexpr (WEIGHTED) w_n[j] = nt_load(sa.ew + k0n + j * kPushThreads + tid);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
-#pragma unroll
-        for (int j = 0; j < kPerThread; ++j) {
-          double v = (double)xv[j];
-          if constexpr (WEIGHTED) v *= (double)w[j];
-          atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
-        }
-#pragma unroll
-        for (int j = 0; j < kPerThread; ++j) {
-          ent[j] = ent_n[j];
-          if constexpr (WEIGHTED) w[j] = w_n[j];
-        }
-        n    = nn;
-        base = bsn;
+      for (int j = 0; j < kPerThread; ++j) {
+        ent_n[j] = nt_load(sa.ent + k0n + j * kPushThreads + tid);
+        if constexpr (WEIGHTED) w_n[j] = nt_load(sa.ew + k0n + j * kPushThreads + tid);
       }
-      flush_window<V, E, R>(sa, acc, win);  // ends with a barrier: s_tile may be rewritten
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        double v = (double)xv[j];
+        if constexpr (WEIGHTED) v *= (double)w[j];
+        atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
+      }
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        ent[j] = ent_n[j];
+        if constexpr (WEIGHTED) w[j] = w_n[j];
+      }
+      n    = nn;
+      base = bsn;
     }
-    if constexpr (FUSED) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's flush atomics are performed
-      __syncthreads();
-      if (tid == 0) {
-        unsigned d = __hip_atomic_fetch_add(sa.win_done + win, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_fin      = (d + 1 == sa.win_tiles[win]);
-      }
-      __syncthreads();
-      if (s_fin) apply_window<V, E, R>(sa, win);  // uniform
-      __syncthreads();  // s_tile / s_fin are rewritten next
-    }
+    flush_window<WB, V, E, R>(sa, acc, win);
   }
 }
 
-template <typename V, typename E, typename R, bool ENC = false>
+// Two 1024-thread blocks per CU need <= 64 VGPRs (8 waves per SIMD): the bound
+// takes the unweighted kernels from 62-65 to 47-54 VGPRs with no spill (at 65 only
+// one block fits a CU).  fp64 entry weights would spill 42 VGPRs under it, so that
+// instantiation keeps one block per CU.
+template <int WB, typename V, typename E, typename R, bool WEIGHTED>
+__global__ __launch_bounds__(kPushThreads, 8) void k_pr_push_q(push_args<V, E, R> sa)
+{
+  push_body<WB, V, E, R, WEIGHTED>(sa);
+}
+
+template <int WB, typename V, typename E, typename R, bool WEIGHTED>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push_q_wide(push_args<V, E, R> sa)
+{
+  push_body<WB, V, E, R, WEIGHTED>(sa);
+}
+
+template <typename V, typename E, typename R>
 __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 {
   auto const& a = sa.a;
@@ -773,14 +517,14 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 #pragma unroll
     for (int j = 0; j < kApplyBatch; ++j) {
       if (f[j]) sa.acc[v + j * stride] = 0ull;
-      vertex_update_from<V, E, R, ENC>(a, (V)(v + j * stride), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j],
-                                       base, pf, my_diff, my_dang);
+      vertex_update_from<V, E, R>(a, (V)(v + j * stride), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base,
+                                  pf, my_diff, my_dang);
     }
   }
   for (; v < a.nv; v += stride) {
     unsigned long long f = sa.acc[v];
     if (f) sa.acc[v] = 0ull;
-    vertex_update<V, E, R, ENC>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
+    vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
 }
@@ -800,94 +544,105 @@ __global__ void k_edge_rows(E const* off, int64_t nv, int64_t ne, uint32_t* rows
   }
 }
 
-struct seg_bounds {
-  int64_t lo[kXcdSegs + 1];  // source segment s = [lo[s], lo[s + 1])
-};
-
-template <typename V>
-__global__ void k_push_keys(V const* idx, uint32_t const* rows, int64_t ne, seg_bounds sb, uint64_t* keys,
-                            uint32_t* vals)
+// key = window << 32 | source, value = edge position
+template <typename C>
+__global__ void k_push_keys(C const* cols, uint32_t const* rows, int64_t ne, int wb, uint64_t* keys, uint32_t* vals)
 {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t src = (uint32_t)idx[e];
-    uint64_t seg = 0;
-    while (seg + 1 < kXcdSegs && (int64_t)src >= sb.lo[seg + 1]) ++seg;
-    keys[e] = (seg << 51) | ((uint64_t)(rows[e] >> kWinBits) << 32) | src;
+    keys[e] = ((uint64_t)(rows[e] >> wb) << 32) | (uint32_t)cols[e];
     vals[e] = (uint32_t)e;
   }
 }
 
-// per-source entry counts (for segments of equal work)
-template <typename C>
-__global__ void k_src_counts(C const* cols, int64_t ne, unsigned long long* cnt)
+// first position of every window w in [0, nwin] among the sorted keys
+__global__ void k_win_starts(uint64_t const* keys, int64_t ne, int64_t nwin, int64_t* ws)
 {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(cnt + (uint32_t)cols[e], 1ull);
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = ne;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)(keys[mid] >> 32) < w) lo = mid + 1;
+      else hi = mid;
+    }
+    ws[w] = lo;
+  }
 }
 
-// lo[s] = first source whose entry prefix reaches s * ne / kXcdSegs
-__global__ void k_seg_bounds(unsigned long long const* pre, int64_t n_cols, int64_t ne, int64_t* lo)
-{
-  int sg = threadIdx.x;
-  if (sg > kXcdSegs) return;
-  if (sg == kXcdSegs) {
-    lo[sg] = n_cols;
-    return;
-  }
-  unsigned long long target = (unsigned long long)(sg * ne / kXcdSegs);
-  int64_t a = 0, b = n_cols;  // first source with pre >= target
-  while (a < b) {
-    int64_t mid = (a + b) >> 1;
-    if (pre[mid] < target) a = mid + 1;
-    else b = mid;
-  }
-  lo[sg] = sg == 0 ? 0 : a;
-}
-
-__global__ void k_seg_unit_start(push_unit const* units, int64_t nunits, int64_t* start)
-{
-  int sg = threadIdx.x;
-  if (sg > kXcdSegs) return;
-  int64_t a = 0, b = nunits;  // first unit with seg >= sg
-  while (a < b) {
-    int64_t mid = (a + b) >> 1;
-    if (units[mid].seg < sg) a = mid + 1;
-    else b = mid;
-  }
-  start[sg] = a;
-}
-
-// key = (source segment, window, source); unit starts: a new (segment, window,
-// 2^kSrcBits source block) or every kPushUnit-th entry
-__global__ void k_unit_flags(uint64_t const* keys, int64_t ne, uint32_t* flag)
+// unit heads: a window's first entry, every entry at a multiple of kPushUnit (so
+// whole units start 32 KB-aligned in ent: measured 5 % faster than window-relative
+// units on RMAT-22), and -- only inside such a chunk whose sources span 2^sb or
+// more -- every change of the aligned 2^sb source block, so an offset from the
+// unit's first source fits sb bits
+__global__ void k_unit_flags(uint64_t const* keys, int64_t ne, int64_t const* ws, int sb, uint32_t* flag)
 {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
-    bool head = k == 0 || (k % kPushUnit) == 0 || (keys[k] >> kSrcBits) != (keys[k - 1] >> kSrcBits);
-    flag[k]   = head ? 1u : 0u;
+    int64_t const w  = (int64_t)(keys[k] >> 32);
+    int64_t const w0 = ws[w], w1 = ws[w + 1];
+    bool head        = k == w0 || k % kPushUnit == 0;
+    if (!head) {
+      int64_t const a   = k / kPushUnit * kPushUnit;
+      int64_t const c0  = a > w0 ? a : w0;
+      int64_t const c1  = a + kPushUnit < w1 ? a + kPushUnit : w1;
+      uint32_t const s0 = (uint32_t)keys[c0], s1 = (uint32_t)keys[c1 - 1];
+      head = ((s1 - s0) >> sb) != 0 && ((uint32_t)keys[k] >> sb) != ((uint32_t)keys[k - 1] >> sb);
+    }
+    flag[k] = head ? 1u : 0u;
   }
 }
 
-template <typename R>
-__global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, R const* w,
-                            uint32_t const* flag, uint32_t const* uid, int64_t ne, uint32_t* ent, R* ew,
-                            push_unit* units)
+__global__ void k_unit_heads(uint64_t const* keys, uint32_t const* flag, uint32_t const* uid, int64_t ne,
+                             push_unit* units)
 {
-  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t key = keys[k];
-    uint32_t e   = vals[k];
-    uint32_t src = (uint32_t)key;
-    ent[k]       = ((src & ((1u << kSrcBits) - 1)) << kWinBits) | (rows[e] & (kWin - 1));
-    if (w) ew[k] = w[e];
-    if (flag[k])
-      units[uid[k]] = push_unit{k, 0, (int64_t)(src >> kSrcBits) << kSrcBits, (int32_t)((key >> 32) & ((1u << 19) - 1)),
-                                (int32_t)(key >> 51)};
-  }
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x)
+    if (flag[k]) units[uid[k]] = push_unit{k, 0, (int64_t)(uint32_t)keys[k], (int64_t)(keys[k] >> 32)};
 }
 
 __global__ void k_unit_ends(push_unit* units, int64_t nunits, int64_t ne)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nunits; i += (int64_t)gridDim.x * blockDim.x)
     units[i].k1 = i + 1 < nunits ? units[i + 1].k0 : ne;
+}
+
+template <typename R>
+__global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, R const* w,
+                            uint32_t const* flag, uint32_t const* uid, push_unit const* units, int64_t ne, int wb,
+                            uint32_t* ent, R* ew)
+{
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const e   = vals[k];
+    int64_t const u    = (int64_t)uid[k] + flag[k] - 1;
+    uint32_t const off = (uint32_t)((uint32_t)keys[k] - units[u].base);
+    ent[k]             = (off << wb) | (rows[e] & ((1u << wb) - 1));
+    if (w) ew[k] = w[e];
+  }
+}
+
+// tile heads: a window's first unit and every kTileUnits-th unit of a window
+__global__ void k_tile_flags(push_unit const* units, int64_t nunits, int64_t const* wu, uint32_t* flag)
+{
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < nunits; u += (int64_t)gridDim.x * blockDim.x)
+    flag[u] = (u - wu[units[u].win]) % kTileUnits == 0 ? 1u : 0u;
+}
+
+__global__ void k_tile_heads(uint32_t const* flag, uint32_t const* tid, int64_t nunits, int64_t* tiles)
+{
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u <= nunits; u += (int64_t)gridDim.x * blockDim.x)
+    if (u == nunits) tiles[tid[nunits]] = nunits;
+    else if (flag[u]) tiles[tid[u]] = u;
+}
+
+// first unit of every window w in [0, nwin] (units are in window order)
+__global__ void k_win_units(push_unit const* units, int64_t nunits, int64_t nwin, int64_t* wu)
+{
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nunits;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (units[mid].win < w) lo = mid + 1;
+      else hi = mid;
+    }
+    wu[w] = lo;
+  }
 }
 
 // Push schedule of an edge list given as (row = destination, col = source) with
@@ -900,49 +655,53 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.built = true;
   pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
   if (!pp.ok) return;
-  int64_t nwin = (n_rows + kWin - 1) / kWin;
-  pp.nacc      = std::max<int64_t>(nwin * kWin, 1);
+  int const wb       = push_win_bits(n_rows);
+  int const sb       = 32 - wb;
+  int64_t const nwin = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
+  pp.win_bits        = wb;
+  pp.nwin            = nwin;
+  pp.nacc            = nwin << wb;
   pp.acc.set_stream(s);
   pp.acc.resize(pp.nacc * sizeof(unsigned long long));
   HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
+  pp.tile_ctr.set_stream(s);
+  pp.tile_ctr.resize(sizeof(unsigned int));
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, sizeof(unsigned int), s));
   pp.nunits = 0;
+  pp.ntiles = 0;
   if (ne == 0) return;
   dbuf<uint64_t> keys_out(ne, s);
   dbuf<uint32_t> vals_out(ne, s);
-  seg_bounds sb{};
-  if (kXcdSegs == 1) {  // one segment: no per-source counting pass
-    sb.lo[0] = 0;
-    sb.lo[kXcdSegs] = n_cols;
-  } else {  // source segments of equal entry counts (one per XCD)
-    dbuf<unsigned long long> cnt(n_cols + 1, s), pre(n_cols + 1, s);
-    fill<unsigned long long>(cnt.data(), n_cols + 1, 0ull, s);
-    hipLaunchKernelGGL(k_src_counts<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, ne, cnt.data());
-    CGX_LAUNCH_CHECK();
-    exclusive_scan<unsigned long long, unsigned long long>(cnt.data(), pre.data(), n_cols + 1, s);
-    dbuf<int64_t> lo(kXcdSegs + 1, s);
-    hipLaunchKernelGGL(k_seg_bounds, dim3(1), dim3(64), 0, s, pre.data(), n_cols, ne, lo.data());
-    CGX_LAUNCH_CHECK();
-    auto hl = to_host(lo.data(), kXcdSegs + 1, s);
-    for (int i = 0; i <= kXcdSegs; ++i) sb.lo[i] = hl[i];
-  }
   {
     dbuf<uint64_t> keys(ne, s);
     dbuf<uint32_t> vals(ne, s);
-    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, sb,
+    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
                        keys.data(), vals.data());
     CGX_LAUNCH_CHECK();
     radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
-                                         51 + bits_for(kXcdSegs - 1), s);
+                                         32 + bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)), s);
   }
+  dbuf<int64_t> ws(nwin + 1, s);
+  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
+                     nwin, ws.data());
+  CGX_LAUNCH_CHECK();
   dbuf<uint32_t> flag(ne + 1, s), uid(ne + 1, s);
   hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                     flag.data());
+                     ws.data(), sb, flag.data());
   CGX_LAUNCH_CHECK();
   fill<uint32_t>(flag.data() + ne, 1, 0u, s);
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
-  int64_t nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
+  int64_t const nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
+  pp.units.set_stream(s);
+  pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
+  push_unit* units = pp.units.data<push_unit>();
+  hipLaunchKernelGGL(k_unit_heads, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
+                     flag.data(), uid.data(), ne, units);
+  CGX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, ne);
+  CGX_LAUNCH_CHECK();
   pp.ent.set_stream(s);
-  pp.ent.resize((ne + kPushUnit) * sizeof(uint32_t));  // padded: k_pr_push_enc loads whole units
+  pp.ent.resize((ne + kPushUnit) * sizeof(uint32_t));  // padded: the kernel loads whole units
   HIP_CHECK(hipMemsetAsync(pp.ent.data<uint32_t>() + ne, 0, kPushUnit * sizeof(uint32_t), s));
   pp.ew.set_stream(s);
   if (w) {
@@ -951,61 +710,29 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   } else {
     pp.ew.release();
   }
-  pp.units.set_stream(s);
-  pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
   hipLaunchKernelGGL(k_push_pack<R>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                     vals_out.data(), rows, w, flag.data(), uid.data(), ne, pp.ent.data<uint32_t>(),
-                     w ? pp.ew.data<R>() : nullptr, pp.units.data<push_unit>());
+                     vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
+                     w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s,
-                     pp.units.data<push_unit>(), nunits, ne);
+  // tiles: runs of <= kTileUnits units of one window, in unit (= queue) order
+  dbuf<int64_t> wu(nwin + 1, s);
+  hipLaunchKernelGGL(k_win_units, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, nwin,
+                     wu.data());
+  CGX_LAUNCH_CHECK();
+  dbuf<uint32_t> tflag(nunits + 1, s), tid(nunits + 1, s);
+  hipLaunchKernelGGL(k_tile_flags, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, wu.data(),
+                     tflag.data());
+  CGX_LAUNCH_CHECK();
+  fill<uint32_t>(tflag.data() + nunits, 1, 0u, s);
+  exclusive_scan<uint32_t, uint32_t>(tflag.data(), tid.data(), nunits + 1, s);
+  int64_t const ntiles = (int64_t)to_host(tid.data() + nunits, 1, s)[0];
+  pp.tiles.set_stream(s);
+  pp.tiles.resize((ntiles + 1) * sizeof(int64_t));
+  hipLaunchKernelGGL(k_tile_heads, dim3(grid_for(nunits + 1, kBlock, 4096)), dim3(kBlock), 0, s, tflag.data(),
+                     tid.data(), nunits, pp.tiles.data<int64_t>());
   CGX_LAUNCH_CHECK();
   pp.nunits = nunits;
-  {
-    dbuf<int64_t> st(kXcdSegs + 1, s);
-    hipLaunchKernelGGL(k_seg_unit_start, dim3(1), dim3(64), 0, s, pp.units.data<push_unit>(), nunits, st.data());
-    CGX_LAUNCH_CHECK();
-    pp.seg_start = to_host(st.data(), kXcdSegs + 1, s);
-  }
-  {  // (segment, window) tiles: runs of units, in unit (= queue) order
-    auto hu = to_host(pp.units.data<push_unit>(), nunits, s);
-    std::vector<int64_t> tiles;
-    // hub windows hold millions of entries: a tile is at most kTileUnits units
-    std::vector<int32_t> twin;
-    std::vector<uint32_t> wt(nwin, 0u);
-    for (int64_t u = 0; u < nunits; ++u)
-      if (u == 0 || hu[u].win != hu[u - 1].win || hu[u].seg != hu[u - 1].seg || u - tiles.back() >= kTileUnits) {
-        tiles.push_back(u);
-        twin.push_back(hu[u].win);
-        ++wt[hu[u].win];
-      }
-    tiles.push_back(nunits);
-    // every window gets at least one (possibly empty) tile, so the fused apply
-    // of k_pr_push_q reaches every vertex
-    for (int64_t w = 0; w < nwin; ++w)
-      if (!wt[w]) {
-        tiles.push_back(nunits);
-        twin.push_back((int32_t)w);
-        wt[w] = 1;
-      }
-    pp.ntiles = (int64_t)tiles.size() - 1;
-    pp.tiles.set_stream(s);
-    pp.tiles.resize(tiles.size() * sizeof(int64_t));
-    to_device(pp.tiles.data<int64_t>(), tiles.data(), tiles.size(), s);
-    pp.tile_win.set_stream(s);
-    pp.tile_win.resize(twin.size() * sizeof(int32_t));
-    to_device(pp.tile_win.data<int32_t>(), twin.data(), twin.size(), s);
-    pp.win_tiles.set_stream(s);
-    pp.win_tiles.resize(wt.size() * sizeof(uint32_t));
-    to_device(pp.win_tiles.data<uint32_t>(), wt.data(), wt.size(), s);
-  }
-  pp.nwin = nwin;
-  pp.win_done.set_stream(s);
-  pp.win_done.resize(std::max<int64_t>(nwin, 1) * sizeof(uint32_t));
-  HIP_CHECK(hipMemsetAsync(pp.win_done.data(), 0, std::max<int64_t>(nwin, 1) * sizeof(uint32_t), s));
-  pp.tile_ctr.set_stream(s);
-  pp.tile_ctr.resize(2 * sizeof(unsigned int));
-  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, 2 * sizeof(unsigned int), s));
+  pp.ntiles = ntiles;
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -1064,53 +791,30 @@ dbuf<V> internal_ids(handle_t& h, graph_t& g, array_view_t const* ext)
   return ids;
 }
 
-// The encoded-x~ push (k_pr_push_enc) is opt-in for unweighted fp32 runs
-// (CGX_PR_PUSH=enc).  Its sums are the same bits as k_pr_push, but on RMAT-22 it
-// measured no faster (0.228 vs 0.225 ms/iteration, same-box A/B): the push is
-// bound by gather latency, not VALU, so the default stays the plain kernel.
-template <typename R>
-bool use_encoded_push(bool weighted)
-{
-  if (weighted || !std::is_same_v<R, float>) return false;
-  char const* e = std::getenv("CGX_PR_PUSH");
-  return e && std::string(e) == "enc";
-}
-
-// Push kernel choice: the tile queue (k_pr_push_q, default); CGX_PR_PUSH=static
-// the statically split k_pr_push; CGX_PR_PUSH=enc the static encoded-x~ kernel
-// (unweighted fp32 only).  All give the same bits (integer sums).
-enum { kPushQueue = 0, kPushStatic = 1, kPushEnc = 2 };
-template <typename R>
-int push_mode(bool weighted)
-{
-  if (use_encoded_push<R>(weighted)) return kPushEnc;
-  char const* e = std::getenv("CGX_PR_PUSH");
-  return e && std::string(e) == "static" ? kPushStatic : kPushQueue;
-}
-
 template <typename V, typename E, typename R>
 void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 {
+  sa.ent      = pp.ent.data<uint32_t>();
+  sa.ew       = pp.ew.empty() ? nullptr : pp.ew.data<R>();
+  sa.units    = pp.units.data<push_unit>();
+  sa.nunits   = pp.nunits;
+  sa.acc      = pp.acc.data<unsigned long long>();
   sa.tiles    = pp.tiles.data<int64_t>();
   sa.ntiles   = pp.ntiles;
   sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
-  sa.tile_win = pp.tile_win.data<int32_t>();
-  sa.win_tiles = pp.win_tiles.data<uint32_t>();
-  sa.win_done  = pp.win_done.data<unsigned int>();
-  sa.nwin      = pp.nwin;
-  sa.tile_ctr_next = sa.tile_ctr ? sa.tile_ctr + 1 : nullptr;
-  if (sa.tile_ctr) HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, 2 * sizeof(unsigned int), s));
-  if (sa.win_done) HIP_CHECK(hipMemsetAsync(sa.win_done, 0, std::max<int64_t>(pp.nwin, 1) * sizeof(unsigned int), s));
+  HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, sizeof(unsigned int), s));
 }
 
-// Fused apply (k_pr_push_q<..., FUSED>) for single-GPU queue runs, opt-in with
-// CGX_PR_FUSED=1.  Same results, but slower on RMAT-22 (0.211 vs 0.205 ms/iteration,
-// same-box A/B): the per-tile drain, barriers and window-counter atomic cost more
-// than the separate k_pr_apply launch (~25 us) they remove.
-inline bool fused_apply_enabled()
+// the push kernel for the schedule's window bits
+template <typename V, typename E, typename R>
+auto push_kernel(pr_push_t const& pp, bool weighted)
 {
-  char const* e = std::getenv("CGX_PR_FUSED");
-  return e && std::string(e) == "1";
+  constexpr bool wide = sizeof(R) == 8;  // fp64 weights: no 8-waves bound (see k_pr_push_q_wide)
+  if (pp.win_bits == 13)
+    return weighted ? (wide ? k_pr_push_q_wide<13, V, E, R, true> : k_pr_push_q<13, V, E, R, true>)
+                    : k_pr_push_q<13, V, E, R, false>;
+  return weighted ? (wide ? k_pr_push_q_wide<12, V, E, R, true> : k_pr_push_q<12, V, E, R, true>)
+                  : k_pr_push_q<12, V, E, R, false>;
 }
 
 template <typename V, typename E, typename R>
@@ -1201,7 +905,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   // iteration state
   int const nblk_iter = (int)adj.num_items;
   int const nblk_init = (int)grid_for(nv, kBlock, 1024);
-  dbuf<double> partials(2 * std::max<int64_t>({nblk_iter, nblk_init, 2048, (nv + kWin - 1) / kWin}), s);
+  dbuf<double> partials(2 * std::max<int64_t>({nblk_iter, nblk_init, 2048, (nv + 4095) / 4096}), s);
   dbuf<pr_state> st(1, s);
   HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(pr_state), s));
   dbuf<R> xa(nv, s), xb(nv, s);
@@ -1236,32 +940,12 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   push = push && adj.pr.ok;
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  int const pmode = push_mode<R>(g.weighted);
-  bool const enc  = push && pmode == kPushEnc;
-  auto pkernel    = pmode == kPushQueue ? (g.weighted ? k_pr_push_q<V, E, R, true> : k_pr_push_q<V, E, R, false>)
-                    : g.weighted        ? k_pr_push<V, E, R, true>
-                    : enc               ? k_pr_push_enc<V, E, R>
-                                        : k_pr_push<V, E, R, false>;
-  auto akernel   = enc ? k_pr_apply<V, E, R, true> : k_pr_apply<V, E, R, false>;
+  auto pkernel = push_kernel<V, E, R>(adj.pr, g.weighted);
   if (push) {
-    sa.ent    = adj.pr.ent.data<uint32_t>();
-    sa.ew     = g.weighted ? adj.pr.ew.data<R>() : nullptr;
-    sa.units  = adj.pr.units.data<push_unit>();
-    sa.nunits = adj.pr.nunits;
-    for (int i = 0; i <= kXcdSegs; ++i) sa.seg_start[i] = i < (int)adj.pr.seg_start.size() ? adj.pr.seg_start[i] : 0;
-    sa.acc    = adj.pr.acc.data<unsigned long long>();
-    if (char const* ab = std::getenv("CGX_PR_ABLATE")) sa.ablate = std::atoi(ab);
-    if (enc) {
-      hipLaunchKernelGGL((k_encode_x<R>), dim3(grid_for(nv, kBlock, 4096)), dim3(kBlock), 0, s, xa.data(), nv);
-      CGX_LAUNCH_CHECK();
-    }
     set_queue_args(sa, adj.pr, s);
-    // 64 KB LDS: two blocks per CU
-    nblk_push  = (int)std::min<int64_t>(pmode == kPushQueue ? sa.ntiles : sa.nunits, 256 * 2);
+    nblk_push  = (int)std::min<int64_t>(sa.ntiles, kPushBlocks);
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
-  bool const fused = push && pmode == kPushQueue && nblk_push > 0 && fused_apply_enabled();
-  auto fkernel     = g.weighted ? k_pr_push_q<V, E, R, true, true> : k_pr_push_q<V, E, R, false, true>;
   // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
   // predicted remainder.  Profiling records one pair of pooled HIP events around each chunk -- an event
   // between every two iterations cost a ~10 us queue gap per iteration -- and
@@ -1285,14 +969,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       a.x_out = bufs[(launched + 1) & 1];
       if (push) {
         sa.a = a;
-        if (fused) {  // queue heads alternate: the launch resets the one the next uses
-          sa.tile_ctr      = adj.pr.tile_ctr.data<unsigned int>() + (launched & 1);
-          sa.tile_ctr_next = adj.pr.tile_ctr.data<unsigned int>() + ((launched + 1) & 1);
-          hipLaunchKernelGGL(fkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
-        } else {
-          if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
-          hipLaunchKernelGGL(akernel, dim3(nblk_apply), dim3(kBlock), 0, s, sa);
-        }
+        if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
+        hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sa);
       } else {
         hipLaunchKernelGGL(kernel, dim3(nblk_iter), dim3(kBlock), 0, s, a);
       }
@@ -1624,26 +1302,15 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   if (max_iter == 0) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
 
   push_args<V, E, R> sp{}, sap{};
-  sp.a      = a;
-  sp.ent    = blk.pp.ent.data<uint32_t>();
-  sp.ew     = g.weighted ? blk.pp.ew.data<R>() : nullptr;
-  sp.units  = blk.pp.units.data<push_unit>();
-  sp.nunits = blk.pp.nunits;
-  for (int i = 0; i <= kXcdSegs; ++i) sp.seg_start[i] = i < (int)blk.pp.seg_start.size() ? blk.pp.seg_start[i] : 0;
-  sp.acc    = blk.pp.acc.data<unsigned long long>();
-  int const pmode = push_mode<R>(g.weighted);
-  bool const enc  = pmode == kPushEnc;
+  sp.a = a;
   set_queue_args(sp, blk.pp, s);
-  if (enc && n_own > 0) {  // x~ of the init pass -> encoded words before the first allgather
-    hipLaunchKernelGGL((k_encode_x<R>), dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s, x_send.data(), n_own);
-    CGX_LAUNCH_CHECK();
-  }
-  sap       = sp;
+  sap = sp;
   // one grid row (R = 1): the block's sums are already the owner's; the apply reads
   // and re-zeroes them in place, no column collective
   bool const col_reduce = R_ > 1;
   sap.acc   = col_reduce ? acc_own.data() : sp.acc;
-  int const nblk_push  = (int)std::min<int64_t>(pmode == kPushQueue ? sp.ntiles : sp.nunits, 256 * 2);
+  int const nblk_push  = (int)std::min<int64_t>(sp.ntiles, kPushBlocks);
+  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
 
@@ -1662,19 +1329,14 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       int const chunk = next_chunk(hst, eps, a.max_iter);
       for (int i = 0; i < chunk; ++i) {
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
-        if (nblk_push)
-          hipLaunchKernelGGL((pmode == kPushQueue ? (g.weighted ? k_pr_push_q<V, E, R, true> : k_pr_push_q<V, E, R, false>)
-                              : g.weighted        ? k_pr_push<V, E, R, true>
-                              : enc               ? k_pr_push_enc<V, E, R>
-                                                  : k_pr_push<V, E, R, false>),
-                             dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
+        if (nblk_push && blk.pp.nunits)
+          hipLaunchKernelGGL(mg_pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
         CGX_LAUNCH_CHECK();
         if (col_reduce) {
           ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
           if (block_acc_bytes) HIP_CHECK(hipMemsetAsync(sp.acc, 0, block_acc_bytes, s));
         }
-        hipLaunchKernelGGL((enc ? k_pr_apply<V, E, R, true> : k_pr_apply<V, E, R, false>), dim3(nblk_apply),
-                           dim3(kBlock), 0, s, sap);
+        hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
         CGX_LAUNCH_CHECK();
         ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
         hipLaunchKernelGGL((k_mg_finish_guarded<V, E, R>), dim3(1), dim3(64), 0, s, a, true);
