@@ -489,6 +489,7 @@ def main():
                          "(code-path rehearsal with several ranks on one GPU; not a performance number)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--traffic-child", choices=["pagerank", "bfs"], default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--bfs-only", action="store_true", help="A/B aid: only the BFS leg, its dict on stdout")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -518,6 +519,11 @@ def main():
         return
     if args.traffic_child == "bfs":
         bfs_leg(p, args, child=True)
+        return
+    if args.bfs_only:
+        r = bfs_leg(p, args)
+        log(f"[bench] bfs RMAT-{args.bfs_scale}: {r['mteps_harmonic_mean']:.1f} MTEPS, {r['ms_mean']:.3f} ms/traversal")
+        print(json.dumps(r), flush=True)
         return
 
     r = pagerank_leg(p, args, args.scale, args.steps, args.warmup, args.ctx)

@@ -104,10 +104,12 @@ struct pr_push_t {
   int64_t nunits = 0;
   buffer acc;          // u64[nacc] fixed-point sums by row, zero between iterations
   int64_t nacc = 0;
-  buffer tiles;        // int64[ntiles + 1]: first unit of every tile (<= 8 units of one window)
-  int64_t ntiles = 0;
-  int64_t nwin = 0;
-  buffer tile_ctr;     // uint32: tile queue head; zero between iterations
+  buffer items;        // int64[nitems + 1]: first unit of every item (a window or a share of one)
+  buffer queue;        // int64[nitems]: item ids of queue 0, 1, ..., 7
+  std::vector<int64_t> qoff;  // queue q = queue[qoff[q], qoff[q + 1])
+  int64_t nitems = 0;
+  int64_t nwin   = 0;
+  buffer tile_ctr;     // uint32 queue heads (128 B apart); zero between iterations
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

@@ -312,9 +312,18 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 //  * push entries are the CSC edges sorted by (window, source) and packed in 32
 //    bits: (source - unit's first source) << WB | (destination - window base);
 //  * a unit is <= kPushUnit entries of one window whose sources span less than
-//    2^(32 - WB); a tile is a run of <= kTileUnits units of one window;
-//  * persistent blocks take tiles from a queue in unit order, sum a tile into the
-//    LDS window and flush it to the global accumulators (integer atomics) once;
+//    2^(32 - WB); an item is a run of units of one window (a whole window, or an
+//    equal share of a window larger than ~E / 2048 entries);
+//  * (from 2^22 rows; below, items are tiles of <= 8 units in one queue) items
+//    are grouped 128 at a time in window order and the groups dealt to 8
+//    queues (balanced by entries); block b takes items from queue b % 8 -- blocks
+//    b and b + 8 share an XCD -- and then steals from the others.  A block sums
+//    an item into the LDS window in source order and flushes it to the global
+//    accumulators (integer atomics) once.  The 64 blocks of an XCD so work on
+//    neighbouring windows that sweep the sources at about the same pace, and the
+//    x~ lines one gathers are in that XCD's L2 for the others: an offline LRU
+//    model of the 8 L2s (RMAT-24) gives 12.9M x~ misses per iteration against
+//    22.4M for one queue of 8-unit tiles;
 //  * sums are 64-bit fixed point (scale 2^62; every destination's sum is at most
 //    the total rank mass 1 since x~[u] w(u, v) summed over v is pr[u]).  Integer
 //    addition is associative: the result is bitwise deterministic whatever the
@@ -333,7 +342,10 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 constexpr int kPushThreads = 1024;
 constexpr int kPerThread   = 8;  // entries per thread per unit
 constexpr int kPushUnit    = kPerThread * kPushThreads;
-constexpr int kTileUnits   = 8;  // RMAT-22: 8: 0.221, 16: 0.222, 32: 0.229, 64: 0.241 ms/iteration
+constexpr int kQueues      = 8;    // XCDs
+constexpr int kTileUnits   = 8;    // units per tile below 2^22 rows (RMAT-22: 8: 0.221, 16: 0.222, 32: 0.229 ms/iteration)
+constexpr int kGroupItems  = 128;  // items per group dealt to a queue
+constexpr int kCtrStride   = 32;   // queue heads 128 B apart
 constexpr int kPushBlocks  = 512;  // persistent grid: two 1024-thread blocks per CU, 256 CUs
 #ifndef CGX_APPLY_BATCH
 #define CGX_APPLY_BATCH 4
@@ -368,9 +380,11 @@ struct push_args {
   push_unit const* units;
   int64_t nunits;
   unsigned long long* acc;  // [n_rows] fixed-point sums, zero between iterations
-  int64_t const* tiles;     // first unit of every tile, ntiles + 1 entries
-  int64_t ntiles;
-  unsigned int* tile_ctr;   // queue head (k_pr_apply resets it)
+  int64_t const* items;     // first unit of every item, nitems + 1 entries
+  int64_t const* queue;     // item ids, queue by queue
+  int64_t qoff[kQueues + 1];
+  int64_t nitems;
+  unsigned int* tile_ctr;   // queue heads, kCtrStride apart (k_pr_apply resets them)
 };
 
 template <typename T>
@@ -400,31 +414,37 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
   __syncthreads();
 }
 
-// The push: persistent blocks take tiles from the queue.  The unit body is
-// branch-free (masked lanes load x~[base] and add 0; the next unit of the tile is
-// always prefetched, the last re-reading itself -- ent and ew are padded by a
-// unit), so the only waits are "gathers done" and "prefetch done".  A queue
-// balances the unequal cost of units (hub-source units gather from few lines,
-// tail units from many): 0.221 vs 0.227 ms/iteration for a static split (RMAT-22).
+// The push: persistent blocks take items from their queue, then from the others.
+// The unit body is branch-free (masked lanes load x~[base] and add 0; the next
+// unit of the item is always prefetched, the last re-reading itself -- ent and ew
+// are padded by a unit), so the only waits are "gathers done" and "prefetch done".
 template <int WB, typename V, typename E, typename R, bool WEIGHTED>
 __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
 {
   constexpr int kWin = 1 << WB;
   __shared__ unsigned long long acc[kWin];
-  __shared__ int64_t s_tile;
+  __shared__ int64_t s_item;
   if (sa.a.st->done) return;
   int const tid = threadIdx.x;
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
   using cunit_t        = __attribute__((address_space(4))) push_unit const;
   cunit_t* const units = (cunit_t*)sa.units;  // read-only here: scalar loads
   R const* const x     = sa.a.x_in;
-  while (true) {
-    if (tid == 0) s_tile = (int64_t)atomicAdd(sa.tile_ctr, 1u);
+  int q                = (int)(blockIdx.x % kQueues);
+  for (int tries = 0; tries < kQueues;) {
+    if (tid == 0) {
+      int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + q * kCtrStride, 1u);
+      s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
+    }
     __syncthreads();
-    int64_t const t = s_tile;
-    __syncthreads();  // every thread has read s_tile before thread 0 takes the next tile
-    if (t >= sa.ntiles) break;  // uniform
-    int64_t const ua = sa.tiles[t], ub = sa.tiles[t + 1];
+    int64_t const it = s_item;
+    __syncthreads();  // every thread has read s_item before thread 0 takes the next
+    if (it < 0) {  // uniform: this queue is drained, steal from the next
+      q = (q + 1) % kQueues;
+      ++tries;
+      continue;
+    }
+    int64_t const ua = sa.items[it], ub = sa.items[it + 1];
     int64_t const win = units[ua].win;
     int64_t k0   = units[ua].k0;
     int n        = (int)(units[ua].k1 - k0);
@@ -495,7 +515,7 @@ template <typename V, typename E, typename R>
 __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 {
   auto const& a = sa.a;
-  if (sa.tile_ctr && blockIdx.x == 0 && threadIdx.x == 0) *sa.tile_ctr = 0u;  // the push has finished
+  if (sa.tile_ctr && blockIdx.x == 0 && threadIdx.x < kQueues) sa.tile_ctr[threadIdx.x * kCtrStride] = 0u;  // push done
   if (a.st->done) return;
   double const base = a.st->base;
   double const pf   = a.st->pers_factor;
@@ -617,34 +637,6 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
   }
 }
 
-// tile heads: a window's first unit and every kTileUnits-th unit of a window
-__global__ void k_tile_flags(push_unit const* units, int64_t nunits, int64_t const* wu, uint32_t* flag)
-{
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < nunits; u += (int64_t)gridDim.x * blockDim.x)
-    flag[u] = (u - wu[units[u].win]) % kTileUnits == 0 ? 1u : 0u;
-}
-
-__global__ void k_tile_heads(uint32_t const* flag, uint32_t const* tid, int64_t nunits, int64_t* tiles)
-{
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u <= nunits; u += (int64_t)gridDim.x * blockDim.x)
-    if (u == nunits) tiles[tid[nunits]] = nunits;
-    else if (flag[u]) tiles[tid[u]] = u;
-}
-
-// first unit of every window w in [0, nwin] (units are in window order)
-__global__ void k_win_units(push_unit const* units, int64_t nunits, int64_t nwin, int64_t* wu)
-{
-  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x) {
-    int64_t lo = 0, hi = nunits;
-    while (lo < hi) {
-      int64_t mid = (lo + hi) >> 1;
-      if (units[mid].win < w) lo = mid + 1;
-      else hi = mid;
-    }
-    wu[w] = lo;
-  }
-}
-
 // Push schedule of an edge list given as (row = destination, col = source) with
 // destinations in [0, n_rows) and sources in [0, n_cols) -- the SG pull adjacency
 // or one MG 2D block.
@@ -665,10 +657,11 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.acc.resize(pp.nacc * sizeof(unsigned long long));
   HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
   pp.tile_ctr.set_stream(s);
-  pp.tile_ctr.resize(sizeof(unsigned int));
-  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, sizeof(unsigned int), s));
+  pp.tile_ctr.resize(kQueues * kCtrStride * sizeof(unsigned int));
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, kQueues * kCtrStride * sizeof(unsigned int), s));
   pp.nunits = 0;
-  pp.ntiles = 0;
+  pp.nitems = 0;
+  pp.qoff.assign(kQueues + 1, 0);
   if (ne == 0) return;
   dbuf<uint64_t> keys_out(ne, s);
   dbuf<uint32_t> vals_out(ne, s);
@@ -714,25 +707,72 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
                      w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
-  // tiles: runs of <= kTileUnits units of one window, in unit (= queue) order
-  dbuf<int64_t> wu(nwin + 1, s);
-  hipLaunchKernelGGL(k_win_units, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, nwin,
-                     wu.data());
-  CGX_LAUNCH_CHECK();
-  dbuf<uint32_t> tflag(nunits + 1, s), tid(nunits + 1, s);
-  hipLaunchKernelGGL(k_tile_flags, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, wu.data(),
-                     tflag.data());
-  CGX_LAUNCH_CHECK();
-  fill<uint32_t>(tflag.data() + nunits, 1, 0u, s);
-  exclusive_scan<uint32_t, uint32_t>(tflag.data(), tid.data(), nunits + 1, s);
-  int64_t const ntiles = (int64_t)to_host(tid.data() + nunits, 1, s)[0];
-  pp.tiles.set_stream(s);
-  pp.tiles.resize((ntiles + 1) * sizeof(int64_t));
-  hipLaunchKernelGGL(k_tile_heads, dim3(grid_for(nunits + 1, kBlock, 4096)), dim3(kBlock), 0, s, tflag.data(),
-                     tid.data(), nunits, pp.tiles.data<int64_t>());
-  CGX_LAUNCH_CHECK();
+  // Items and queues.  From 2^22 rows (8K windows): an item is a window's units,
+  // or an equal share of a window of more than 1.5 tg entries; groups of
+  // kGroupItems consecutive items are dealt to the 8 queues by longest-processing-
+  // time on their entries (RMAT-24: 0.986 -> 0.950 ms/iteration, same-box A/B).
+  // Below: one queue of tiles of <= 8 units of a window (RMAT-22: the XCD queues
+  // measured 0.199 -> 0.216, the last groups' imbalance outweighing the L2 hits).
+  auto hu = to_host(units, nunits, s);
+  bool const xcd_queues = wb == 13;
+  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * 4));
+  std::vector<int64_t> item_u, item_e;
+  for (int64_t u0 = 0; u0 < nunits;) {
+    int64_t u1 = u0;
+    while (u1 < nunits && hu[u1].win == hu[u0].win) ++u1;
+    int64_t const size = hu[u1 - 1].k1 - hu[u0].k0;
+    int64_t const n    = std::max<int64_t>(1, (size + tg / 2) / tg);
+    int64_t k          = 0;
+    for (int64_t u = u0; u < u1; ++u) {
+      int64_t const done = hu[u].k0 - hu[u0].k0;
+      bool const head    = u == u0 || (xcd_queues ? (k < n && done * n >= k * size) : (u - u0) % kTileUnits == 0);
+      if (head) {
+        item_u.push_back(u);
+        item_e.push_back(0);
+        ++k;
+      }
+      item_e.back() += hu[u].k1 - hu[u].k0;
+    }
+    u0 = u1;
+  }
+  int64_t const nitems = (int64_t)item_u.size();
+  item_u.push_back(nunits);
+  std::vector<int64_t> queue;
+  queue.reserve(nitems);
+  if (xcd_queues) {
+    int64_t const ngroups = (nitems + kGroupItems - 1) / kGroupItems;
+    std::vector<int64_t> gsize(ngroups, 0), gorder(ngroups);
+    for (int64_t i = 0; i < nitems; ++i) gsize[i / kGroupItems] += item_e[i];
+    for (int64_t g = 0; g < ngroups; ++g) gorder[g] = g;
+    std::stable_sort(gorder.begin(), gorder.end(), [&](int64_t a, int64_t b) { return gsize[a] > gsize[b]; });
+    std::vector<int> gq(ngroups, 0);
+    int64_t load[kQueues] = {};
+    for (int64_t g : gorder) {
+      int best = 0;
+      for (int q = 1; q < kQueues; ++q)
+        if (load[q] < load[best]) best = q;
+      gq[g] = best;
+      load[best] += gsize[g];
+    }
+    for (int q = 0; q < kQueues; ++q) {
+      pp.qoff[q] = (int64_t)queue.size();
+      for (int64_t i = 0; i < nitems; ++i)
+        if (gq[i / kGroupItems] == q) queue.push_back(i);
+    }
+  } else {  // everything in queue 0; the other labels' blocks steal from it at once
+    for (int64_t i = 0; i < nitems; ++i) queue.push_back(i);
+    pp.qoff[0] = 0;
+    for (int q = 1; q < kQueues; ++q) pp.qoff[q] = nitems;
+  }
+  pp.qoff[kQueues] = (int64_t)queue.size();
+  pp.items.set_stream(s);
+  pp.items.resize(item_u.size() * sizeof(int64_t));
+  to_device(pp.items.data<int64_t>(), item_u.data(), item_u.size(), s);
+  pp.queue.set_stream(s);
+  pp.queue.resize(std::max<size_t>(queue.size(), 1) * sizeof(int64_t));
+  to_device(pp.queue.data<int64_t>(), queue.data(), queue.size(), s);
   pp.nunits = nunits;
-  pp.ntiles = ntiles;
+  pp.nitems = nitems;
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -799,10 +839,12 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.units    = pp.units.data<push_unit>();
   sa.nunits   = pp.nunits;
   sa.acc      = pp.acc.data<unsigned long long>();
-  sa.tiles    = pp.tiles.data<int64_t>();
-  sa.ntiles   = pp.ntiles;
+  sa.items    = pp.items.data<int64_t>();
+  sa.queue    = pp.queue.data<int64_t>();
+  sa.nitems   = pp.nitems;
+  for (int q = 0; q <= kQueues; ++q) sa.qoff[q] = q < (int)pp.qoff.size() ? pp.qoff[q] : 0;
   sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
-  HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, sizeof(unsigned int), s));
+  HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, kQueues * kCtrStride * sizeof(unsigned int), s));
 }
 
 // the push kernel for the schedule's window bits
@@ -943,7 +985,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   auto pkernel = push_kernel<V, E, R>(adj.pr, g.weighted);
   if (push) {
     set_queue_args(sa, adj.pr, s);
-    nblk_push  = (int)std::min<int64_t>(sa.ntiles, kPushBlocks);
+    nblk_push  = sa.nitems ? kPushBlocks : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
   // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
@@ -1309,7 +1351,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   // and re-zeroes them in place, no column collective
   bool const col_reduce = R_ > 1;
   sap.acc   = col_reduce ? acc_own.data() : sp.acc;
-  int const nblk_push  = (int)std::min<int64_t>(sp.ntiles, kPushBlocks);
+  int const nblk_push  = sp.nitems ? kPushBlocks : 0;
   auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);

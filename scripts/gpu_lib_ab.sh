@@ -9,7 +9,7 @@ for rep in 1 2; do
   for spec in $LIBS; do
     name=${spec%%=*}; path=${spec#*=}
     if [ "$path" = default ]; then unset CUGRAPH_AMD_LIB; else export CUGRAPH_AMD_LIB=$PWD/$path; fi
-    timeout -k 10 300 env $EXTRA python -u bench.py --no-cpu-baseline --no-louvain --no-bfs --no-traffic --steps 5 > $OUT/b_${name}_$rep.json 2> $OUT/b_${name}_$rep.err
-    rc=$?; echo "== $name rep $rep"; grep "edges/s" $OUT/b_${name}_$rep.err; [ $rc -eq 0 ] || { tail $OUT/b_${name}_$rep.err; exit $rc; }
+    timeout -k 10 300 env $EXTRA python -u bench.py ${BENCH_AB_ARGS:---no-cpu-baseline --no-louvain --no-bfs --no-traffic --steps 5} > $OUT/b_${name}_$rep.json 2> $OUT/b_${name}_$rep.err
+    rc=$?; echo "== $name rep $rep"; grep "\[bench\].*/s\|MTEPS" $OUT/b_${name}_$rep.err; [ $rc -eq 0 ] || { tail $OUT/b_${name}_$rep.err; exit $rc; }
   done
 done
