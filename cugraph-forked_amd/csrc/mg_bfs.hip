@@ -1,22 +1,31 @@
 // Multi-GPU BFS (one process per GPU).
 //
-// Reference: cpp/src/traversal/bfs_impl.cuh:94-287 (MG path: frontier broadcast
-// over the column communicator, all-to-all of (destination, parent) over the row
-// communicator, termination allreduce).  Here every rank owns the
-// out-adjacency of its own vertices (a 1D partition by source owner, built once
-// from the 2D blocks and cached), and a level is either
+// Reference: cpp/src/traversal/bfs_impl.cuh:94-287 (MG path: the frontier is
+// broadcast inside the communicator that shares the edge block's sources
+// (extract_transform_v_frontier_e.cuh:858-876), the (destination, parent) pairs go
+// to the destinations' owners with one all-to-all inside the other communicator
+// (transform_reduce_v_frontier_outgoing_e_by_dst.cuh:396-451), then a termination
+// allreduce).  A level is either
 //
-//  * top-down: own frontier vertices emit (v, u) candidates; they are sorted by
-//    (v, u), reduced to the smallest parent per v, and sent to v's owner in one
-//    all-to-all (global ids are contiguous per owner, so the sort also groups by
-//    destination rank); owners claim unvisited v with parent = smallest u;
-//  * bottom-up (symmetric graphs, direction_optimizing): the frontier bitmap of
-//    every rank is allgathered (V/8 bytes), each rank scans its unvisited
-//    vertices' sorted adjacency and stops at the first frontier neighbour.
+//  * top-down, on the 2D partition (mg_graph.hpp): rank (r, c) holds the edges
+//    from row r's vertices (one contiguous global range) to column c's.  The own
+//    frontiers of the C ranks of row r are allgathered inside the row
+//    communicator; every rank expands them over its block into (v, u) candidates,
+//    sorts them by (v, u), keeps the smallest parent per v, and sends them to v's
+//    owner -- one of the R ranks of column c -- with one all-to-all inside the
+//    column communicator; owners claim unvisited v with parent = smallest u.  On a
+//    1 x P grid the column has one rank: no candidate exchange at all;
+//  * bottom-up (symmetric graphs, direction_optimizing): every rank owns the
+//    out-adjacency of its own vertices (a 1D partition by source owner, built once
+//    from the 2D blocks and cached); the frontier bitmap of every rank is
+//    allgathered (V/8 bytes), each rank scans its unvisited vertices' sorted
+//    adjacency and stops at the first frontier neighbour.
 //
 // Both pick the frontier neighbour with the smallest global id, so distances and
-// predecessors do not depend on the direction schedule (Beamer alpha 14 / beta 24
-// on global counts).  Predecessors are returned as external ids.
+// predecessors do not depend on the direction schedule.  The direction switch keeps
+// Beamer's alpha 14 / beta 24 on global counts: a bottom-up level here also pays a
+// V/8-byte bitmap allgather, so the single-GPU tuning (40 / 64, bfs.hip) does not
+// carry over unmeasured.  Predecessors are returned as external ids.
 #include "capi.hpp"
 #include "comm.hpp"
 #include "mg_graph.hpp"
@@ -139,6 +148,55 @@ bfs_rows_t& mg_rows(handle_t& h, graph_t& g)
   return *rows;
 }
 
+// this rank's 2D edge block as a CSR over row r's vertices (local index u - row_lo)
+struct bfs_block_t {
+  int64_t row_lo = 0, nrow = 0, ne = 0;
+  buffer off;  // int64[nrow + 1]
+  buffer idx;  // uint32 global destination ids, ascending per row
+};
+
+template <typename V>
+__global__ void k_block_keys(V const* src, V const* dst, int64_t n, int64_t row_lo, unsigned long long* keys)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    keys[i] = ((unsigned long long)((int64_t)src[i] - row_lo) << 32) | (unsigned long long)(uint32_t)dst[i];
+}
+
+template <typename V>
+bfs_block_t& mg_block_csr(handle_t& h, graph_t& g)
+{
+  mg_graph_t& mg = *g.mg;
+  if (mg.bfs_block) return *static_cast<bfs_block_t*>(mg.bfs_block.get());
+  hipStream_t s = h.stream;
+  auto blk      = std::make_shared<bfs_block_t>();
+  int const r   = mg.p / mg.C;
+  blk->row_lo   = mg.voff[r * mg.C];
+  blk->nrow     = mg.voff[r * mg.C + mg.C] - blk->row_lo;
+  int64_t const m = mg.ne;
+  blk->ne       = m;
+  dbuf<unsigned long long> k1(std::max<int64_t>(m, 1), s), k2(std::max<int64_t>(m, 1), s);
+  dbuf<uint32_t> rr(std::max<int64_t>(m, 1), s);
+  blk->idx.set_stream(s);
+  blk->idx.resize(std::max<int64_t>(m, 1) * sizeof(uint32_t));
+  blk->off.set_stream(s);
+  blk->off.resize((blk->nrow + 1) * sizeof(int64_t));
+  if (m) {
+    hipLaunchKernelGGL(k_block_keys<V>, dim3(blocks(m)), dim3(kBlock), 0, s, mg.src.data<V>(), mg.dst.data<V>(), m,
+                       blk->row_lo, k1.data());
+    CGX_LAUNCH_CHECK();
+    radix_sort_keys<unsigned long long>(k1.data(), k2.data(), m, 0, 64, s);
+    hipLaunchKernelGGL(k_split_row_keys, dim3(blocks(m)), dim3(kBlock), 0, s, k2.data(), m, rr.data(),
+                       blk->idx.data<uint32_t>());
+    CGX_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_offsets_u32, dim3(blocks(blk->nrow + 1)), dim3(kBlock), 0, s, rr.data(), m, blk->nrow,
+                     blk->off.data<int64_t>());
+  CGX_LAUNCH_CHECK();
+  HIP_CHECK(hipStreamSynchronize(s));
+  mg.bfs_block = blk;
+  return *blk;
+}
+
 // ---------------------------------------------------------------- level kernels
 struct level_ctr {
   unsigned long long next_n;  // own vertices discovered
@@ -195,11 +253,13 @@ __global__ void k_init_sources(V const* src_global, size_t n, int64_t lo, int64_
   }
 }
 
-// exclusive prefix of frontier degrees is in `pre`; one thread per candidate edge
+// 2D top-down: frontier = row-local source ids gathered from the row (pads
+// UINT32_MAX); candidate v << gb | parent for every block edge; v is filtered only
+// when it is this rank's own vertex and already visited
 template <typename V>
-__global__ void k_td_candidates(uint32_t const* frontier, int64_t nf, unsigned long long const* pre, int64_t m,
-                                int64_t const* off, uint32_t const* idx, int64_t lo, int64_t hi, V const* dist,
-                                int gb, unsigned long long* out)
+__global__ void k_block_candidates(uint32_t const* frontier, int64_t nf, unsigned long long const* pre, int64_t m,
+                                   int64_t const* off, uint32_t const* idx, int64_t row_lo, int64_t lo, int64_t hi,
+                                   V const* dist, int gb, unsigned long long* out)
 {
   V const INF = std::numeric_limits<V>::max();
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
@@ -209,14 +269,27 @@ __global__ void k_td_candidates(uint32_t const* frontier, int64_t nf, unsigned l
       if ((int64_t)pre[mid] <= t) a = mid;
       else b = mid - 1;
     }
-    uint32_t u    = frontier[a];
-    int64_t e     = off[u] + (t - (int64_t)pre[a]);
-    uint32_t v    = idx[e];
-    bool visited  = (int64_t)v >= lo && (int64_t)v < hi && dist[(int64_t)v - lo] != INF;  // own: known locally
-    // compact key v << gb | parent (gb = global id bits): the sort runs over 2 gb bits;
-    // the sentinel ~0 still sorts last (v = parent = 2^gb - 1 would be a visited self loop)
-    out[t]        = visited ? ~0ull : (((unsigned long long)v << gb) | (unsigned long long)(uint32_t)(lo + u));
+    uint32_t u   = frontier[a];  // never a pad: pads have degree 0
+    int64_t e    = off[u] + (t - (int64_t)pre[a]);
+    uint32_t v   = idx[e];
+    bool visited = (int64_t)v >= lo && (int64_t)v < hi && dist[(int64_t)v - lo] != INF;
+    out[t]       = visited ? ~0ull : (((unsigned long long)v << gb) | (unsigned long long)(row_lo + u));
   }
+}
+
+__global__ void k_gathered_degrees(uint32_t const* frontier, int64_t nf, int64_t const* off, unsigned long long* deg)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const u = frontier[i];
+    deg[i]           = u == 0xffffffffu ? 0ull : (unsigned long long)(off[u + 1] - off[u]);
+  }
+}
+
+// own frontier (local ids) -> row-local ids, padded to `pad` entries with UINT32_MAX
+__global__ void k_to_row_local(uint32_t const* q, int64_t n, int64_t shift, int64_t pad, uint32_t* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < pad; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = i < n ? (uint32_t)((int64_t)q[i] + shift) : 0xffffffffu;
 }
 
 template <typename V>
@@ -431,6 +504,17 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   bool bottom_up = false;
   size_t levels = 0, bu_steps = 0;
   int const gb = bits_for((unsigned long long)std::max<int64_t>(g.num_vertices - 1, 0));  // candidate key bits
+  // 2D top-down: the block CSR, the row / column communicators, the column owners' id ranges
+  bfs_block_t& blk = mg_block_csr<V>(h, g);
+  comm_t& rowc     = *ctx.row;
+  comm_t& colc     = *ctx.col;
+  CGX_EXPECTS(rowc.size == mg.C && colc.size == mg.R, CUGRAPH_INVALID_HANDLE,
+              "MG BFS: the handle's grid does not match the graph's");
+  std::vector<int64_t> colvoff(mg.R + 1);
+  for (int q = 0; q < mg.R; ++q) colvoff[q] = mg.voff[q * mg.C + mg.p % mg.C];
+  colvoff[mg.R] = g.num_vertices;
+  dbuf<int64_t> colvoff_d(mg.R + 1, s);
+  to_device(colvoff_d.data(), colvoff.data(), colvoff.size(), s);
   while (nf > 0 && depth < limit) {
     if (dir_opt) {
       if (!bottom_up && m_f > m_u / 14.0) bottom_up = true;
@@ -451,24 +535,33 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       CGX_LAUNCH_CHECK();
       ++bu_steps;
     } else {
-      // candidates of the own frontier, smallest parent per destination, to the owners
-      dbuf<unsigned long long> dg(std::max<int64_t>(nf_own, 1), s), pre(std::max<int64_t>(nf_own + 1, 1), s);
-      int64_t mcand = 0;
-      if (nf_own) {
-        hipLaunchKernelGGL(k_frontier_degrees<V>, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own,
-                           rows.off.data<int64_t>(), dg.data());
+      // 2D: the row's own frontiers to every rank of the row (row-local source ids)
+      auto row_counts = rowc.host_allgather<int64_t>(nf_own, s);
+      int64_t mx      = 0;
+      for (auto x : row_counts) mx = std::max(mx, x);
+      int64_t const nfg = mx * (int64_t)rowc.size;
+      int64_t mcand     = 0;
+      dbuf<uint32_t> fsend(std::max<int64_t>(mx, 1), s), fgath(std::max<int64_t>(nfg, 1), s);
+      dbuf<unsigned long long> dg(std::max<int64_t>(nfg, 1), s), pre(std::max<int64_t>(nfg, 1), s);
+      if (mx) {
+        hipLaunchKernelGGL(k_to_row_local, dim3(blocks(mx)), dim3(kBlock), 0, s, qa.data(), nf_own,
+                           lo - blk.row_lo, mx, fsend.data());
         CGX_LAUNCH_CHECK();
-        exclusive_scan<unsigned long long, unsigned long long>(dg.data(), pre.data(), nf_own, s);
-        auto last = to_host(pre.data() + nf_own - 1, 1, s)[0] + to_host(dg.data() + nf_own - 1, 1, s)[0];
-        mcand     = (int64_t)last;
+        rowc.allgather<uint32_t>(fsend.data(), fgath.data(), (size_t)mx, s);
+        hipLaunchKernelGGL(k_gathered_degrees, dim3(blocks(nfg)), dim3(kBlock), 0, s, fgath.data(), nfg,
+                           blk.off.data<int64_t>(), dg.data());
+        CGX_LAUNCH_CHECK();
+        exclusive_scan<unsigned long long, unsigned long long>(dg.data(), pre.data(), nfg, s);
+        mcand = (int64_t)(to_host(pre.data() + nfg - 1, 1, s)[0] + to_host(dg.data() + nfg - 1, 1, s)[0]);
       }
+      // candidates over the block, smallest parent per destination
       dbuf<unsigned long long> cand(std::max<int64_t>(mcand, 1), s), cs(std::max<int64_t>(mcand, 1), s),
         cu(std::max<int64_t>(mcand, 1), s);
       int64_t nu = 0;
       if (mcand) {
-        hipLaunchKernelGGL(k_td_candidates<V>, dim3(blocks(mcand)), dim3(kBlock), 0, s, qa.data(), nf_own,
-                           pre.data(), mcand, rows.off.data<int64_t>(), rows.idx.data<uint32_t>(), lo, hi, dist,
-                           gb, cand.data());
+        hipLaunchKernelGGL(k_block_candidates<V>, dim3(blocks(mcand)), dim3(kBlock), 0, s, fgath.data(), nfg,
+                           pre.data(), mcand, blk.off.data<int64_t>(), blk.idx.data<uint32_t>(), blk.row_lo, lo, hi,
+                           dist, gb, cand.data());
         CGX_LAUNCH_CHECK();
         radix_sort_keys<unsigned long long>(cand.data(), cs.data(), mcand, 0, 2 * gb, s);
         dbuf<size_t> cnt(1, s);
@@ -482,17 +575,19 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
           CGX_LAUNCH_CHECK();
         }
       }
-      // per-owner split points (the sentinel ~0 run, if any, sorts last and is dropped)
-      std::vector<size_t> counts(P, 0);
+      // to the destinations' owners: the R ranks of column c (the sentinel run, if
+      // any, sorts last and is dropped)
+      std::vector<size_t> counts(colc.size, 0);
       if (nu) {
-        dbuf<int64_t> pos(P + 1, s);
-        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), nu, voff_d.data(), P, pos.data());
+        dbuf<int64_t> pos(colc.size + 1, s);
+        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), nu, colvoff_d.data(), colc.size,
+                           pos.data());
         CGX_LAUNCH_CHECK();
-        auto hp = to_host(pos.data(), P + 1, s);
-        for (int q = 0; q < P; ++q) counts[q] = (size_t)(hp[q + 1] - hp[q]);
+        auto hp = to_host(pos.data(), colc.size + 1, s);
+        for (int q = 0; q < colc.size; ++q) counts[q] = (size_t)(hp[q + 1] - hp[q]);
       }
       std::vector<size_t> rcnt;
-      auto got = exchange<int64_t>(comm, reinterpret_cast<int64_t const*>(cu.data()), counts, rcnt, s);
+      auto got = exchange<int64_t>(colc, reinterpret_cast<int64_t const*>(cu.data()), counts, rcnt, s);
       if (got.n)
         hipLaunchKernelGGL(k_td_claim<V>, dim3(capped(got.n)), dim3(kBlock), 0, s,
                            reinterpret_cast<unsigned long long const*>(got.data()), (int64_t)got.n, lo, dist,

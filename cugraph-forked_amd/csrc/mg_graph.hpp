@@ -37,6 +37,7 @@ struct mg_graph_t {
   // per-algorithm caches (pagerank.hip, mg_bfs.hip, mg_sssp.hip)
   std::shared_ptr<void> pr_block;
   std::shared_ptr<void> bfs_rows;
+  std::shared_ptr<void> bfs_block;  // the 2D block as a CSR over the row's sources (mg_bfs.hip)
   std::shared_ptr<void> sssp_rows;  // weighted out-rows by source owner (mg_sssp.hip)
 };
 

@@ -120,7 +120,8 @@ def test_mg_pagerank_vs_oracle(world, C, weighted):
     tmp.spawn(_worker, args=(world, _free_port(), C, 11, weighted, "pagerank"), nprocs=world, join=True)
 
 
-@pytest.mark.parametrize("world,C,algo", [(2, 2, "bfs"), (4, 2, "bfs_do"), (3, 3, "bfs_do")])
+@pytest.mark.parametrize("world,C,algo", [(2, 2, "bfs"), (4, 2, "bfs_do"), (3, 3, "bfs_do"), (2, 1, "bfs"),
+                                          (4, 1, "bfs_do")])
 def test_mg_bfs_vs_oracle(world, C, algo):
     import torch.multiprocessing as tmp
     tmp.spawn(_worker, args=(world, _free_port(), C, 12, False, algo), nprocs=world, join=True)
@@ -386,3 +387,17 @@ def test_mg_rank_without_edges(algo, monkeypatch):
         tmp.spawn(_sssp_worker, args=(3, port, 3, 10, True, float("inf")), nprocs=3, join=True)
     else:
         tmp.spawn(_worker, args=(3, port, 3, 10, False, algo), nprocs=3, join=True)
+
+
+# The reference's 8-GPU grid (mg_utilities.cpp:60-66: R = 2 x C = 4) rehearsed with 8
+# ranks on the one test GPU over torch.distributed/gloo: the same partition, id
+# routing and per-level / per-iteration collectives an 8 x MI355X node runs over
+# RCCL (performance unmeasured here).
+@pytest.mark.parametrize("algo", ["pagerank", "bfs_do", "bfs", "louvain"])
+def test_mg_world8_reference_grid(algo):
+    import torch.multiprocessing as tmp
+    port = _free_port()
+    if algo == "louvain":
+        tmp.spawn(_louvain_worker, args=(8, port, 4, 10, True), nprocs=8, join=True)
+    else:
+        tmp.spawn(_worker, args=(8, port, 4, 11, False, algo), nprocs=8, join=True)
