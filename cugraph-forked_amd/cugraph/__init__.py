@@ -13,7 +13,8 @@ from .structure import DiGraph, Graph, from_edgelist, from_pandas_edgelist
 from .algorithms import (bfs, eigenvector_centrality, hits, katz_centrality, louvain, pagerank, shortest_path,
                          shortest_path_length, sssp)
 from . import generators
+from . import dask  # noqa: F401  (multi-GPU, one process per GPU)
 
 __all__ = ["Graph", "DiGraph", "from_edgelist", "from_pandas_edgelist", "pagerank", "bfs", "sssp",
            "shortest_path", "shortest_path_length", "louvain", "katz_centrality", "eigenvector_centrality", "hits",
-           "generators"]
+           "generators", "dask"]

@@ -92,6 +92,58 @@ class Graph:
         self.renumbered = False  # ids stay external at the Python level; libcugraph_c renumbers
         self._plc_graph = self._make_plc_graph(w)
 
+    def from_dask_cudf_edgelist(self, input_ddf, source="source", destination="destination", edge_attr=None,
+                                renumber=True, store_transposed=False, legacy_renum_only=False):
+        """graph_classes.py:173-244 -> simpleDistributedGraph.py.  One process per GPU:
+        every rank calls this collectively with ITS partition of the edge list (a pandas
+        DataFrame / dict of arrays or tensors); cugraph.dask.comms.comms.initialize()
+        must have been called.  The partitions are symmetrised (undirected) and
+        de-duplicated across the ranks (cugraph.dask._shuffle), then
+        cugraph_mg_graph_create builds the 2D-partitioned graph."""
+        import torch
+        import torch.distributed as dist
+        from .dask import _shuffle
+        from .dask.comms import comms as dcomms
+        if self.edgelist is not None:
+            raise RuntimeError("Graph already has values")
+        if not renumber:
+            raise ValueError("the distributed graph is always renumbered (cugraph_mg_graph_create)")
+        cols = list(input_ddf.columns) if hasattr(input_ddf, "columns") else list(input_ddf.keys())
+        if source not in cols or destination not in cols:
+            raise ValueError("source column names and/or destination column names not found in input. "
+                             "Recheck the source and destination parameters")
+        if isinstance(edge_attr, (list, tuple)):
+            if len(edge_attr) != 1:
+                raise ValueError(f"Invalid number of edge attributes passed. {edge_attr}")
+            edge_attr = edge_attr[0]
+        if edge_attr is not None and edge_attr not in cols:
+            raise ValueError("edge_attr column name not found in input.Recheck the edge_attr parameter")
+        h = dcomms.get_default_handle()
+        src, dst = _column(input_ddf, source), _column(input_ddf, destination)
+        w = None
+        if edge_attr is not None:
+            w = _column(input_ddf, edge_attr)
+            if w.dtype not in (torch.float32, torch.float64):
+                w = w.to(torch.float32)
+            self.graph_properties.weights = True
+        src, dst, w = _shuffle.shuffle_dedup(src, dst, w, self.graph_properties.directed)
+        hi = torch.tensor([int(max(src.max(), dst.max())) if src.numel() else 0], dtype=torch.int64)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        vt = torch.int32 if int(hi) < 2**31 - 1 else torch.int64
+        src, dst = src.to(vt), dst.to(vt)
+        ne = torch.tensor([src.numel()], dtype=torch.int64)
+        dist.all_reduce(ne)
+        self.edgelist = {"src": src, "dst": dst, "weights": w}
+        self.store_transposed = bool(store_transposed)
+        self.renumbered = True
+        self._handle = h
+        self._distributed = True
+        self._num_edges_global = int(ne)
+        p = _plc()
+        props = p.GraphProperties(is_symmetric=not self.graph_properties.directed, is_multigraph=False)
+        self._plc_graph = p.MGGraph(h, props, src, dst, w, store_transposed=self.store_transposed,
+                                    num_edges=self._num_edges_global)
+
     def from_pandas_edgelist(self, pdf, source="source", destination="destination", edge_attr=None,
                              renumber=True, store_transposed=False, legacy_renum_only=False):
         """graph_classes.py:295-350."""
@@ -120,8 +172,18 @@ class Graph:
         if self._plc_weighted is None:
             import torch
             ones = torch.ones(self.edgelist["src"].numel(), dtype=torch.float32, device="cuda")
-            self._plc_weighted = self._make_plc_graph(ones)
+            if getattr(self, "_distributed", False):
+                p = _plc()
+                props = p.GraphProperties(is_symmetric=not self.graph_properties.directed, is_multigraph=False)
+                self._plc_weighted = p.MGGraph(self._handle, props, self.edgelist["src"], self.edgelist["dst"], ones,
+                                               store_transposed=self.store_transposed,
+                                               num_edges=self._num_edges_global)
+            else:
+                self._plc_weighted = self._make_plc_graph(ones)
         return self._plc_weighted
+
+    def is_distributed(self):
+        return getattr(self, "_distributed", False)
 
     # ------------------------------------------------------------ queries
     def is_directed(self):

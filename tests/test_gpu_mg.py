@@ -401,3 +401,59 @@ def test_mg_world8_reference_grid(algo):
         tmp.spawn(_louvain_worker, args=(8, port, 4, 10, True), nprocs=8, join=True)
     else:
         tmp.spawn(_worker, args=(8, port, 4, 11, False, algo), nprocs=8, join=True)
+
+
+def _dask_worker(rank, world, port, C):
+    """cugraph.dask (one process per GPU): each rank passes its partition of a raw
+    edge list (duplicates, both directions, spread over the ranks) to
+    Graph.from_dask_cudf_edgelist; PageRank / BFS / Louvain partitions, gathered, must
+    match single-GPU cugraph on the whole edge list (the reference's
+    python/cugraph/cugraph/tests/mg/test_mg_pagerank.py pattern)."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import pandas as pd
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cugraph
+    from cugraph.dask.comms import comms as Comms
+    from oracle import rmat
+
+    s, d = rmat.rmat(10, 16 << 10, seed=9)
+    w = rmat.rmat_weights(s.size, seed=10).astype(np.float32)
+    df = pd.DataFrame({"src": s.astype(np.int64), "dst": d.astype(np.int64), "wt": w})
+    Comms.initialize(pcols=C, backend="torch")
+    assert Comms.get_2D_partition() == (world // C, C)
+    part = df.iloc[rank::world]
+    dg = cugraph.Graph(directed=False)
+    dg.from_dask_cudf_edgelist(part, source="src", destination="dst", edge_attr="wt")
+    pr = cugraph.dask.gather(cugraph.dask.pagerank(dg, tol=1e-6)).sort_values("vertex")
+    root = int(s[0])
+    bf = cugraph.dask.gather(cugraph.dask.bfs(dg, root)).sort_values("vertex")
+    lv, q = cugraph.dask.louvain(dg)
+    lv = cugraph.dask.gather(lv)
+    if rank == 0:
+        g = cugraph.Graph(directed=False)
+        g.from_pandas_edgelist(df, source="src", destination="dst", edge_attr="wt")
+        ref = cugraph.pagerank(g, tol=1e-6).sort_values("vertex")
+        assert np.array_equal(pr["vertex"].to_numpy(), ref["vertex"].to_numpy())
+        rel = np.abs(pr["pagerank"].to_numpy() - ref["pagerank"].to_numpy()) / ref["pagerank"].to_numpy()
+        assert rel.max() < 1e-5, rel.max()
+        rb = cugraph.bfs(g, root).sort_values("vertex")
+        assert np.array_equal(bf["distance"].to_numpy(), rb["distance"].to_numpy())
+        # Louvain: a partition of every vertex, modularity within the SG result's range
+        assert np.array_equal(np.sort(lv["vertex"].to_numpy()), ref["vertex"].to_numpy())
+        _, q_sg = cugraph.louvain(g)
+        assert q > 0.5 * q_sg
+    Comms.destroy()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C", [(2, 1), (4, 2)])
+def test_dask_api_vs_single_gpu(world, C):
+    import torch.multiprocessing as tmp
+    tmp.spawn(_dask_worker, args=(world, _free_port(), C), nprocs=world, join=True)
