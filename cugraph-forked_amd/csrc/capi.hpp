@@ -100,6 +100,9 @@ struct pr_push_t {
   int win_bits = 12;   // destination window = 2^win_bits consecutive rows
   buffer ent;          // uint32[E + unit]: (source - unit's first source) << win_bits | (row - window base)
   buffer ew;           // weight_t[E + unit] for weighted graphs
+  bool packed = false; // 16-bit entries (unweighted): ent16 + seg_base instead of ent
+  buffer ent16;        // uint16[E' + unit]: delta << win_bits | slot, or a source jump
+  buffer seg_base;     // uint32[nunits * 16]: running source before each 512-entry wave segment
   buffer units;        // push_unit[nunits], in (window, source) order
   int64_t nunits = 0;
   buffer acc;          // u64[nacc] fixed-point sums by row, zero between iterations

@@ -366,6 +366,14 @@ inline int push_win_bits(int64_t n_rows)
   return n_rows >= (int64_t(1) << 22) ? 13 : 12;
 }
 
+// 16-bit packed entries for unweighted graphs (push_body16); CGX_PR_PACKED=0 keeps
+// the 32-bit format (measurement / A-B only)
+inline bool packed_enabled()
+{
+  char const* e = std::getenv("CGX_PR_PACKED");
+  return !(e && std::string(e) == "0");
+}
+
 struct push_unit {
   int64_t k0, k1;  // entries [k0, k1)
   int64_t base;    // source id of offset 0 (the unit's first source)
@@ -377,6 +385,8 @@ struct push_args {
   pr_args<V, E, R> a;
   uint32_t const* ent;
   R const* ew;  // entry weights (weighted graphs)
+  uint16_t const* ent16;     // packed 16-bit entries (unweighted graphs, see push_body16)
+  uint32_t const* seg_base;  // packed: running source before every 512-entry wave segment
   push_unit const* units;
   int64_t nunits;
   unsigned long long* acc;  // [n_rows] fixed-point sums, zero between iterations
@@ -511,6 +521,118 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_q_wide(push_args<V, E,
   push_body<WB, V, E, R, WEIGHTED>(sa);
 }
 
+// ---- packed 16-bit entries (unweighted graphs)
+// In (window, source) order most entries repeat or nearly repeat the previous
+// entry's source: RMAT-22 / 4K windows, source delta 0 for 74 % and <= 14 for 96 %
+// of the entries (RMAT-24 / 8K windows: <= 6 for 92 %).  An entry is 16 bits:
+//   delta << WB | slot                  for delta < 2^(16-WB) - 1, or
+//   (2^(16-WB) - 1) << WB | payload      a "jump": source += payload, no edge,
+// so a larger gap costs one or more jump entries before an entry of delta 0.  A
+// wave's 512 consecutive entries (8 rows of 64) start from seg_base[unit * 16 +
+// wave]; a row's sources are an inclusive prefix sum of the deltas (DPP) plus the
+// carry, the same dependent-load depth as the 32-bit format (no escape loads).
+// Entry bytes per edge ~2.1 instead of 4: the 4E entry stream is the push's floor.
+constexpr int kSegEntries = 512;  // entries per wave segment (8 rows of 64 lanes)
+constexpr int kSegsPerUnit = kPushUnit / kSegEntries;
+
+// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+template <int WB, typename V, typename E, typename R>
+__device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
+{
+  constexpr int kWin        = 1 << WB;
+  constexpr uint32_t kJump  = (1u << (16 - WB)) - 1;  // delta code of a jump entry
+  constexpr uint32_t kLow   = (1u << WB) - 1;
+  constexpr int kRows       = kSegEntries / 64;
+  static_assert(kRows == kPerThread, "a wave segment is one unit row per thread");
+  __shared__ unsigned long long acc[kWin];
+  __shared__ int64_t s_item;
+  if (sa.a.st->done) return;
+  int const tid  = threadIdx.x;
+  int const lane = tid & 63;
+  int const wave = tid >> 6;
+  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
+  using cunit_t        = __attribute__((address_space(4))) push_unit const;
+  cunit_t* const units = (cunit_t*)sa.units;
+  R const* const x     = sa.a.x_in;
+  int q                = (int)(blockIdx.x % kQueues);
+  for (int tries = 0; tries < kQueues;) {
+    if (tid == 0) {
+      int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + q * kCtrStride, 1u);
+      s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
+    }
+    __syncthreads();
+    int64_t const it = s_item;
+    __syncthreads();
+    if (it < 0) {
+      q = (q + 1) % kQueues;
+      ++tries;
+      continue;
+    }
+    int64_t const ua = sa.items[it], ub = sa.items[it + 1];
+    int64_t const win = units[ua].win;
+    int64_t k0 = units[ua].k0;
+    int n      = (int)(units[ua].k1 - k0) - wave * kSegEntries;  // entries of this wave's segment (may be <= 0)
+    uint32_t base = __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]);
+    uint16_t ent[kRows];
+#pragma unroll
+    for (int j = 0; j < kRows; ++j) ent[j] = nt_load(sa.ent16 + k0 + wave * kSegEntries + j * 64 + lane);  // padded
+    for (int64_t un = ua; un < ub; ++un) {
+      uint32_t sc[kRows], slot[kRows];
+      bool live[kRows];
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) {
+        bool const ok   = j * 64 + lane < n;
+        uint32_t const e = ok ? (uint32_t)ent[j] : (kJump << WB);  // past the end: a jump of 0
+        bool const jump = (e >> WB) == kJump;
+        live[j]         = !jump;
+        slot[j]         = e & kLow;
+        sc[j]           = wave_incl_scan(jump ? (e & kLow) : (e >> WB));
+      }
+      R xv[kRows];
+      uint32_t run = base;
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) {
+        uint32_t const src = run + sc[j];
+        run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
+        xv[j] = x[src];  // every lane loads (jumps and the tail read a valid source id)
+        xv[j] = live[j] ? xv[j] : R(0);
+      }
+      int64_t const nx  = un + 1 < ub ? un + 1 : un;
+      int64_t const k0n = units[nx].k0;
+      int const nn      = (int)(units[nx].k1 - k0n) - wave * kSegEntries;
+      uint32_t const bn = sa.seg_base[nx * kSegsPerUnit + wave];
+      uint16_t ent_n[kRows];
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) ent_n[j] = nt_load(sa.ent16 + k0n + wave * kSegEntries + j * 64 + lane);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) atomicAdd(&acc[slot[j]], to_fixed((double)xv[j]));
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) ent[j] = ent_n[j];
+      n    = nn;
+      base = __builtin_amdgcn_readfirstlane(bn);
+    }
+    flush_window<WB, V, E, R>(sa, acc, win);
+  }
+}
+
+template <int WB, typename V, typename E, typename R>
+__global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
+{
+  push_body16<WB, V, E, R>(sa);
+}
+
 template <typename V, typename E, typename R>
 __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 {
@@ -637,76 +759,114 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
   }
 }
 
-// Push schedule of an edge list given as (row = destination, col = source) with
-// destinations in [0, n_rows) and sources in [0, n_cols) -- the SG pull adjacency
-// or one MG 2D block.
-template <typename C, typename R>
-void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
-                         int64_t n_cols, pr_push_t& pp)
+// ---- packed 16-bit schedule construction (push_body16)
+// jumps in front of real entry k: its source gap D to the previous entry of the
+// window (0 before the window's first) is coded in the entry when D <= dmax,
+// else by ceil(D / pmax) jumps and an entry of delta 0
+__global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t dmax, uint32_t pmax,
+                              uint32_t* mj)
 {
-  pp.built = true;
-  pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
-  if (!pp.ok) return;
-  int const wb       = push_win_bits(n_rows);
-  int const sb       = 32 - wb;
-  int64_t const nwin = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
-  pp.win_bits        = wb;
-  pp.nwin            = nwin;
-  pp.nacc            = nwin << wb;
-  pp.acc.set_stream(s);
-  pp.acc.resize(pp.nacc * sizeof(unsigned long long));
-  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
-  pp.tile_ctr.set_stream(s);
-  pp.tile_ctr.resize(kQueues * kCtrStride * sizeof(unsigned int));
-  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, kQueues * kCtrStride * sizeof(unsigned int), s));
-  pp.nunits = 0;
-  pp.nitems = 0;
-  pp.qoff.assign(kQueues + 1, 0);
-  if (ne == 0) return;
-  dbuf<uint64_t> keys_out(ne, s);
-  dbuf<uint32_t> vals_out(ne, s);
-  {
-    dbuf<uint64_t> keys(ne, s);
-    dbuf<uint32_t> vals(ne, s);
-    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
-                       keys.data(), vals.data());
-    CGX_LAUNCH_CHECK();
-    radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
-                                         32 + bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)), s);
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const w     = (int64_t)(keys[k] >> 32);
+    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
+    uint32_t const D    = (uint32_t)keys[k] - prev;
+    mj[k]               = D > dmax ? (D + pmax - 1) / pmax : 0u;
   }
-  dbuf<int64_t> ws(nwin + 1, s);
-  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                     nwin, ws.data());
-  CGX_LAUNCH_CHECK();
-  dbuf<uint32_t> flag(ne + 1, s), uid(ne + 1, s);
-  hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                     ws.data(), sb, flag.data());
-  CGX_LAUNCH_CHECK();
-  fill<uint32_t>(flag.data() + ne, 1, 0u, s);
-  exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
-  int64_t const nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
-  pp.units.set_stream(s);
-  pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
-  push_unit* units = pp.units.data<push_unit>();
-  hipLaunchKernelGGL(k_unit_heads, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                     flag.data(), uid.data(), ne, units);
-  CGX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, ne);
-  CGX_LAUNCH_CHECK();
-  pp.ent.set_stream(s);
-  pp.ent.resize((ne + kPushUnit) * sizeof(uint32_t));  // padded: the kernel loads whole units
-  HIP_CHECK(hipMemsetAsync(pp.ent.data<uint32_t>() + ne, 0, kPushUnit * sizeof(uint32_t), s));
-  pp.ew.set_stream(s);
-  if (w) {
-    pp.ew.resize((ne + kPushUnit) * sizeof(R));  // padded like ent
-    HIP_CHECK(hipMemsetAsync(pp.ew.data<R>() + ne, 0, kPushUnit * sizeof(R), s));
-  } else {
-    pp.ew.release();
+}
+
+// real entry k at k + cm[k] (cm = inclusive prefix of the jump counts), its jumps
+// right before it
+__global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, int64_t ne,
+                         int64_t const* ws, uint32_t const* mj, unsigned long long const* cm, int wb, uint32_t pmax,
+                         uint16_t* ent16)
+{
+  uint32_t const jump = (1u << (16 - wb)) - 1, low = (1u << wb) - 1;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const w     = (int64_t)(keys[k] >> 32);
+    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
+    uint32_t const D    = (uint32_t)keys[k] - prev;
+    uint32_t const m    = mj[k];
+    int64_t const pos   = k + (int64_t)cm[k];
+    uint32_t const slot = rows[vals[k]] & low;
+    if (m == 0) {
+      ent16[pos] = (uint16_t)((D << wb) | slot);
+    } else {
+      for (uint32_t j = 0; j < m; ++j) {
+        uint32_t const pay   = j + 1 < m ? pmax : D - pmax * (m - 1);
+        ent16[pos - m + j] = (uint16_t)((jump << wb) | pay);
+      }
+      ent16[pos] = (uint16_t)slot;  // delta 0
+    }
   }
-  hipLaunchKernelGGL(k_push_pack<R>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                     vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
-                     w ? pp.ew.data<R>() : nullptr);
-  CGX_LAUNCH_CHECK();
+}
+
+// window starts in packed positions (nws[nwin] = total)
+__global__ void k_packed_win_starts(int64_t const* ws, unsigned long long const* cm, int64_t nwin, int64_t total, int64_t* nws)
+{
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x)
+    nws[w] = w == nwin ? total : ws[w] + (ws[w] > 0 ? (int64_t)cm[ws[w] - 1] : 0);
+}
+
+// unit heads over packed positions: window starts and multiples of kPushUnit
+__global__ void k_packed_unit_flags(int64_t total, uint32_t* flag)
+{
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x)
+    flag[p] = p % kPushUnit == 0 ? 1u : 0u;
+}
+__global__ void k_packed_mark_starts(int64_t const* nws, int64_t nwin, int64_t total, uint32_t* flag)
+{
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwin; w += (int64_t)gridDim.x * blockDim.x)
+    if (nws[w] < total) flag[nws[w]] = 1u;
+}
+__global__ void k_packed_unit_heads(uint32_t const* flag, uint32_t const* uid, int64_t total, int64_t const* nws,
+                                    int64_t nwin, push_unit* units)
+{
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    if (!flag[p]) continue;
+    int64_t lo = 0, hi = nwin - 1;  // last window with nws[w] <= p
+    while (lo < hi) {
+      int64_t mid = (lo + hi + 1) >> 1;
+      if (nws[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    units[uid[p]] = push_unit{p, 0, 0, lo};
+  }
+}
+
+// running source before the first entry of every (unit, wave segment)
+__global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t const* keys, int64_t ne,
+                            int64_t const* ws, uint32_t const* mj, unsigned long long const* cm, uint32_t dmax,
+                            uint32_t pmax, uint32_t* seg_base)
+{
+  int64_t const n = nunits * kSegsPerUnit;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    push_unit const u = units[i / kSegsPerUnit];
+    int64_t const p   = u.k0 + (i % kSegsPerUnit) * kSegEntries;
+    uint32_t base     = 0;
+    if (p < u.k1) {
+      int64_t lo = 0, hi = ne - 1;  // first real entry with k + cm[k] >= p
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (mid + (int64_t)cm[mid] < p) lo = mid + 1;
+        else hi = mid;
+      }
+      int64_t const k     = lo;
+      uint32_t const m    = mj[k];
+      int64_t const j     = p - (k + (int64_t)cm[k] - m);
+      int64_t const w     = (int64_t)(keys[k] >> 32);
+      uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
+      uint32_t const src  = (uint32_t)keys[k];
+      uint32_t const D    = src - prev;
+      base = j < (int64_t)m ? prev + pmax * (uint32_t)j : src - (m ? 0u : (D <= dmax ? D : 0u));
+    }
+    seg_base[i] = base;
+  }
+}
+
+// Items and queues over the units (host logic, once per graph)
+inline void build_items(hipStream_t s, pr_push_t& pp, push_unit const* units, int64_t nunits, bool xcd_queues_wanted)
+{
+  int64_t const ne = nunits ? to_host(&units[nunits - 1].k1, 1, s)[0] : 0;
   // Items and queues.  From 2^22 rows (8K windows): an item is a window's units,
   // or an equal share of a window of more than 1.5 tg entries; groups of
   // kGroupItems consecutive items are dealt to the 8 queues by longest-processing-
@@ -714,7 +874,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   // Below: one queue of tiles of <= 8 units of a window (RMAT-22: the XCD queues
   // measured 0.199 -> 0.216, the last groups' imbalance outweighing the L2 hits).
   auto hu = to_host(units, nunits, s);
-  bool const xcd_queues = wb == 13;
+  bool const xcd_queues = xcd_queues_wanted;
   int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * 4));
   std::vector<int64_t> item_u, item_e;
   for (int64_t u0 = 0; u0 < nunits;) {
@@ -771,8 +931,136 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.queue.set_stream(s);
   pp.queue.resize(std::max<size_t>(queue.size(), 1) * sizeof(int64_t));
   to_device(pp.queue.data<int64_t>(), queue.data(), queue.size(), s);
-  pp.nunits = nunits;
   pp.nitems = nitems;
+}
+
+// Push schedule of an edge list given as (row = destination, col = source) with
+// destinations in [0, n_rows) and sources in [0, n_cols) -- the SG pull adjacency
+// or one MG 2D block.
+template <typename C, typename R>
+void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
+                         int64_t n_cols, pr_push_t& pp)
+{
+  pp.built = true;
+  pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
+  if (!pp.ok) return;
+  int const wb       = push_win_bits(n_rows);
+  int const sb       = 32 - wb;
+  int64_t const nwin = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
+  pp.win_bits        = wb;
+  pp.nwin            = nwin;
+  pp.nacc            = nwin << wb;
+  pp.acc.set_stream(s);
+  pp.acc.resize(pp.nacc * sizeof(unsigned long long));
+  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
+  pp.tile_ctr.set_stream(s);
+  pp.tile_ctr.resize(kQueues * kCtrStride * sizeof(unsigned int));
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, kQueues * kCtrStride * sizeof(unsigned int), s));
+  pp.nunits = 0;
+  pp.nitems = 0;
+  pp.qoff.assign(kQueues + 1, 0);
+  if (ne == 0) return;
+  dbuf<uint64_t> keys_out(ne, s);
+  dbuf<uint32_t> vals_out(ne, s);
+  {
+    dbuf<uint64_t> keys(ne, s);
+    dbuf<uint32_t> vals(ne, s);
+    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
+                       keys.data(), vals.data());
+    CGX_LAUNCH_CHECK();
+    radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
+                                         32 + bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)), s);
+  }
+  dbuf<int64_t> ws(nwin + 1, s);
+  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
+                     nwin, ws.data());
+  CGX_LAUNCH_CHECK();
+  pp.packed = false;
+  if (!w && packed_enabled()) {  // 16-bit entries unless the jumps would grow the entries by more than half
+    uint32_t const dmax = (1u << (16 - wb)) - 2;  // coded deltas 0 .. dmax; dmax + 1 marks a jump
+    uint32_t const pmax = (1u << wb) - 1;         // jump payloads 1 .. pmax
+    dbuf<uint32_t> mj(ne + 1, s);
+    dbuf<unsigned long long> ex(ne + 1, s);
+    hipLaunchKernelGGL(k_jump_counts, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
+                       ws.data(), dmax, pmax, mj.data());
+    CGX_LAUNCH_CHECK();
+    fill<uint32_t>(mj.data() + ne, 1, 0u, s);
+    exclusive_scan<uint32_t, unsigned long long>(mj.data(), ex.data(), ne + 1, s);
+    int64_t const total = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
+    unsigned long long const* cm = ex.data() + 1;  // inclusive prefix
+    if (total <= ne + ne / 2 && (uint64_t)total < (1ull << 32)) {
+      pp.packed = true;
+      pp.ent16.set_stream(s);
+      pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // padded: the kernel loads whole units
+      HIP_CHECK(hipMemsetAsync(pp.ent16.data<uint16_t>() + total, 0, kPushUnit * sizeof(uint16_t), s));
+      hipLaunchKernelGGL(k_pack16, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
+                         vals_out.data(), rows, ne, ws.data(), mj.data(), cm, wb, pmax, pp.ent16.data<uint16_t>());
+      CGX_LAUNCH_CHECK();
+      dbuf<int64_t> nws(nwin + 1, s);
+      hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
+                         cm, nwin, total, nws.data());
+      dbuf<uint32_t> pflag(total + 1, s), puid(total + 1, s);
+      hipLaunchKernelGGL(k_packed_unit_flags, dim3(grid_for(total, kBlock, 16384)), dim3(kBlock), 0, s, total,
+                         pflag.data());
+      hipLaunchKernelGGL(k_packed_mark_starts, dim3(grid_for(nwin, kBlock, 4096)), dim3(kBlock), 0, s, nws.data(),
+                         nwin, total, pflag.data());
+      CGX_LAUNCH_CHECK();
+      fill<uint32_t>(pflag.data() + total, 1, 0u, s);
+      exclusive_scan<uint32_t, uint32_t>(pflag.data(), puid.data(), total + 1, s);
+      int64_t const nunits = (int64_t)to_host(puid.data() + total, 1, s)[0];
+      pp.units.set_stream(s);
+      pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
+      push_unit* units = pp.units.data<push_unit>();
+      hipLaunchKernelGGL(k_packed_unit_heads, dim3(grid_for(total, kBlock, 16384)), dim3(kBlock), 0, s, pflag.data(),
+                         puid.data(), total, nws.data(), nwin, units);
+      CGX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, total);
+      CGX_LAUNCH_CHECK();
+      pp.seg_base.set_stream(s);
+      pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
+      hipLaunchKernelGGL(k_seg_bases, dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0, s, units,
+                         nunits, keys_out.data(), ne, ws.data(), mj.data(), cm, dmax, pmax,
+                         pp.seg_base.data<uint32_t>());
+      CGX_LAUNCH_CHECK();
+      pp.ent.release();
+      pp.ew.release();
+      build_items(s, pp, units, nunits, wb == 13);
+      pp.nunits = nunits;
+      HIP_CHECK(hipStreamSynchronize(s));
+      return;
+    }
+  }
+  dbuf<uint32_t> flag(ne + 1, s), uid(ne + 1, s);
+  hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
+                     ws.data(), sb, flag.data());
+  CGX_LAUNCH_CHECK();
+  fill<uint32_t>(flag.data() + ne, 1, 0u, s);
+  exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
+  int64_t const nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
+  pp.units.set_stream(s);
+  pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
+  push_unit* units = pp.units.data<push_unit>();
+  hipLaunchKernelGGL(k_unit_heads, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
+                     flag.data(), uid.data(), ne, units);
+  CGX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, ne);
+  CGX_LAUNCH_CHECK();
+  pp.ent.set_stream(s);
+  pp.ent.resize((ne + kPushUnit) * sizeof(uint32_t));  // padded: the kernel loads whole units
+  HIP_CHECK(hipMemsetAsync(pp.ent.data<uint32_t>() + ne, 0, kPushUnit * sizeof(uint32_t), s));
+  pp.ew.set_stream(s);
+  if (w) {
+    pp.ew.resize((ne + kPushUnit) * sizeof(R));  // padded like ent
+    HIP_CHECK(hipMemsetAsync(pp.ew.data<R>() + ne, 0, kPushUnit * sizeof(R), s));
+  } else {
+    pp.ew.release();
+  }
+  hipLaunchKernelGGL(k_push_pack<R>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
+                     vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
+                     w ? pp.ew.data<R>() : nullptr);
+  CGX_LAUNCH_CHECK();
+  build_items(s, pp, units, nunits, wb == 13);
+  pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -836,6 +1124,8 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 {
   sa.ent      = pp.ent.data<uint32_t>();
   sa.ew       = pp.ew.empty() ? nullptr : pp.ew.data<R>();
+  sa.ent16    = pp.ent16.data<uint16_t>();
+  sa.seg_base = pp.seg_base.data<uint32_t>();
   sa.units    = pp.units.data<push_unit>();
   sa.nunits   = pp.nunits;
   sa.acc      = pp.acc.data<unsigned long long>();
@@ -847,10 +1137,11 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, kQueues * kCtrStride * sizeof(unsigned int), s));
 }
 
-// the push kernel for the schedule's window bits
+// the push kernel for the schedule's window bits and entry format
 template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted)
 {
+  if (pp.packed) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R> : k_pr_push16<12, V, E, R>;
   constexpr bool wide = sizeof(R) == 8;  // fp64 weights: no 8-waves bound (see k_pr_push_q_wide)
   if (pp.win_bits == 13)
     return weighted ? (wide ? k_pr_push_q_wide<13, V, E, R, true> : k_pr_push_q<13, V, E, R, true>)
