@@ -146,7 +146,8 @@ def test_empty_and_edgeless_graph():
     assert np.allclose(got, ref, rtol=1e-6)
 
 
-@pytest.mark.parametrize("weighted,symmetric,renumber", [(False, True, True), (True, False, False)])
+@pytest.mark.parametrize("weighted,symmetric,renumber", [(False, True, True), (True, False, False),
+                                                        (False, False, False)])
 def test_rmat_multi_window_push(weighted, symmetric, renumber):
     """Scale 20: > 2^19 sources (several source segments per window) and ~128
     destination windows of the push path (pagerank.hip), against the oracle and
@@ -194,3 +195,19 @@ def test_sparse_wide_push(nv, ne):
     ref = opr.pagerank(nv, s, d, None, 0.85, 1e-6, 500)
     rel = np.abs(got[:nv] - ref) / ref
     assert rel.max() < REL, rel.max()
+
+
+@pytest.mark.parametrize("scale,renumber", [(12, True), (20, True), (20, False)])
+def test_packed_entries_bitwise_equal_plain(scale, renumber, monkeypatch):
+    """The 16-bit packed push entries (pagerank.hip push_body16: source deltas, jump
+    entries, per-wave-segment bases) must give the same fixed-point sums -- so the
+    same bits -- as the 32-bit entries (CGX_PR_PACKED=0)."""
+    s, d, _ = rmat_graph(scale, False, True)
+    h, G = make_graph(s, d, None, transposed=True, renumber=renumber, symmetric=True)
+    r_packed = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    it = h.last_iterations()
+    monkeypatch.setenv("CGX_PR_PACKED", "0")
+    h2, G2 = make_graph(s, d, None, transposed=True, renumber=renumber, symmetric=True)
+    r_plain = host(plc().pagerank(h2, G2, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    assert h2.last_iterations() == it
+    assert np.array_equal(r_packed, r_plain)
