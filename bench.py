@@ -490,6 +490,7 @@ def main():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--traffic-child", choices=["pagerank", "bfs"], default=None, help=argparse.SUPPRESS)
     ap.add_argument("--bfs-only", action="store_true", help="A/B aid: only the BFS leg, its dict on stdout")
+    ap.add_argument("--louvain-only", action="store_true", help="A/B aid: only the Louvain leg, its dict on stdout")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -523,6 +524,11 @@ def main():
     if args.bfs_only:
         r = bfs_leg(p, args)
         log(f"[bench] bfs RMAT-{args.bfs_scale}: {r['mteps_harmonic_mean']:.1f} MTEPS, {r['ms_mean']:.3f} ms/traversal")
+        print(json.dumps(r), flush=True)
+        return
+    if args.louvain_only:
+        r = louvain_leg(p, args)
+        log(f"[bench] louvain RMAT-{r['scale']}: {r['time_s']:.3f}s Q={r['modularity']:.6f} levels={r['levels']}")
         print(json.dumps(r), flush=True)
         return
 

@@ -32,6 +32,8 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <cfloat>
+#include <cmath>
+#include <cstring>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -308,6 +310,460 @@ __global__ void k_to_vertex(uint32_t const* x, int64_t n, V* out)
     out[i] = (V)x[i];
 }
 
+// ------------------------------------------------ hash local move
+// One block per chunk of whole rows (<= kHashRows rows, <= kHashEdges edges, so a
+// chunk's distinct (row, neighbour cluster) pairs fit an LDS table at load <= 1/2).
+// The pair sums are 64-bit fixed point (scale 2^(61 - e), every row weight < 2^e):
+// order-independent, and exact for integer weights, so the gains are the same IEEE
+// values as the sort path's and the oracle's.  Replaces key build + radix sort +
+// two reduce_by_key passes (~20 B of HBM traffic per edge per pass) by one pass
+// over the edges.
+constexpr int kHashEdges   = 2048;
+constexpr int kHashRows    = 512;
+constexpr int kHashSlots   = 4096;
+constexpr int kHashThreads = 512;
+constexpr u64 kEmptyKey    = ~0ull;
+
+struct hash_sweep_args {
+  uint32_t const* src;
+  uint32_t const* dst;
+  double const* w;
+  int64_t const* off;
+  int64_t const* chunks;  // 2 per chunk: first row, end row
+  uint32_t const* c;
+  uint32_t base;
+  double const* self;
+  double const* a;
+  uint8_t const* present;
+  double const* k;
+  double m, gamma, scale, inv_scale;
+  uint32_t* next;
+  bool up_down;
+};
+
+__device__ inline unsigned pair_slot(u64 key, int bits) { return (unsigned)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits)); }
+// monotone map double -> u64 (larger gain -> larger key)
+__device__ inline u64 order_bits(double d)
+{
+  u64 const b = (u64)__double_as_longlong(d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double unorder_bits(u64 o)
+{
+  return __longlong_as_double((long long)((o >> 63) ? (o & 0x7fffffffffffffffull) : ~o));
+}
+
+__global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
+{
+#pragma clang fp contract(off)
+  __shared__ u64 key[kHashSlots];
+  __shared__ u64 val[kHashSlots];
+  __shared__ double old_s[kHashRows];
+  __shared__ u64 best[kHashRows];
+  __shared__ uint32_t bestc[kHashRows];
+  int const tid = threadIdx.x;
+  int64_t const r0 = p.chunks[2 * blockIdx.x], r1 = p.chunks[2 * blockIdx.x + 1];
+  int const nrow   = (int)(r1 - r0);
+  int64_t const e0 = p.off[r0], e1 = p.off[r1];
+  int bits         = 6;  // table of 2^bits >= 2 * edges slots
+  while ((1 << bits) < 2 * (int)(e1 - e0)) ++bits;
+  int const nslot = 1 << bits;
+  unsigned const mask = (unsigned)nslot - 1;
+  for (int i = tid; i < nslot; i += kHashThreads) {
+    key[i] = kEmptyKey;
+    val[i] = 0;
+  }
+  for (int i = tid; i < nrow; i += kHashThreads) {
+    old_s[i] = 0.0;
+    best[i]  = 0;
+    bestc[i] = 0xffffffffu;
+  }
+  __syncthreads();
+  for (int64_t e = e0 + tid; e < e1; e += kHashThreads) {
+    u64 const kk = ((u64)(p.src[e] - (uint32_t)r0) << 32) | p.c[p.dst[e]];
+    u64 const v  = (u64)__double2ll_rn(p.w[e] * p.scale);
+    unsigned h   = pair_slot(kk, bits);
+    while (true) {
+      u64 const prev = atomicCAS(&key[h], kEmptyKey, kk);
+      if (prev == kEmptyKey || prev == kk) {
+        atomicAdd(&val[h], v);
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  __syncthreads();
+  // weight into the own cluster, self loop excluded (k_old_sum)
+  for (int i = tid; i < nrow; i += kHashThreads) {
+    int64_t const u = r0 + i;
+    u64 const kk    = ((u64)i << 32) | p.c[u + p.base];
+    unsigned h      = pair_slot(kk, bits);
+    while (key[h] != kEmptyKey) {
+      if (key[h] == kk) {
+        old_s[i] = (double)(long long)val[h] * p.inv_scale - p.self[u];
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  __syncthreads();
+  // gains (k_gain), per-row maximum
+  for (int h = tid; h < nslot; h += kHashThreads) {
+    u64 const kk = key[h];
+    if (kk == kEmptyKey) continue;
+    int const i       = (int)(kk >> 32);
+    uint32_t const cc = (uint32_t)kk;
+    int64_t const u   = r0 + i;
+    uint32_t const cu = p.c[u + p.base];
+    double s          = (double)(long long)val[h] * p.inv_scale;
+    if (cc == cu) s = s - p.self[u];
+    double a_new = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
+    double a_old = p.a[cu];
+    double kv    = p.k[u];
+    double dq    = 2.0 * (((s - old_s[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+    u64 const o  = order_bits(dq);
+    val[h]       = o;
+    atomicMax(&best[i], o);
+  }
+  __syncthreads();
+  // ties: the smaller cluster (best_gain_op)
+  for (int h = tid; h < nslot; h += kHashThreads) {
+    u64 const kk = key[h];
+    if (kk == kEmptyKey) continue;
+    int const i = (int)(kk >> 32);
+    if (val[h] == best[i]) atomicMin(&bestc[i], (uint32_t)kk);
+  }
+  __syncthreads();
+  for (int i = tid; i < nrow; i += kHashThreads) {
+    if (best[i] == 0) continue;  // no edges
+    int64_t const u = r0 + i;
+    double const dq = unorder_bits(best[i]);
+    uint32_t const b = bestc[i];
+    if (dq > 0.0 && ((b > p.c[u + p.base]) == p.up_down)) p.next[u] = b;
+  }
+}
+
+// out[0] != 0: some weight is negative (or NaN); out[1] = largest row weight's bits
+__global__ void k_level_stats(double const* w, int64_t ne, double const* k, int64_t nr, u64* out)
+{
+  __shared__ u64 sn[kBlock], sk[kBlock];
+  u64 neg = 0, kmax = 0;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+    if (!(w[e] >= 0.0)) neg = 1;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nr; r += (int64_t)gridDim.x * blockDim.x) {
+    u64 const b = (u64)__double_as_longlong(k[r]);
+    kmax        = b > kmax ? b : kmax;
+  }
+  sn[threadIdx.x] = neg;
+  sk[threadIdx.x] = kmax;
+  __syncthreads();
+  for (int st = kBlock / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+      sn[threadIdx.x] |= sn[threadIdx.x + st];
+      sk[threadIdx.x] = sk[threadIdx.x] > sk[threadIdx.x + st] ? sk[threadIdx.x] : sk[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (sn[0]) atomicOr(&out[0], 1ull);
+    atomicMax(&out[1], sk[0]);
+  }
+}
+
+// big-row edges gathered into their own COO: rows[j]'s edges start at first[j] and
+// land at pos[j] (pos has nb + 1 entries)
+__global__ void k_gather_rows(int64_t const* first, int64_t const* pos, int64_t nb, uint32_t const* src,
+                              uint32_t const* dst, double const* w, int64_t n, uint32_t* os, uint32_t* od, double* ow)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nb - 1;  // last j with pos[j] <= i
+    while (lo < hi) {
+      int64_t mid = (lo + hi + 1) >> 1;
+      if (pos[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    int64_t const e = first[lo] + (i - pos[lo]);
+    os[i]           = src[e];
+    od[i]           = dst[e];
+    ow[i]           = w[e];
+  }
+}
+
+// ------------------------------------------------ hash local move, heavy rows
+// Rows of degree > kHashEdges (RMAT hubs: ~15 % of the edges at level 0, more after
+// the first contraction) in two LDS passes instead of a radix sort:
+//  A. one block per segment of <= kBigSeg edges of one row: LDS table keyed by the
+//     neighbour cluster -> the segment's distinct (cluster, partial sum) pairs,
+//     written grouped by bucket (hash of the cluster, 2^logb buckets per row sized
+//     for ~kBigPerBucket distinct clusters each); the own-cluster partial is added
+//     to the row's own-sum (integer fixed point: order-free);
+//  B. one block per (row, bucket): merges that bucket's partials of every segment
+//     of the row in an LDS table, evaluates the gains, keeps the bucket's best;
+//  C. one thread per row: best over the buckets -> move.
+// A bucket whose distinct clusters exceed the table's cap raises a flag and the
+// level falls back to the sort path for its heavy rows (never seen on RMAT).
+constexpr int kBigSeg        = 4096;
+constexpr int kBigSlots      = 8192;
+constexpr int kBigThreads    = 1024;
+constexpr int kBigMaxBuckets = 4096;
+constexpr int kBigPerBucket  = 1024;
+constexpr int kBigMaxSegs    = 2048;
+constexpr int kBktSlots      = 4096;
+constexpr int kBktThreads    = 512;
+constexpr int kBktCap        = 3072;  // < kBktSlots - kBktThreads: probing always ends
+constexpr uint32_t kEmpty32  = 0xffffffffu;
+
+struct big_seg {
+  int64_t e0, e1;  // edges in the level COO
+  int64_t pbase;   // first partial slot
+  int64_t boff;    // this segment's 2^logb + 1 bucket offsets
+  uint32_t j, pad;
+};
+struct big_row {
+  int64_t first;        // first edge
+  uint32_t row, logb;   // row index, log2 of the bucket count
+  uint32_t sbeg, send;  // segments
+  uint32_t bbeg, pad;   // first (row, bucket) block
+};
+
+struct big_args {
+  uint32_t const* dst;
+  double const* w;
+  uint32_t const* c;
+  uint32_t base;
+  big_seg const* segs;
+  big_row const* rows;
+  int64_t nrows;
+  uint32_t* pkey;
+  u64* pval;
+  int32_t* boffs;
+  u64* own;
+  u64 const* bblocks;
+  double const* self;
+  double const* a;
+  uint8_t const* present;
+  double const* k;
+  double m, gamma, scale, inv_scale;
+  u64* best_q;
+  uint32_t* best_c;
+  int* overflow;
+  int cap;
+  uint32_t* next;
+  bool up_down;
+};
+
+__device__ inline unsigned slot32(uint32_t x, int bits) { return (x * 0x9E3779B1u) >> (32 - bits); }
+__device__ inline unsigned bucket_of(uint32_t x, unsigned logb)
+{
+  return logb ? ((x ^ 0x5bd1e995u) * 0x85EBCA6Bu) >> (32 - logb) : 0u;
+}
+
+// exclusive scan of a[0, n) in LDS, n <= T * PER; returns the total
+template <int T, int PER>
+__device__ uint32_t block_excl_scan(uint32_t* a, int n, uint32_t* wsum)
+{
+  int const t = threadIdx.x;
+  uint32_t v[PER], s = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    int const i = PER * t + q;
+    v[q]        = i < n ? a[i] : 0u;
+    s += v[q];
+  }
+  uint32_t x = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t const y = __shfl_up(x, d, 64);
+    if ((t & 63) >= d) x += y;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = x;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t r = 0;
+    for (int i = 0; i < T / 64; ++i) {
+      uint32_t const q = wsum[i];
+      wsum[i]          = r;
+      r += q;
+    }
+    wsum[T / 64] = r;
+  }
+  __syncthreads();
+  uint32_t run = x - s + wsum[t >> 6];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    int const i = PER * t + q;
+    if (i < n) a[i] = run;
+    run += v[q];
+  }
+  uint32_t const total = wsum[T / 64];
+  __syncthreads();
+  return total;
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
+{
+  __shared__ uint32_t key[kBigSlots];
+  __shared__ u64 val[kBigSlots];
+  __shared__ uint32_t hist[kBigMaxBuckets];
+  __shared__ uint32_t wsum[kBigThreads / 64 + 1];
+  int const tid     = threadIdx.x;
+  big_seg const sg  = p.segs[blockIdx.x];
+  big_row const rw  = p.rows[sg.j];
+  int const nbk     = 1 << rw.logb;
+  for (int i = tid; i < kBigSlots; i += kBigThreads) {
+    key[i] = kEmpty32;
+    val[i] = 0;
+  }
+  for (int i = tid; i < nbk; i += kBigThreads) hist[i] = 0;
+  __syncthreads();
+  for (int64_t e = sg.e0 + tid; e < sg.e1; e += kBigThreads) {
+    uint32_t const cc = p.c[p.dst[e]];
+    u64 const v       = (u64)__double2ll_rn(p.w[e] * p.scale);
+    unsigned h        = slot32(cc, 13);
+    while (true) {
+      uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
+      if (prev == kEmpty32 || prev == cc) {
+        atomicAdd(&val[h], v);
+        break;
+      }
+      h = (h + 1) & (kBigSlots - 1);
+    }
+  }
+  __syncthreads();
+  uint32_t const cu = p.c[rw.row + p.base];
+  for (int i = tid; i < kBigSlots; i += kBigThreads) {
+    uint32_t const cc = key[i];
+    if (cc == kEmpty32) continue;
+    if (cc == cu) atomicAdd(&p.own[sg.j], val[i]);
+    atomicAdd(&hist[bucket_of(cc, rw.logb)], 1u);
+  }
+  __syncthreads();
+  uint32_t const total = block_excl_scan<kBigThreads, kBigMaxBuckets / kBigThreads>(hist, nbk, wsum);
+  for (int b = tid; b < nbk; b += kBigThreads) p.boffs[sg.boff + b] = (int32_t)hist[b];
+  if (tid == 0) p.boffs[sg.boff + nbk] = (int32_t)total;
+  __syncthreads();
+  for (int i = tid; i < kBigSlots; i += kBigThreads) {
+    uint32_t const cc = key[i];
+    if (cc == kEmpty32) continue;
+    uint32_t const pos     = atomicAdd(&hist[bucket_of(cc, rw.logb)], 1u);
+    p.pkey[sg.pbase + pos] = cc;
+    p.pval[sg.pbase + pos] = val[i];
+  }
+}
+
+__global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
+{
+#pragma clang fp contract(off)
+  __shared__ uint32_t key[kBktSlots];
+  __shared__ u64 val[kBktSlots];
+  __shared__ uint32_t pre[kBigMaxSegs];
+  __shared__ int64_t start[kBigMaxSegs];
+  __shared__ uint32_t wsum[kBktThreads / 64 + 1];
+  __shared__ uint32_t distinct, bc;
+  __shared__ int over;
+  __shared__ u64 bq;
+  int const tid  = threadIdx.x;
+  u64 const jb   = p.bblocks[blockIdx.x];
+  uint32_t const j = (uint32_t)(jb >> 32), b = (uint32_t)jb;
+  big_row const rw = p.rows[j];
+  int const nbk    = 1 << rw.logb;
+  int const ns     = (int)(rw.send - rw.sbeg);
+  for (int i = tid; i < ns; i += kBktThreads) {
+    big_seg const sg = p.segs[rw.sbeg + i];
+    int32_t const lo = p.boffs[sg.boff + b], hi = p.boffs[sg.boff + b + 1];
+    pre[i]           = (uint32_t)(hi - lo);
+    start[i]         = sg.pbase + lo;
+  }
+  for (int i = tid; i < kBktSlots; i += kBktThreads) {
+    key[i] = kEmpty32;
+    val[i] = 0;
+  }
+  if (tid == 0) {
+    distinct = 0;
+    over     = 0;
+    bq       = 0;
+    bc       = kEmpty32;
+  }
+  __syncthreads();
+  uint32_t const total = block_excl_scan<kBktThreads, kBigMaxSegs / kBktThreads>(pre, ns, wsum);
+  for (uint32_t f = tid; f < total; f += kBktThreads) {
+    int lo = 0, hi = ns - 1;  // last segment with pre <= f
+    while (lo < hi) {
+      int const mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= f) lo = mid;
+      else hi = mid - 1;
+    }
+    int64_t const x   = start[lo] + (f - pre[lo]);
+    uint32_t const cc = p.pkey[x];
+    u64 const v       = p.pval[x];
+    unsigned h        = slot32(cc, 12);
+    bool stop         = false;
+    while (true) {
+      uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
+      if (prev == kEmpty32 || prev == cc) {
+        atomicAdd(&val[h], v);
+        if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= p.cap) {
+          over = 1;
+          stop = true;
+        }
+        break;
+      }
+      h = (h + 1) & (kBktSlots - 1);
+    }
+    if (stop) break;
+  }
+  __syncthreads();
+  if (over) {
+    if (tid == 0) atomicOr(p.overflow, 1);
+    return;
+  }
+  uint32_t const u  = rw.row;
+  uint32_t const cu = p.c[u + p.base];
+  double const kv   = p.k[u], a_old = p.a[cu], self = p.self[u];
+  double const old_s = (double)(long long)p.own[j] * p.inv_scale - self;
+  for (int h = tid; h < kBktSlots; h += kBktThreads) {
+    uint32_t const cc = key[h];
+    if (cc == kEmpty32) continue;
+    double s = (double)(long long)val[h] * p.inv_scale;
+    if (cc == cu) s = s - self;
+    double a_new = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
+    double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+    u64 const o  = order_bits(dq);
+    val[h]       = o;
+    atomicMax(&bq, o);
+  }
+  __syncthreads();
+  for (int h = tid; h < kBktSlots; h += kBktThreads)
+    if (key[h] != kEmpty32 && val[h] == bq) atomicMin(&bc, key[h]);
+  __syncthreads();
+  if (tid == 0) {
+    p.best_q[blockIdx.x] = bq;
+    p.best_c[blockIdx.x] = bc;
+  }
+  (void)nbk;
+}
+
+__global__ void k_big_move(big_args p)
+{
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < p.nrows; j += (int64_t)gridDim.x * blockDim.x) {
+    big_row const rw = p.rows[j];
+    u64 best         = 0;
+    uint32_t bc      = kEmpty32;
+    for (uint32_t i = rw.bbeg; i < rw.bbeg + (1u << rw.logb); ++i) {
+      u64 const o = p.best_q[i];
+      if (o == 0) continue;
+      uint32_t const c = p.best_c[i];
+      if (o > best || (o == best && c < bc)) {
+        best = o;
+        bc   = c;
+      }
+    }
+    if (best == 0) continue;
+    double const dq = unorder_bits(best);
+    if (dq > 0.0 && ((bc > p.c[rw.row + p.base]) == p.up_down)) p.next[rw.row] = bc;
+  }
+}
+
 inline unsigned blocks(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 16384); }
 
 // ---------------------------------------------------------------- driver
@@ -389,23 +845,22 @@ void cluster_weights(louvain_state& S, level_graph const& g, uint32_t const* c, 
   }
 }
 
-// one synchronous local-move sweep (update_clustering_by_delta_modularity) over
-// this rank's rows; next[row] = the row's cluster after the sweep
-void sweep(louvain_state& S, level_graph const& g, uint32_t const* c, uint32_t* next, double const* k,
-           double const* self, double const* a, uint8_t const* present, bool up_down)
+// the sort-based local move over the edges (src, dst, w)[0, ne) of some of the
+// rows (whole rows only): next[row] is written for the rows that move
+void sweep_sorted(louvain_state& S, level_graph const& g, uint32_t const* src, uint32_t const* dst, double const* w,
+                  int64_t ne, uint32_t const* c, uint32_t* next, double const* k, double const* self, double const* a,
+                  uint8_t const* present, bool up_down)
 {
   hipStream_t s = S.s;
-  int64_t nv = g.nv, nr = g.nrows, ne = g.ne;
+  int64_t nv = g.nv, nr = g.nrows;
   uint32_t const base = (uint32_t)g.base;
-  if (nr) HIP_CHECK(hipMemcpyAsync(next, c + g.base, nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   if (ne == 0) return;
   dbuf<u64> keys(ne, s), keys2(ne, s);
   dbuf<double> w2(ne, s), psum(ne, s);
   int const cb = bits_for((unsigned long long)std::max<int64_t>(nv - 1, 0));
-  hipLaunchKernelGGL(k_sweep_keys, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), c, ne, cb,
-                     keys.data());
+  hipLaunchKernelGGL(k_sweep_keys, dim3(blocks(ne)), dim3(kBlock), 0, s, src, dst, c, ne, cb, keys.data());
   CGX_LAUNCH_CHECK();
-  radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0,
+  radix_sort_pairs<u64, double>(keys.data(), keys2.data(), w, w2.data(), (size_t)ne, 0,
                                 cb + bits_for(std::max<int64_t>(nr - 1, 0)), s);
   // (row, neighbour cluster) -> sum of weights; `keys` reused for the pair keys
   int64_t np = reduce_by_key(keys2.data(), w2.data(), (size_t)ne, keys.data(), psum.data(), rocprim::plus<double>(),
@@ -428,6 +883,241 @@ void sweep(louvain_state& S, level_graph const& g, uint32_t const* c, uint32_t* 
   hipLaunchKernelGGL(k_move, dim3(blocks(nu)), dim3(kBlock), 0, s, uu.data(), best.data(), nu, c, base, next, up_down);
   CGX_LAUNCH_CHECK();
   (void)nv;
+}
+
+// Per-level schedule of the local move (the level graph is fixed across its
+// sweeps): rows of degree <= kHashEdges go to the LDS-hash kernel in chunks of
+// whole rows; heavier rows (the RMAT hubs, a prefix when rows are in descending
+// degree order as contraction numbers them) keep the sort path over their own edges.
+struct sweep_plan {
+  bool hash       = false;
+  int64_t e_big   = 0;  // edges of the rows on the sort path
+  uint32_t const* bsrc = nullptr;
+  uint32_t const* bdst = nullptr;
+  double const* bw     = nullptr;
+  dbuf<uint32_t> gsrc, gdst;  // big rows gathered, when they are not a prefix
+  dbuf<double> gw;
+  dbuf<int64_t> chunks;
+  int64_t nchunks = 0;
+  double scale = 0, inv_scale = 0;
+  int64_t const* off = nullptr;  // the level's row offsets
+  // heavy rows on the LDS two-pass path (k_big_*); big_hash false: sort path
+  bool big_hash = false;
+  int64_t nbig = 0, nsegs = 0, nbblocks = 0;
+  dbuf<big_row> brows;
+  dbuf<big_seg> bsegs;
+  dbuf<u64> bblocks, own, best_q;
+  dbuf<uint32_t> best_c, pkey;
+  dbuf<u64> pval;
+  dbuf<int32_t> boffs;
+  dbuf<int> overflow;
+};
+
+inline bool hash_sweep_enabled()
+{
+  char const* e = std::getenv("CGX_LOUVAIN_HASH");  // "0": sort path only (A/B, tests)
+  return !(e && e[0] == '0');
+}
+
+// CGX_LOUVAIN_BIG=sort: heavy rows on the sort path (A/B, tests)
+inline bool big_hash_enabled()
+{
+  char const* e = std::getenv("CGX_LOUVAIN_BIG");
+  return !(e && std::strcmp(e, "sort") == 0);
+}
+
+// CGX_LOUVAIN_BIG_CAP: lower the (row, bucket) table cap (tests of the fallback)
+inline int big_bucket_cap()
+{
+  char const* e = std::getenv("CGX_LOUVAIN_BIG_CAP");
+  int const v   = e ? std::atoi(e) : 0;
+  return v > 0 && v < kBktCap ? v : kBktCap;
+}
+
+inline int ceil_log2(int64_t x)
+{
+  int l = 0;
+  while ((1ll << l) < x) ++l;
+  return l;
+}
+
+void plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh, std::vector<int64_t> const& big, sweep_plan& P)
+{
+  int64_t const nb = (int64_t)big.size();
+  std::vector<big_row> rows(nb);
+  std::vector<big_seg> segs;
+  std::vector<u64> bb;
+  int64_t pstart = 0, boff = 0;
+  for (int64_t j = 0; j < nb; ++j) {
+    int64_t const r = big[j], first = oh[r], d = oh[r + 1] - oh[r];
+    int64_t const nseg = (d + kBigSeg - 1) / kBigSeg;
+    if (nseg > kBigMaxSegs) return;  // > 8M edges in one row: sort path
+    int const logb = std::min(ceil_log2((d + kBigPerBucket - 1) / kBigPerBucket), ceil_log2(kBigMaxBuckets));
+    big_row& rw = rows[j];
+    rw.first    = first;
+    rw.row      = (uint32_t)r;
+    rw.logb     = (uint32_t)logb;
+    rw.sbeg     = (uint32_t)segs.size();
+    rw.bbeg     = (uint32_t)bb.size();
+    for (int64_t q = 0; q < nseg; ++q) {
+      big_seg sg;
+      sg.e0    = first + q * kBigSeg;
+      sg.e1    = std::min(first + d, sg.e0 + kBigSeg);
+      sg.pbase = pstart + q * kBigSeg;
+      sg.boff  = boff;
+      sg.j     = (uint32_t)j;
+      sg.pad   = 0;
+      boff += (1 << logb) + 1;
+      segs.push_back(sg);
+    }
+    rw.send = (uint32_t)segs.size();
+    rw.pad  = 0;
+    for (int b = 0; b < (1 << logb); ++b) bb.push_back(((u64)j << 32) | (u64)b);
+    pstart += d;
+  }
+  P.nbig     = nb;
+  P.nsegs    = (int64_t)segs.size();
+  P.nbblocks = (int64_t)bb.size();
+  P.brows.resize(nb, s);
+  P.bsegs.resize(P.nsegs, s);
+  P.bblocks.resize(P.nbblocks, s);
+  to_device(P.brows.data(), rows.data(), nb, s);
+  to_device(P.bsegs.data(), segs.data(), P.nsegs, s);
+  to_device(P.bblocks.data(), bb.data(), P.nbblocks, s);
+  P.own.resize(nb, s);
+  P.best_q.resize(P.nbblocks, s);
+  P.best_c.resize(P.nbblocks, s);
+  P.pkey.resize(pstart, s);
+  P.pval.resize(pstart, s);
+  P.boffs.resize(boff, s);
+  P.overflow.resize(1, s);
+  HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+  P.big_hash = true;
+}
+
+void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, double const* k, sweep_plan& P)
+{
+  hipStream_t s    = S.s;
+  int64_t const nr = g.nrows, ne = g.ne;
+  if (ne == 0 || nr == 0 || !hash_sweep_enabled()) return;
+  dbuf<u64> st(2, s);
+  fill<u64>(st.data(), 2, 0ull, s);
+  hipLaunchKernelGGL(k_level_stats, dim3(std::min<unsigned>(blocks(std::max(ne, nr)), 2048)), dim3(kBlock), 0, s,
+                     g.w.data(), ne, k, nr, st.data());
+  CGX_LAUNCH_CHECK();
+  auto sh = to_host(st.data(), 2, s);
+  if (sh[0]) return;  // negative weights: the fixed-point sums assume w >= 0
+  double kmax;
+  std::memcpy(&kmax, &sh[1], sizeof(double));
+  if (!(kmax < 1e300)) return;
+  int const e = kmax > 0 ? std::ilogb(kmax) + 1 : 0;  // every row weight < 2^e
+  P.scale     = std::ldexp(1.0, 61 - e);
+  P.inv_scale = std::ldexp(1.0, e - 61);
+
+  auto oh = to_host(off, (size_t)nr + 1, s);
+  std::vector<int64_t> ch, big;
+  int64_t r0 = 0, ce = 0;
+  auto close = [&](int64_t r1) {
+    if (ce > 0) {
+      ch.push_back(r0);
+      ch.push_back(r1);
+    }
+    ce = 0;
+  };
+  for (int64_t r = 0; r < nr; ++r) {
+    int64_t const d = oh[r + 1] - oh[r];
+    if (d > kHashEdges) {
+      close(r);
+      big.push_back(r);
+      r0 = r + 1;
+      continue;
+    }
+    if (ce + d > kHashEdges || r - r0 == kHashRows) {
+      close(r);
+      r0 = r;
+    }
+    ce += d;
+  }
+  close(nr);
+  P.nchunks = (int64_t)ch.size() / 2;
+  if (P.nchunks) {
+    P.chunks.resize(ch.size(), s);
+    to_device(P.chunks.data(), ch.data(), ch.size(), s);
+  }
+  int64_t const nb = (int64_t)big.size();
+  if (nb && big_hash_enabled()) plan_big_rows(s, oh, big, P);
+  if (nb) {
+    bool const prefix = big.back() == nb - 1;
+    if (prefix) {
+      P.e_big = oh[nb];
+      P.bsrc  = g.src.data();
+      P.bdst  = g.dst.data();
+      P.bw    = g.w.data();
+    } else {
+      std::vector<int64_t> first(nb), pos(nb + 1, 0);
+      for (int64_t j = 0; j < nb; ++j) {
+        first[j]   = oh[big[j]];
+        pos[j + 1] = pos[j] + (oh[big[j] + 1] - oh[big[j]]);
+      }
+      P.e_big = pos[nb];
+      dbuf<int64_t> fd(nb, s), pd(nb + 1, s);
+      to_device(fd.data(), first.data(), nb, s);
+      to_device(pd.data(), pos.data(), nb + 1, s);
+      P.gsrc.resize(P.e_big, s);
+      P.gdst.resize(P.e_big, s);
+      P.gw.resize(P.e_big, s);
+      hipLaunchKernelGGL(k_gather_rows, dim3(blocks(P.e_big)), dim3(kBlock), 0, s, fd.data(), pd.data(), nb,
+                         g.src.data(), g.dst.data(), g.w.data(), P.e_big, P.gsrc.data(), P.gdst.data(), P.gw.data());
+      CGX_LAUNCH_CHECK();
+      HIP_CHECK(hipStreamSynchronize(s));  // fd / pd go out of scope
+      P.bsrc = P.gsrc.data();
+      P.bdst = P.gdst.data();
+      P.bw   = P.gw.data();
+    }
+  }
+  P.off  = off;
+  P.hash = true;
+}
+
+// one synchronous local-move sweep (update_clustering_by_delta_modularity) over
+// this rank's rows; next[row] = the row's cluster after the sweep
+void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const* c, uint32_t* next,
+           double const* k, double const* self, double const* a, uint8_t const* present, bool up_down)
+{
+  hipStream_t s = S.s;
+  if (g.nrows) HIP_CHECK(hipMemcpyAsync(next, c + g.base, g.nrows * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  if (g.ne == 0) return;
+  if (!P.hash) {
+    sweep_sorted(S, g, g.src.data(), g.dst.data(), g.w.data(), g.ne, c, next, k, self, a, present, up_down);
+    return;
+  }
+  if (P.e_big && P.big_hash) {
+    big_args ba{g.dst.data(), g.w.data(), c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
+                P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, present, k, S.m, S.gamma,
+                P.scale, P.inv_scale, P.best_q.data(), P.best_c.data(), P.overflow.data(), big_bucket_cap(), next,
+                up_down};
+    fill<u64>(P.own.data(), P.nbig, 0ull, s);
+    fill<int>(P.overflow.data(), 1, 0, s);
+    hipLaunchKernelGGL(k_big_partials, dim3((unsigned)P.nsegs), dim3(kBigThreads), 0, s, ba);
+    CGX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_big_buckets, dim3((unsigned)P.nbblocks), dim3(kBktThreads), 0, s, ba);
+    CGX_LAUNCH_CHECK();
+    if (to_host_scalar(P.overflow.data(), s) == 0) {
+      hipLaunchKernelGGL(k_big_move, dim3(blocks(P.nbig)), dim3(kBlock), 0, s, ba);
+      CGX_LAUNCH_CHECK();
+    } else {
+      P.big_hash = false;  // a bucket outgrew its table: this level's heavy rows use the sort path
+      sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down);
+    }
+  } else if (P.e_big) {
+    sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down);
+  }
+  if (P.nchunks) {
+    hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), c, (uint32_t)g.base, self, a,
+                       present, k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down};
+    hipLaunchKernelGGL(k_sweep_hash, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
+    CGX_LAUNCH_CHECK();
+  }
 }
 
 // contract the level graph by `labels` (graph_contraction / coarsen_graph): sum
@@ -552,13 +1242,15 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     fill<uint8_t>(present.data(), nv, 1, s);
     dbuf<uint32_t> clusters(nv, s), next(nv, s);
     iota<uint32_t>(clusters.data(), nv, 0u, s);
+    sweep_plan plan;
+    plan_sweeps(S, cur, off.data(), k.data(), plan);
     double new_q = modularity(S, cur, clusters.data(), a.data(), present.data());
     lap("setup", nv, cur.ne, new_q);
     double cur_q = new_q - 1.0;
     bool up_down = true;
     while (new_q > cur_q + 0.0001) {
       cur_q = new_q;
-      sweep(S, cur, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down);
+      sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down);
       std::swap(clusters, next);
       cluster_weights(S, cur, clusters.data(), k.data(), has_edges.data(), a.data(), present.data());
       up_down = !up_down;
@@ -925,12 +1617,14 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     fill<uint8_t>(present.data(), nv, 1, s);
     dbuf<uint32_t> clusters(nv, s), next(r1, s);
     iota<uint32_t>(clusters.data(), nv, 0u, s);
+    sweep_plan plan;
+    plan_sweeps(S, cur, off.data(), k.data(), plan);
     double new_q = modularity(S, cur, clusters.data(), a.data(), present.data());
     double cur_q = new_q - 1.0;
     bool up_down = true;
     while (new_q > cur_q + 0.0001) {
       cur_q = new_q;
-      sweep(S, cur, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down);
+      sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down);
       allgatherv_dense<uint32_t>(comm, next.data(), voff, clusters.data(), s);
       cluster_weights(S, cur, clusters.data(), k.data(), has_edges.data(), a.data(), present.data());
       up_down = !up_down;

@@ -144,3 +144,33 @@ def test_dendrogram_levels_compose_to_clusters():
         assert i == 0 or x.size == lv[i - 1].max() + 1
         flat = x[flat]
     assert np.array_equal(flat, host(c))
+
+
+@pytest.mark.parametrize("renumber,env", [(True, {}), (False, {}), (True, {"CGX_LOUVAIN_BIG": "sort"}),
+                                          (False, {"CGX_LOUVAIN_BIG_CAP": "16"})])
+def test_hash_sweep_equals_sort_sweep(renumber, env, monkeypatch):
+    """The LDS-hash local move (louvain.hip: k_sweep_hash for rows of <= 2048 edges,
+    k_big_partials / k_big_buckets / k_big_move for heavier rows; fixed-point pair
+    sums) against the sort + reduce_by_key local move (CGX_LOUVAIN_HASH=0) on
+    RMAT-16 with integer weights: every sum is exact in both, so the clustering,
+    modularity and level count are identical.  Variants: heavy rows on the sort
+    path inside the hash schedule (not a prefix of the rows without renumbering:
+    gathered COO), and a (row, bucket) table cap of 16 that overflows, so the level
+    falls back to the sort path for its heavy rows mid-sweep."""
+    s, d = rmat.rmat(16, 16 << 16, seed=11)
+    w = np.floor(rmat.rmat_weights(s.size, seed=12).astype(np.float64) * 8.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    deg = np.bincount(s)
+    assert deg.max() > 2048 and deg[0] <= 2048  # hub rows exist, and row 0 is not one
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    h, G = make_graph(s, d, w, renumber=renumber, symmetric=True)
+    v, c, q = run(h, G)
+    lv = h.last_louvain_levels()
+    for k in env:
+        monkeypatch.delenv(k)
+    monkeypatch.setenv("CGX_LOUVAIN_HASH", "0")
+    h2, G2 = make_graph(s, d, w, renumber=renumber, symmetric=True)
+    v2, c2, q2 = run(h2, G2)
+    assert np.array_equal(v, v2) and np.array_equal(c, c2)
+    assert q == q2 and lv == h2.last_louvain_levels()
