@@ -31,6 +31,7 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -317,12 +318,12 @@ __global__ void k_to_vertex(uint32_t const* x, int64_t n, V* out)
 // order-independent, and exact for integer weights, so the gains are the same IEEE
 // values as the sort path's and the oracle's.  Replaces key build + radix sort +
 // two reduce_by_key passes (~20 B of HBM traffic per edge per pass) by one pass
-// over the edges.
-constexpr int kHashEdges   = 2048;
-constexpr int kHashRows    = 512;
-constexpr int kHashSlots   = 4096;
-constexpr int kHashThreads = 512;
-constexpr u64 kEmptyKey    = ~0ull;
+// over the edges.  Small blocks (256 threads, ~34 KB of LDS with 32-bit pair keys:
+// 4 per CU) so that one block's gathers overlap another's LDS phases.
+constexpr int kHashEdges   = 1024;
+constexpr int kHashRows    = 256;
+constexpr int kHashSlots   = 2048;
+constexpr int kHashThreads = 256;
 
 struct hash_sweep_args {
   uint32_t const* src;
@@ -341,7 +342,27 @@ struct hash_sweep_args {
   bool up_down;
 };
 
-__device__ inline unsigned pair_slot(u64 key, int bits) { return (unsigned)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits)); }
+// (row in chunk, neighbour cluster) keys: 8 + 24 bits when the level has < 2^24 - 1
+// ids (never the all-ones empty key), else 32 + 32
+template <typename K>
+struct pair_key;
+template <>
+struct pair_key<uint32_t> {
+  static constexpr uint32_t empty = ~0u;
+  __device__ static uint32_t make(int i, uint32_t c) { return ((uint32_t)i << 24) | c; }
+  __device__ static int row(uint32_t k) { return (int)(k >> 24); }
+  __device__ static uint32_t cluster(uint32_t k) { return k & 0xffffffu; }
+  __device__ static unsigned slot(uint32_t k, int bits) { return (k * 0x9E3779B1u) >> (32 - bits); }
+};
+template <>
+struct pair_key<u64> {
+  static constexpr u64 empty = ~0ull;
+  __device__ static u64 make(int i, uint32_t c) { return ((u64)i << 32) | c; }
+  __device__ static int row(u64 k) { return (int)(k >> 32); }
+  __device__ static uint32_t cluster(u64 k) { return (uint32_t)k; }
+  __device__ static unsigned slot(u64 k, int bits) { return (unsigned)((k * 0x9E3779B97F4A7C15ull) >> (64 - bits)); }
+};
+
 // monotone map double -> u64 (larger gain -> larger key)
 __device__ inline u64 order_bits(double d)
 {
@@ -353,39 +374,51 @@ __device__ inline double unorder_bits(u64 o)
   return __longlong_as_double((long long)((o >> 63) ? (o & 0x7fffffffffffffffull) : ~o));
 }
 
+template <typename K>
 __global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
 {
 #pragma clang fp contract(off)
-  __shared__ u64 key[kHashSlots];
+  using PK = pair_key<K>;
+  __shared__ K key[kHashSlots];
   __shared__ u64 val[kHashSlots];
-  __shared__ double old_s[kHashRows];
-  __shared__ u64 best[kHashRows];
-  __shared__ uint32_t bestc[kHashRows];
-  int const tid = threadIdx.x;
+  __shared__ uint32_t r_cu[kHashRows], r_bc[kHashRows];
+  __shared__ double r_k[kHashRows], r_aold[kHashRows], r_old[kHashRows];
+  __shared__ u64 r_best[kHashRows];
+  int const tid    = threadIdx.x;
   int64_t const r0 = p.chunks[2 * blockIdx.x], r1 = p.chunks[2 * blockIdx.x + 1];
   int const nrow   = (int)(r1 - r0);
   int64_t const e0 = p.off[r0], e1 = p.off[r1];
   int bits         = 6;  // table of 2^bits >= 2 * edges slots
   while ((1 << bits) < 2 * (int)(e1 - e0)) ++bits;
-  int const nslot = 1 << bits;
+  int const nslot     = 1 << bits;
   unsigned const mask = (unsigned)nslot - 1;
   for (int i = tid; i < nslot; i += kHashThreads) {
-    key[i] = kEmptyKey;
+    key[i] = PK::empty;
     val[i] = 0;
   }
-  for (int i = tid; i < nrow; i += kHashThreads) {
-    old_s[i] = 0.0;
-    best[i]  = 0;
-    bestc[i] = 0xffffffffu;
+  // thread t owns row t of the chunk
+  bool const has_row = tid < nrow;
+  int64_t const u    = r0 + tid;
+  uint32_t cu        = 0;
+  double self        = 0.0;
+  if (has_row) {
+    cu           = p.c[u + p.base];
+    self         = p.self[u];
+    r_cu[tid]    = cu;
+    r_k[tid]     = p.k[u];
+    r_aold[tid]  = p.a[cu];
+    r_old[tid]   = 0.0;
+    r_best[tid]  = 0;
+    r_bc[tid]    = 0xffffffffu;
   }
   __syncthreads();
   for (int64_t e = e0 + tid; e < e1; e += kHashThreads) {
-    u64 const kk = ((u64)(p.src[e] - (uint32_t)r0) << 32) | p.c[p.dst[e]];
-    u64 const v  = (u64)__double2ll_rn(p.w[e] * p.scale);
-    unsigned h   = pair_slot(kk, bits);
+    K const kk  = PK::make((int)(p.src[e] - (uint32_t)r0), p.c[p.dst[e]]);
+    u64 const v = (u64)__double2ll_rn(p.w[e] * p.scale);
+    unsigned h  = PK::slot(kk, bits);
     while (true) {
-      u64 const prev = atomicCAS(&key[h], kEmptyKey, kk);
-      if (prev == kEmptyKey || prev == kk) {
+      K const prev = atomicCAS(&key[h], PK::empty, kk);
+      if (prev == PK::empty || prev == kk) {
         atomicAdd(&val[h], v);
         break;
       }
@@ -394,52 +427,47 @@ __global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
   }
   __syncthreads();
   // weight into the own cluster, self loop excluded (k_old_sum)
-  for (int i = tid; i < nrow; i += kHashThreads) {
-    int64_t const u = r0 + i;
-    u64 const kk    = ((u64)i << 32) | p.c[u + p.base];
-    unsigned h      = pair_slot(kk, bits);
-    while (key[h] != kEmptyKey) {
+  if (has_row) {
+    K const kk = PK::make(tid, cu);
+    unsigned h = PK::slot(kk, bits);
+    while (key[h] != PK::empty) {
       if (key[h] == kk) {
-        old_s[i] = (double)(long long)val[h] * p.inv_scale - p.self[u];
+        r_old[tid] = (double)(long long)val[h] * p.inv_scale - self;
         break;
       }
       h = (h + 1) & mask;
     }
   }
   __syncthreads();
-  // gains (k_gain), per-row maximum
+  // gains (k_gain), per-row maximum.  For the own cluster s = sum - self = old_s,
+  // the same IEEE value as k_gain's.
   for (int h = tid; h < nslot; h += kHashThreads) {
-    u64 const kk = key[h];
-    if (kk == kEmptyKey) continue;
-    int const i       = (int)(kk >> 32);
-    uint32_t const cc = (uint32_t)kk;
-    int64_t const u   = r0 + i;
-    uint32_t const cu = p.c[u + p.base];
-    double s          = (double)(long long)val[h] * p.inv_scale;
-    if (cc == cu) s = s - p.self[u];
-    double a_new = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
-    double a_old = p.a[cu];
-    double kv    = p.k[u];
-    double dq    = 2.0 * (((s - old_s[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
-    u64 const o  = order_bits(dq);
-    val[h]       = o;
-    atomicMax(&best[i], o);
+    K const kk = key[h];
+    if (kk == PK::empty) continue;
+    int const i       = PK::row(kk);
+    uint32_t const cc = PK::cluster(kk);
+    double s          = cc == r_cu[i] ? r_old[i] : (double)(long long)val[h] * p.inv_scale;
+    double a_new      = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
+    double a_old      = r_aold[i];
+    double kv         = r_k[i];
+    double dq = 2.0 * (((s - r_old[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+    u64 const o = order_bits(dq);
+    val[h]      = o;
+    atomicMax(&r_best[i], o);
   }
   __syncthreads();
   // ties: the smaller cluster (best_gain_op)
   for (int h = tid; h < nslot; h += kHashThreads) {
-    u64 const kk = key[h];
-    if (kk == kEmptyKey) continue;
-    int const i = (int)(kk >> 32);
-    if (val[h] == best[i]) atomicMin(&bestc[i], (uint32_t)kk);
+    K const kk = key[h];
+    if (kk == PK::empty) continue;
+    int const i = PK::row(kk);
+    if (val[h] == r_best[i]) atomicMin(&r_bc[i], PK::cluster(kk));
   }
   __syncthreads();
-  for (int i = tid; i < nrow; i += kHashThreads) {
-    if (best[i] == 0) continue;  // no edges
-    int64_t const u = r0 + i;
-    double const dq = unorder_bits(best[i]);
-    uint32_t const b = bestc[i];
-    if (dq > 0.0 && ((b > p.c[u + p.base]) == p.up_down)) p.next[u] = b;
+  if (has_row && r_best[tid] != 0) {
+    double const dq  = unorder_bits(r_best[tid]);
+    uint32_t const b = r_bc[tid];
+    if (dq > 0.0 && ((b > cu) == p.up_down)) p.next[u] = b;
   }
 }
 
@@ -502,12 +530,12 @@ __global__ void k_gather_rows(int64_t const* first, int64_t const* pos, int64_t 
 //  C. one thread per row: best over the buckets -> move.
 // A bucket whose distinct clusters exceed the table's cap raises a flag and the
 // level falls back to the sort path for its heavy rows (never seen on RMAT).
-constexpr int kBigSeg        = 4096;
-constexpr int kBigSlots      = 8192;
-constexpr int kBigThreads    = 1024;
-constexpr int kBigMaxBuckets = 4096;
-constexpr int kBigPerBucket  = 1024;
-constexpr int kBigMaxSegs    = 2048;
+constexpr int kBigSeg        = 2048;
+constexpr int kBigSlots      = 4096;
+constexpr int kBigThreads    = 512;
+constexpr int kBigMaxBuckets = 1024;  // LDS of pass A: 52 KB -> 3 blocks per CU
+constexpr int kBigPerBucket  = 2048;
+constexpr int kBigMaxSegs    = 2048;  // rows of <= 4M edges (heavier: sort path)
 constexpr int kBktSlots      = 4096;
 constexpr int kBktThreads    = 512;
 constexpr int kBktCap        = 3072;  // < kBktSlots - kBktThreads: probing always ends
@@ -523,7 +551,8 @@ struct big_row {
   int64_t first;        // first edge
   uint32_t row, logb;   // row index, log2 of the bucket count
   uint32_t sbeg, send;  // segments
-  uint32_t bbeg, pad;   // first (row, bucket) block
+  uint32_t bbeg;        // first (row, bucket) block
+  uint32_t single;      // one segment: pass A moves the row itself
 };
 
 struct big_args {
@@ -600,17 +629,70 @@ __device__ uint32_t block_excl_scan(uint32_t* a, int n, uint32_t* wsum)
   return total;
 }
 
+// the block's LDS table holds every neighbour cluster of row rw.row: gains, best,
+// move (k_gain + best_gain_op + k_move for one row); bq / bc: LDS scratch
+__device__ void move_whole_row(big_args const& p, big_row const& rw, uint32_t const* key, u64* val, int nslot,
+                               unsigned bits, u64& bq, uint32_t& bc, double& old_sh)
+{
+#pragma clang fp contract(off)
+  int const tid      = threadIdx.x;
+  uint32_t const u   = rw.row;
+  uint32_t const cu  = p.c[u + p.base];
+  double const self  = p.self[u];
+  if (tid == 0) {
+    double o       = 0.0;
+    unsigned h     = slot32(cu, (int)bits);
+    while (key[h] != kEmpty32) {
+      if (key[h] == cu) {
+        o = (double)(long long)val[h] * p.inv_scale - self;
+        break;
+      }
+      h = (h + 1) & (unsigned)(nslot - 1);
+    }
+    old_sh = o;
+    bq     = 0;
+    bc     = kEmpty32;
+  }
+  __syncthreads();
+  double const kv = p.k[u], a_old = p.a[cu], old_s = old_sh;
+  for (int h = tid; h < nslot; h += blockDim.x) {
+    uint32_t const cc = key[h];
+    if (cc == kEmpty32) continue;
+    double s     = cc == cu ? old_s : (double)(long long)val[h] * p.inv_scale;
+    double a_new = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
+    double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+    u64 const o  = order_bits(dq);
+    val[h]       = o;
+    atomicMax(&bq, o);
+  }
+  __syncthreads();
+  for (int h = tid; h < nslot; h += blockDim.x)
+    if (key[h] != kEmpty32 && val[h] == bq) atomicMin(&bc, key[h]);
+  __syncthreads();
+  if (tid == 0 && bq != 0) {
+    double const dq = unorder_bits(bq);
+    if (dq > 0.0 && ((bc > cu) == p.up_down)) p.next[u] = bc;
+  }
+}
+
 __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
 {
   __shared__ uint32_t key[kBigSlots];
   __shared__ u64 val[kBigSlots];
   __shared__ uint32_t hist[kBigMaxBuckets];
   __shared__ uint32_t wsum[kBigThreads / 64 + 1];
+  __shared__ u64 bq;
+  __shared__ uint32_t bc;
+  __shared__ double old_sh;
   int const tid     = threadIdx.x;
   big_seg const sg  = p.segs[blockIdx.x];
   big_row const rw  = p.rows[sg.j];
   int const nbk     = 1 << rw.logb;
-  for (int i = tid; i < kBigSlots; i += kBigThreads) {
+  int bits          = 6;  // 2^bits >= 2 * edges slots
+  while ((1 << bits) < 2 * (int)(sg.e1 - sg.e0)) ++bits;
+  int const nslot     = 1 << bits;
+  unsigned const mask = (unsigned)nslot - 1;
+  for (int i = tid; i < nslot; i += kBigThreads) {
     key[i] = kEmpty32;
     val[i] = 0;
   }
@@ -619,19 +701,23 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
   for (int64_t e = sg.e0 + tid; e < sg.e1; e += kBigThreads) {
     uint32_t const cc = p.c[p.dst[e]];
     u64 const v       = (u64)__double2ll_rn(p.w[e] * p.scale);
-    unsigned h        = slot32(cc, 13);
+    unsigned h        = slot32(cc, bits);
     while (true) {
       uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
       if (prev == kEmpty32 || prev == cc) {
         atomicAdd(&val[h], v);
         break;
       }
-      h = (h + 1) & (kBigSlots - 1);
+      h = (h + 1) & mask;
     }
   }
   __syncthreads();
+  if (rw.single) {
+    move_whole_row(p, rw, key, val, nslot, (unsigned)bits, bq, bc, old_sh);
+    return;
+  }
   uint32_t const cu = p.c[rw.row + p.base];
-  for (int i = tid; i < kBigSlots; i += kBigThreads) {
+  for (int i = tid; i < nslot; i += kBigThreads) {
     uint32_t const cc = key[i];
     if (cc == kEmpty32) continue;
     if (cc == cu) atomicAdd(&p.own[sg.j], val[i]);
@@ -642,7 +728,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
   for (int b = tid; b < nbk; b += kBigThreads) p.boffs[sg.boff + b] = (int32_t)hist[b];
   if (tid == 0) p.boffs[sg.boff + nbk] = (int32_t)total;
   __syncthreads();
-  for (int i = tid; i < kBigSlots; i += kBigThreads) {
+  for (int i = tid; i < nslot; i += kBigThreads) {
     uint32_t const cc = key[i];
     if (cc == kEmpty32) continue;
     uint32_t const pos     = atomicAdd(&hist[bucket_of(cc, rw.logb)], 1u);
@@ -674,10 +760,6 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
     pre[i]           = (uint32_t)(hi - lo);
     start[i]         = sg.pbase + lo;
   }
-  for (int i = tid; i < kBktSlots; i += kBktThreads) {
-    key[i] = kEmpty32;
-    val[i] = 0;
-  }
   if (tid == 0) {
     distinct = 0;
     over     = 0;
@@ -686,6 +768,16 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
   }
   __syncthreads();
   uint32_t const total = block_excl_scan<kBktThreads, kBigMaxSegs / kBktThreads>(pre, ns, wsum);
+  int bits             = 6;  // 2^bits >= 2 * partials slots, at most kBktSlots (then the cap guards)
+  while ((1 << bits) < kBktSlots && (1u << bits) < 2 * total) ++bits;
+  int const nslot     = 1 << bits;
+  unsigned const mask = (unsigned)nslot - 1;
+  int const cap       = p.cap;  // below kBktSlots slots total <= nslot / 2: never full
+  for (int i = tid; i < nslot; i += kBktThreads) {
+    key[i] = kEmpty32;
+    val[i] = 0;
+  }
+  __syncthreads();
   for (uint32_t f = tid; f < total; f += kBktThreads) {
     int lo = 0, hi = ns - 1;  // last segment with pre <= f
     while (lo < hi) {
@@ -696,19 +788,19 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
     int64_t const x   = start[lo] + (f - pre[lo]);
     uint32_t const cc = p.pkey[x];
     u64 const v       = p.pval[x];
-    unsigned h        = slot32(cc, 12);
+    unsigned h        = slot32(cc, bits);
     bool stop         = false;
     while (true) {
       uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
       if (prev == kEmpty32 || prev == cc) {
         atomicAdd(&val[h], v);
-        if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= p.cap) {
+        if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= cap) {
           over = 1;
           stop = true;
         }
         break;
       }
-      h = (h + 1) & (kBktSlots - 1);
+      h = (h + 1) & mask;
     }
     if (stop) break;
   }
@@ -721,7 +813,7 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
   uint32_t const cu = p.c[u + p.base];
   double const kv   = p.k[u], a_old = p.a[cu], self = p.self[u];
   double const old_s = (double)(long long)p.own[j] * p.inv_scale - self;
-  for (int h = tid; h < kBktSlots; h += kBktThreads) {
+  for (int h = tid; h < nslot; h += kBktThreads) {
     uint32_t const cc = key[h];
     if (cc == kEmpty32) continue;
     double s = (double)(long long)val[h] * p.inv_scale;
@@ -733,7 +825,7 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
     atomicMax(&bq, o);
   }
   __syncthreads();
-  for (int h = tid; h < kBktSlots; h += kBktThreads)
+  for (int h = tid; h < nslot; h += kBktThreads)
     if (key[h] != kEmpty32 && val[h] == bq) atomicMin(&bc, key[h]);
   __syncthreads();
   if (tid == 0) {
@@ -747,6 +839,7 @@ __global__ void k_big_move(big_args p)
 {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < p.nrows; j += (int64_t)gridDim.x * blockDim.x) {
     big_row const rw = p.rows[j];
+    if (rw.single) continue;
     u64 best         = 0;
     uint32_t bc      = kEmpty32;
     for (uint32_t i = rw.bbeg; i < rw.bbeg + (1u << rw.logb); ++i) {
@@ -911,6 +1004,7 @@ struct sweep_plan {
   dbuf<u64> pval;
   dbuf<int32_t> boffs;
   dbuf<int> overflow;
+  std::vector<int64_t> big, big_first, big_deg;  // every heavy row (host)
 };
 
 inline bool hash_sweep_enabled()
@@ -941,18 +1035,28 @@ inline int ceil_log2(int64_t x)
   return l;
 }
 
-void plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh, std::vector<int64_t> const& big, sweep_plan& P)
+// the heavy rows the LDS passes take; returns the others (sort path)
+std::vector<int64_t> plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh, std::vector<int64_t> const& big,
+                                   sweep_plan& P)
 {
-  int64_t const nb = (int64_t)big.size();
-  std::vector<big_row> rows(nb);
+  std::vector<int64_t> rest;
+  std::vector<big_row> rows;
   std::vector<big_seg> segs;
   std::vector<u64> bb;
   int64_t pstart = 0, boff = 0;
-  for (int64_t j = 0; j < nb; ++j) {
-    int64_t const r = big[j], first = oh[r], d = oh[r + 1] - oh[r];
-    int64_t const nseg = (d + kBigSeg - 1) / kBigSeg;
-    if (nseg > kBigMaxSegs) return;  // > 8M edges in one row: sort path
-    int const logb = std::min(ceil_log2((d + kBigPerBucket - 1) / kBigPerBucket), ceil_log2(kBigMaxBuckets));
+  char const* md       = std::getenv("CGX_LOUVAIN_BIG_MAXDEG");  // tests: a lower limit
+  int64_t const maxdeg = std::min<int64_t>(md ? std::atoll(md) : INT64_MAX, (int64_t)kBigMaxBuckets * kBktCap * 4 / 5);
+  for (int64_t r : big) {
+    int64_t const first = oh[r], d = oh[r + 1] - oh[r];
+    int64_t const nseg  = (d + kBigSeg - 1) / kBigSeg;
+    if (nseg > kBigMaxSegs || d > maxdeg) {
+      rest.push_back(r);  // a bucket could outgrow its table
+      continue;
+    }
+    int64_t const j = (int64_t)rows.size();
+    rows.emplace_back();
+    bool const single = nseg == 1;
+    int const logb    = single ? 0 : std::min(ceil_log2((d + kBigPerBucket - 1) / kBigPerBucket), ceil_log2(kBigMaxBuckets));
     big_row& rw = rows[j];
     rw.first    = first;
     rw.row      = (uint32_t)r;
@@ -967,14 +1071,17 @@ void plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh, std::vector<in
       sg.boff  = boff;
       sg.j     = (uint32_t)j;
       sg.pad   = 0;
-      boff += (1 << logb) + 1;
+      if (!single) boff += (1 << logb) + 1;
       segs.push_back(sg);
     }
-    rw.send = (uint32_t)segs.size();
-    rw.pad  = 0;
-    for (int b = 0; b < (1 << logb); ++b) bb.push_back(((u64)j << 32) | (u64)b);
+    rw.send   = (uint32_t)segs.size();
+    rw.single = single ? 1u : 0u;
+    if (!single)
+      for (int b = 0; b < (1 << logb); ++b) bb.push_back(((u64)j << 32) | (u64)b);
     pstart += d;
   }
+  int64_t const nb = (int64_t)rows.size();
+  if (nb == 0) return rest;
   P.nbig     = nb;
   P.nsegs    = (int64_t)segs.size();
   P.nbblocks = (int64_t)bb.size();
@@ -993,6 +1100,44 @@ void plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh, std::vector<in
   P.overflow.resize(1, s);
   HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
   P.big_hash = true;
+  return rest;
+}
+
+// the edges of `rows` for the sort path: the level COO itself when they are a
+// prefix of the rows, else gathered
+void build_sort_coo(hipStream_t s, level_graph const& g, sweep_plan& P, std::vector<int64_t> const& rows)
+{
+  int64_t const nb = (int64_t)rows.size();
+  P.e_big          = 0;
+  if (nb == 0) return;
+  std::vector<int64_t> first(nb), pos(nb + 1, 0);
+  bool prefix = true;
+  for (int64_t j = 0; j < nb; ++j) {
+    size_t const q = (size_t)(std::lower_bound(P.big.begin(), P.big.end(), rows[j]) - P.big.begin());
+    first[j]       = P.big_first[q];
+    pos[j + 1]     = pos[j] + P.big_deg[q];
+    prefix         = prefix && rows[j] == j;
+  }
+  P.e_big = pos[nb];
+  if (prefix) {
+    P.bsrc = g.src.data();
+    P.bdst = g.dst.data();
+    P.bw   = g.w.data();
+    return;
+  }
+  dbuf<int64_t> fd(nb, s), pd(nb + 1, s);
+  to_device(fd.data(), first.data(), nb, s);
+  to_device(pd.data(), pos.data(), nb + 1, s);
+  P.gsrc.resize(P.e_big, s);
+  P.gdst.resize(P.e_big, s);
+  P.gw.resize(P.e_big, s);
+  hipLaunchKernelGGL(k_gather_rows, dim3(blocks(P.e_big)), dim3(kBlock), 0, s, fd.data(), pd.data(), nb, g.src.data(),
+                     g.dst.data(), g.w.data(), P.e_big, P.gsrc.data(), P.gdst.data(), P.gw.data());
+  CGX_LAUNCH_CHECK();
+  HIP_CHECK(hipStreamSynchronize(s));  // fd / pd go out of scope
+  P.bsrc = P.gsrc.data();
+  P.bdst = P.gdst.data();
+  P.bw   = P.gw.data();
 }
 
 void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, double const* k, sweep_plan& P)
@@ -1044,37 +1189,12 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, dou
     P.chunks.resize(ch.size(), s);
     to_device(P.chunks.data(), ch.data(), ch.size(), s);
   }
-  int64_t const nb = (int64_t)big.size();
-  if (nb && big_hash_enabled()) plan_big_rows(s, oh, big, P);
-  if (nb) {
-    bool const prefix = big.back() == nb - 1;
-    if (prefix) {
-      P.e_big = oh[nb];
-      P.bsrc  = g.src.data();
-      P.bdst  = g.dst.data();
-      P.bw    = g.w.data();
-    } else {
-      std::vector<int64_t> first(nb), pos(nb + 1, 0);
-      for (int64_t j = 0; j < nb; ++j) {
-        first[j]   = oh[big[j]];
-        pos[j + 1] = pos[j] + (oh[big[j] + 1] - oh[big[j]]);
-      }
-      P.e_big = pos[nb];
-      dbuf<int64_t> fd(nb, s), pd(nb + 1, s);
-      to_device(fd.data(), first.data(), nb, s);
-      to_device(pd.data(), pos.data(), nb + 1, s);
-      P.gsrc.resize(P.e_big, s);
-      P.gdst.resize(P.e_big, s);
-      P.gw.resize(P.e_big, s);
-      hipLaunchKernelGGL(k_gather_rows, dim3(blocks(P.e_big)), dim3(kBlock), 0, s, fd.data(), pd.data(), nb,
-                         g.src.data(), g.dst.data(), g.w.data(), P.e_big, P.gsrc.data(), P.gdst.data(), P.gw.data());
-      CGX_LAUNCH_CHECK();
-      HIP_CHECK(hipStreamSynchronize(s));  // fd / pd go out of scope
-      P.bsrc = P.gsrc.data();
-      P.bdst = P.gdst.data();
-      P.bw   = P.gw.data();
-    }
+  for (int64_t r : big) {
+    P.big_first.push_back(oh[r]);
+    P.big_deg.push_back(oh[r + 1] - oh[r]);
   }
+  P.big = big;
+  build_sort_coo(s, g, P, big_hash_enabled() ? plan_big_rows(s, oh, big, P) : big);
   P.off  = off;
   P.hash = true;
 }
@@ -1091,7 +1211,8 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     sweep_sorted(S, g, g.src.data(), g.dst.data(), g.w.data(), g.ne, c, next, k, self, a, present, up_down);
     return;
   }
-  if (P.e_big && P.big_hash) {
+  bool sorted_all = false;
+  if (P.big_hash) {
     big_args ba{g.dst.data(), g.w.data(), c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
                 P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, present, k, S.m, S.gamma,
                 P.scale, P.inv_scale, P.best_q.data(), P.best_c.data(), P.overflow.data(), big_bucket_cap(), next,
@@ -1100,22 +1221,29 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     fill<int>(P.overflow.data(), 1, 0, s);
     hipLaunchKernelGGL(k_big_partials, dim3((unsigned)P.nsegs), dim3(kBigThreads), 0, s, ba);
     CGX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_big_buckets, dim3((unsigned)P.nbblocks), dim3(kBktThreads), 0, s, ba);
+    if (P.nbblocks) hipLaunchKernelGGL(k_big_buckets, dim3((unsigned)P.nbblocks), dim3(kBktThreads), 0, s, ba);
     CGX_LAUNCH_CHECK();
     if (to_host_scalar(P.overflow.data(), s) == 0) {
       hipLaunchKernelGGL(k_big_move, dim3(blocks(P.nbig)), dim3(kBlock), 0, s, ba);
       CGX_LAUNCH_CHECK();
     } else {
       P.big_hash = false;  // a bucket outgrew its table: this level's heavy rows use the sort path
+      HIP_CHECK(hipMemcpyAsync(next, c + g.base, g.nrows * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      build_sort_coo(s, g, P, P.big);
       sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down);
+      sorted_all = true;
     }
-  } else if (P.e_big) {
-    sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down);
   }
+  if (P.e_big && !sorted_all)
+    sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down);
   if (P.nchunks) {
     hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), c, (uint32_t)g.base, self, a,
                        present, k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down};
-    hipLaunchKernelGGL(k_sweep_hash, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
+    static bool const wide = std::getenv("CGX_LOUVAIN_WIDE_KEYS") != nullptr;  // tests of the 64-bit keys
+    if (g.nv < (1 << 24) - 1 && !wide)
+      hipLaunchKernelGGL(k_sweep_hash<uint32_t>, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
+    else
+      hipLaunchKernelGGL(k_sweep_hash<u64>, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
     CGX_LAUNCH_CHECK();
   }
 }

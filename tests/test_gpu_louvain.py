@@ -147,7 +147,8 @@ def test_dendrogram_levels_compose_to_clusters():
 
 
 @pytest.mark.parametrize("renumber,env", [(True, {}), (False, {}), (True, {"CGX_LOUVAIN_BIG": "sort"}),
-                                          (False, {"CGX_LOUVAIN_BIG_CAP": "16"})])
+                                          (False, {"CGX_LOUVAIN_BIG_CAP": "16"}),
+                                          (False, {"CGX_LOUVAIN_BIG_MAXDEG": "3000"})])
 def test_hash_sweep_equals_sort_sweep(renumber, env, monkeypatch):
     """The LDS-hash local move (louvain.hip: k_sweep_hash for rows of <= 2048 edges,
     k_big_partials / k_big_buckets / k_big_move for heavier rows; fixed-point pair
@@ -156,7 +157,9 @@ def test_hash_sweep_equals_sort_sweep(renumber, env, monkeypatch):
     modularity and level count are identical.  Variants: heavy rows on the sort
     path inside the hash schedule (not a prefix of the rows without renumbering:
     gathered COO), and a (row, bucket) table cap of 16 that overflows, so the level
-    falls back to the sort path for its heavy rows mid-sweep."""
+    falls back to the sort path for its heavy rows mid-sweep, and rows above 3000
+    edges on the sort path beside the LDS passes (the > 2.5M-edge rule).  (The 64-bit pair
+    keys of levels with >= 2^24 - 1 ids: test_hash_sweep_wide_keys, own process.)"""
     s, d = rmat.rmat(16, 16 << 16, seed=11)
     w = np.floor(rmat.rmat_weights(s.size, seed=12).astype(np.float64) * 8.0) + 1.0
     s, d, w = og.symmetrize_dedup(s, d, w)
@@ -174,3 +177,31 @@ def test_hash_sweep_equals_sort_sweep(renumber, env, monkeypatch):
     v2, c2, q2 = run(h2, G2)
     assert np.array_equal(v, v2) and np.array_equal(c, c2)
     assert q == q2 and lv == h2.last_louvain_levels()
+
+
+def test_hash_sweep_wide_keys():
+    """k_sweep_hash<u64> (levels with >= 2^24 - 1 ids) forced on RMAT-14, in a child
+    process since the switch is read once: same clustering as the sort path."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys, numpy as np; sys.path[:0] = ['tests', '.', 'cugraph-forked_amd']\n"
+        "from gpu_util import make_graph, plc, host\n"
+        "from oracle import rmat, graph as og\n"
+        "s, d = rmat.rmat(14, 16 << 14, seed=5)\n"
+        "w = np.floor(rmat.rmat_weights(s.size, seed=6).astype(np.float64) * 8.0) + 1.0\n"
+        "s, d, w = og.symmetrize_dedup(s, d, w)\n"
+        "h, G = make_graph(s, d, w, renumber=True, symmetric=True)\n"
+        "v, c, q = plc().louvain(h, G, 100, 1.0, False)\n"
+        "np.save(sys.argv[1], host(c)); print(repr(q))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for mode, env in (("wide", {"CGX_LOUVAIN_WIDE_KEYS": "1"}), ("sort", {"CGX_LOUVAIN_HASH": "0"})):
+        f = f"/tmp/cgx_lv_{mode}_{os.getpid()}.npy"
+        r = subprocess.run([sys.executable, "-c", code, f], cwd=root, env={**os.environ, **env}, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[mode] = (np.load(f), float(r.stdout.strip().splitlines()[-1]))
+        os.remove(f)
+    assert np.array_equal(out["wide"][0], out["sort"][0]) and out["wide"][1] == out["sort"][1]
