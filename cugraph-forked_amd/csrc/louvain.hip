@@ -412,17 +412,38 @@ __global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
     r_bc[tid]    = 0xffffffffu;
   }
   __syncthreads();
-  for (int64_t e = e0 + tid; e < e1; e += kHashThreads) {
-    K const kk  = PK::make((int)(p.src[e] - (uint32_t)r0), p.c[p.dst[e]]);
-    u64 const v = (u64)__double2ll_rn(p.w[e] * p.scale);
-    unsigned h  = PK::slot(kk, bits);
-    while (true) {
-      K const prev = atomicCAS(&key[h], PK::empty, kk);
-      if (prev == PK::empty || prev == kk) {
-        atomicAdd(&val[h], v);
-        break;
+  {
+    // all of this thread's edges (<= kEPT) loaded, then their clusters, then the
+    // inserts: the gathers overlap instead of waiting behind each CAS loop
+    constexpr int kEPT = kHashEdges / kHashThreads;
+    uint32_t ri[kEPT], dv[kEPT];
+    double wv[kEPT];
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      int64_t const e = e0 + tid + q * kHashThreads;
+      if (e < e1) {
+        ri[q] = p.src[e] - (uint32_t)r0;
+        dv[q] = p.dst[e];
+        wv[q] = p.w[e];
       }
-      h = (h + 1) & mask;
+    }
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q)
+      if (e0 + tid + q * kHashThreads < e1) dv[q] = p.c[dv[q]];
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      if (e0 + tid + q * kHashThreads >= e1) break;
+      K const kk  = PK::make((int)ri[q], dv[q]);
+      u64 const v = (u64)__double2ll_rn(wv[q] * p.scale);
+      unsigned h  = PK::slot(kk, bits);
+      while (true) {
+        K const prev = atomicCAS(&key[h], PK::empty, kk);
+        if (prev == PK::empty || prev == kk) {
+          atomicAdd(&val[h], v);
+          break;
+        }
+        h = (h + 1) & mask;
+      }
     }
   }
   __syncthreads();
@@ -441,19 +462,37 @@ __global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
   __syncthreads();
   // gains (k_gain), per-row maximum.  For the own cluster s = sum - self = old_s,
   // the same IEEE value as k_gain's.
-  for (int h = tid; h < nslot; h += kHashThreads) {
-    K const kk = key[h];
-    if (kk == PK::empty) continue;
-    int const i       = PK::row(kk);
-    uint32_t const cc = PK::cluster(kk);
-    double s          = cc == r_cu[i] ? r_old[i] : (double)(long long)val[h] * p.inv_scale;
-    double a_new      = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
-    double a_old      = r_aold[i];
-    double kv         = r_k[i];
-    double dq = 2.0 * (((s - r_old[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
-    u64 const o = order_bits(dq);
-    val[h]      = o;
-    atomicMax(&r_best[i], o);
+  {
+    constexpr int kSPT = kHashSlots / kHashThreads;
+    double an[kSPT];
+    uint8_t pr[kSPT];
+#pragma unroll
+    for (int q = 0; q < kSPT; ++q) {  // the neighbour clusters' weights, all in flight
+      int const h = tid + q * kHashThreads;
+      K const kk  = h < nslot ? key[h] : PK::empty;
+      if (kk != PK::empty) {
+        uint32_t const cc = PK::cluster(kk);
+        pr[q]             = p.present[cc];
+        an[q]             = p.a[cc];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kSPT; ++q) {
+      int const h = tid + q * kHashThreads;
+      if (h >= nslot) break;
+      K const kk = key[h];
+      if (kk == PK::empty) continue;
+      int const i       = PK::row(kk);
+      uint32_t const cc = PK::cluster(kk);
+      double s          = cc == r_cu[i] ? r_old[i] : (double)(long long)val[h] * p.inv_scale;
+      double a_new      = pr[q] ? an[q] : (double)FLT_MAX;
+      double a_old      = r_aold[i];
+      double kv         = r_k[i];
+      double dq = 2.0 * (((s - r_old[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+      u64 const o = order_bits(dq);
+      val[h]      = o;
+      atomicMax(&r_best[i], o);
+    }
   }
   __syncthreads();
   // ties: the smaller cluster (best_gain_op)
@@ -629,6 +668,42 @@ __device__ uint32_t block_excl_scan(uint32_t* a, int n, uint32_t* wsum)
   return total;
 }
 
+// gains of one row's neighbour clusters key[0, nslot) (sums in val, replaced by the
+// ordered gains), the maximum into bq.  The clusters' weights are gathered for all
+// of a thread's slots before any of them is used.
+template <int T, int S>
+__device__ void gains_one_row(big_args const& p, uint32_t const* key, u64* val, int nslot, uint32_t cu, double old_s,
+                              double kv, double a_old, u64& bq)
+{
+#pragma clang fp contract(off)
+  constexpr int kSPT = S / T;
+  int const tid      = threadIdx.x;
+  double an[kSPT];
+  uint8_t pr[kSPT];
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q) {
+    int const h       = tid + q * T;
+    uint32_t const cc = h < nslot ? key[h] : kEmpty32;
+    if (cc != kEmpty32) {
+      pr[q] = p.present[cc];
+      an[q] = p.a[cc];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q) {
+    int const h = tid + q * T;
+    if (h >= nslot) break;
+    uint32_t const cc = key[h];
+    if (cc == kEmpty32) continue;
+    double s     = cc == cu ? old_s : (double)(long long)val[h] * p.inv_scale;
+    double a_new = pr[q] ? an[q] : (double)FLT_MAX;
+    double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+    u64 const o  = order_bits(dq);
+    val[h]       = o;
+    atomicMax(&bq, o);
+  }
+}
+
 // the block's LDS table holds every neighbour cluster of row rw.row: gains, best,
 // move (k_gain + best_gain_op + k_move for one row); bq / bc: LDS scratch
 __device__ void move_whole_row(big_args const& p, big_row const& rw, uint32_t const* key, u64* val, int nslot,
@@ -655,16 +730,7 @@ __device__ void move_whole_row(big_args const& p, big_row const& rw, uint32_t co
   }
   __syncthreads();
   double const kv = p.k[u], a_old = p.a[cu], old_s = old_sh;
-  for (int h = tid; h < nslot; h += blockDim.x) {
-    uint32_t const cc = key[h];
-    if (cc == kEmpty32) continue;
-    double s     = cc == cu ? old_s : (double)(long long)val[h] * p.inv_scale;
-    double a_new = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
-    double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
-    u64 const o  = order_bits(dq);
-    val[h]       = o;
-    atomicMax(&bq, o);
-  }
+  gains_one_row<kBigThreads, kBigSlots>(p, key, val, nslot, cu, old_s, kv, a_old, bq);
   __syncthreads();
   for (int h = tid; h < nslot; h += blockDim.x)
     if (key[h] != kEmpty32 && val[h] == bq) atomicMin(&bc, key[h]);
@@ -698,17 +764,35 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
   }
   for (int i = tid; i < nbk; i += kBigThreads) hist[i] = 0;
   __syncthreads();
-  for (int64_t e = sg.e0 + tid; e < sg.e1; e += kBigThreads) {
-    uint32_t const cc = p.c[p.dst[e]];
-    u64 const v       = (u64)__double2ll_rn(p.w[e] * p.scale);
-    unsigned h        = slot32(cc, bits);
-    while (true) {
-      uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
-      if (prev == kEmpty32 || prev == cc) {
-        atomicAdd(&val[h], v);
-        break;
+  {
+    constexpr int kEPT = kBigSeg / kBigThreads;
+    uint32_t dv[kEPT];
+    double wv[kEPT];
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      int64_t const e = sg.e0 + tid + q * kBigThreads;
+      if (e < sg.e1) {
+        dv[q] = p.dst[e];
+        wv[q] = p.w[e];
       }
-      h = (h + 1) & mask;
+    }
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q)
+      if (sg.e0 + tid + q * kBigThreads < sg.e1) dv[q] = p.c[dv[q]];
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      if (sg.e0 + tid + q * kBigThreads >= sg.e1) break;
+      uint32_t const cc = dv[q];
+      u64 const v       = (u64)__double2ll_rn(wv[q] * p.scale);
+      unsigned h        = slot32(cc, bits);
+      while (true) {
+        uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
+        if (prev == kEmpty32 || prev == cc) {
+          atomicAdd(&val[h], v);
+          break;
+        }
+        h = (h + 1) & mask;
+      }
     }
   }
   __syncthreads();
@@ -754,6 +838,11 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
   big_row const rw = p.rows[j];
   int const nbk    = 1 << rw.logb;
   int const ns     = (int)(rw.send - rw.sbeg);
+  // row data first: independent of the partials, in flight meanwhile
+  uint32_t const u  = rw.row;
+  uint32_t const cu = p.c[u + p.base];
+  double const kv   = p.k[u], a_old = p.a[cu], self = p.self[u];
+  double const old_s = (double)(long long)p.own[j] * p.inv_scale - self;
   for (int i = tid; i < ns; i += kBktThreads) {
     big_seg const sg = p.segs[rw.sbeg + i];
     int32_t const lo = p.boffs[sg.boff + b], hi = p.boffs[sg.boff + b + 1];
@@ -778,52 +867,50 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
     val[i] = 0;
   }
   __syncthreads();
-  for (uint32_t f = tid; f < total; f += kBktThreads) {
-    int lo = 0, hi = ns - 1;  // last segment with pre <= f
-    while (lo < hi) {
-      int const mid = (lo + hi + 1) >> 1;
-      if (pre[mid] <= f) lo = mid;
-      else hi = mid - 1;
-    }
-    int64_t const x   = start[lo] + (f - pre[lo]);
-    uint32_t const cc = p.pkey[x];
-    u64 const v       = p.pval[x];
-    unsigned h        = slot32(cc, bits);
-    bool stop         = false;
-    while (true) {
-      uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
-      if (prev == kEmpty32 || prev == cc) {
-        atomicAdd(&val[h], v);
-        if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= cap) {
-          over = 1;
-          stop = true;
-        }
-        break;
+  constexpr int kPPT = 4;  // partials per thread per batch, loaded before their inserts
+  bool stop          = false;
+  for (uint32_t f0 = 0; f0 < total && !stop; f0 += kPPT * kBktThreads) {
+    uint32_t kq[kPPT];
+    u64 vq[kPPT];
+#pragma unroll
+    for (int q = 0; q < kPPT; ++q) {
+      uint32_t const f = f0 + tid + q * kBktThreads;
+      if (f >= total) break;
+      int lo = 0, hi = ns - 1;  // last segment with pre <= f
+      while (lo < hi) {
+        int const mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= f) lo = mid;
+        else hi = mid - 1;
       }
-      h = (h + 1) & mask;
+      int64_t const x = start[lo] + (f - pre[lo]);
+      kq[q]           = p.pkey[x];
+      vq[q]           = p.pval[x];
     }
-    if (stop) break;
+#pragma unroll
+    for (int q = 0; q < kPPT; ++q) {
+      if (stop || f0 + tid + q * kBktThreads >= total) break;
+      uint32_t const cc = kq[q];
+      unsigned h        = slot32(cc, bits);
+      while (true) {
+        uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
+        if (prev == kEmpty32 || prev == cc) {
+          atomicAdd(&val[h], vq[q]);
+          if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= cap) {
+            over = 1;
+            stop = true;
+          }
+          break;
+        }
+        h = (h + 1) & mask;
+      }
+    }
   }
   __syncthreads();
   if (over) {
     if (tid == 0) atomicOr(p.overflow, 1);
     return;
   }
-  uint32_t const u  = rw.row;
-  uint32_t const cu = p.c[u + p.base];
-  double const kv   = p.k[u], a_old = p.a[cu], self = p.self[u];
-  double const old_s = (double)(long long)p.own[j] * p.inv_scale - self;
-  for (int h = tid; h < nslot; h += kBktThreads) {
-    uint32_t const cc = key[h];
-    if (cc == kEmpty32) continue;
-    double s = (double)(long long)val[h] * p.inv_scale;
-    if (cc == cu) s = s - self;
-    double a_new = p.present[cc] ? p.a[cc] : (double)FLT_MAX;
-    double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
-    u64 const o  = order_bits(dq);
-    val[h]       = o;
-    atomicMax(&bq, o);
-  }
+  gains_one_row<kBktThreads, kBktSlots>(p, key, val, nslot, cu, old_s, kv, a_old, bq);
   __syncthreads();
   for (int h = tid; h < nslot; h += kBktThreads)
     if (key[h] != kEmpty32 && val[h] == bq) atomicMin(&bc, key[h]);
