@@ -944,6 +944,71 @@ __global__ void k_big_move(big_args p)
   }
 }
 
+// Chunk schedule of a level (the host loop took 28 ms at RMAT-23 level 0): thread t
+// walks rows [256 t, 256 t + 256) greedily -- a chunk closes before the row that
+// would take it past kHashEdges edges; rows above kHashEdges are heavy rows.
+// Pass 0 counts chunks and heavy rows per thread, pass 1 writes them at the
+// scanned positions.  Chunks never cross a 256-row block (= kHashRows).
+__global__ void k_chunk_walk(int64_t const* off, int64_t nr, int pass, uint32_t* ccount, uint32_t* bcount,
+                             int64_t const* cpos, int64_t const* bpos, int64_t* chunks, int64_t* bigrows)
+{
+  int64_t const nblk = (nr + kHashRows - 1) / kHashRows;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nblk; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const rb = t * kHashRows, re = rb + kHashRows < nr ? rb + kHashRows : nr;
+    int64_t nc = 0, nb = 0, r0 = rb, ce = 0;
+    int64_t* co = pass ? chunks + 2 * cpos[t] : nullptr;
+    int64_t* bo = pass ? bigrows + bpos[t] : nullptr;
+    int64_t lo = off[rb];
+    for (int64_t r = rb; r < re; ++r) {
+      int64_t const hi = off[r + 1], d = hi - lo;
+      lo               = hi;
+      if (d > kHashEdges) {
+        if (ce > 0) {
+          if (pass) {
+            co[2 * nc]     = r0;
+            co[2 * nc + 1] = r;
+          }
+          ++nc;
+        }
+        if (pass) bo[nb] = r;
+        ++nb;
+        ce = 0;
+        r0 = r + 1;
+        continue;
+      }
+      if (ce + d > kHashEdges) {
+        if (pass) {
+          co[2 * nc]     = r0;
+          co[2 * nc + 1] = r;
+        }
+        ++nc;
+        ce = 0;
+        r0 = r;
+      }
+      ce += d;
+    }
+    if (ce > 0) {
+      if (pass) {
+        co[2 * nc]     = r0;
+        co[2 * nc + 1] = re;
+      }
+      ++nc;
+    }
+    if (!pass) {
+      ccount[t] = (uint32_t)nc;
+      bcount[t] = (uint32_t)nb;
+    }
+  }
+}
+
+__global__ void k_big_info(int64_t const* rows, int64_t const* off, int64_t n, int64_t* first, int64_t* deg)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    first[i] = off[rows[i]];
+    deg[i]   = off[rows[i] + 1] - first[i];
+  }
+}
+
 inline unsigned blocks(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 16384); }
 
 // ---------------------------------------------------------------- driver
@@ -1123,9 +1188,9 @@ inline int ceil_log2(int64_t x)
 }
 
 // the heavy rows the LDS passes take; returns the others (sort path)
-std::vector<int64_t> plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh, std::vector<int64_t> const& big,
-                                   sweep_plan& P)
+std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P)
 {
+  std::vector<int64_t> const& big = P.big;
   std::vector<int64_t> rest;
   std::vector<big_row> rows;
   std::vector<big_seg> segs;
@@ -1133,8 +1198,8 @@ std::vector<int64_t> plan_big_rows(hipStream_t s, std::vector<int64_t> const& oh
   int64_t pstart = 0, boff = 0;
   char const* md       = std::getenv("CGX_LOUVAIN_BIG_MAXDEG");  // tests: a lower limit
   int64_t const maxdeg = std::min<int64_t>(md ? std::atoll(md) : INT64_MAX, (int64_t)kBigMaxBuckets * kBktCap * 4 / 5);
-  for (int64_t r : big) {
-    int64_t const first = oh[r], d = oh[r + 1] - oh[r];
+  for (size_t q = 0; q < big.size(); ++q) {
+    int64_t const r = big[q], first = P.big_first[q], d = P.big_deg[q];
     int64_t const nseg  = (d + kBigSeg - 1) / kBigSeg;
     if (nseg > kBigMaxSegs || d > maxdeg) {
       rest.push_back(r);  // a bucket could outgrow its table
@@ -1246,42 +1311,32 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, dou
   P.scale     = std::ldexp(1.0, 61 - e);
   P.inv_scale = std::ldexp(1.0, e - 61);
 
-  auto oh = to_host(off, (size_t)nr + 1, s);
-  std::vector<int64_t> ch, big;
-  int64_t r0 = 0, ce = 0;
-  auto close = [&](int64_t r1) {
-    if (ce > 0) {
-      ch.push_back(r0);
-      ch.push_back(r1);
-    }
-    ce = 0;
-  };
-  for (int64_t r = 0; r < nr; ++r) {
-    int64_t const d = oh[r + 1] - oh[r];
-    if (d > kHashEdges) {
-      close(r);
-      big.push_back(r);
-      r0 = r + 1;
-      continue;
-    }
-    if (ce + d > kHashEdges || r - r0 == kHashRows) {
-      close(r);
-      r0 = r;
-    }
-    ce += d;
+  int64_t const nblk = (nr + kHashRows - 1) / kHashRows;
+  dbuf<uint32_t> cc(nblk, s), bc(nblk, s);
+  dbuf<int64_t> cp(nblk + 1, s), bp(nblk + 1, s);
+  unsigned const wg = grid_for(nblk, kBlock, 16384);
+  hipLaunchKernelGGL(k_chunk_walk, dim3(wg), dim3(kBlock), 0, s, off, nr, 0, cc.data(), bc.data(), nullptr, nullptr,
+                     nullptr, nullptr);
+  CGX_LAUNCH_CHECK();
+  exclusive_scan<uint32_t, int64_t>(cc.data(), cp.data(), (size_t)nblk, s);
+  exclusive_scan<uint32_t, int64_t>(bc.data(), bp.data(), (size_t)nblk, s);
+  int64_t const tc = to_host_scalar(cp.data() + nblk - 1, s) + to_host_scalar(cc.data() + nblk - 1, s);
+  int64_t const tb = to_host_scalar(bp.data() + nblk - 1, s) + to_host_scalar(bc.data() + nblk - 1, s);
+  P.nchunks        = tc;
+  P.chunks.resize(std::max<int64_t>(2 * tc, 1), s);
+  dbuf<int64_t> bigd(std::max<int64_t>(tb, 1), s);
+  hipLaunchKernelGGL(k_chunk_walk, dim3(wg), dim3(kBlock), 0, s, off, nr, 1, cc.data(), bc.data(), cp.data(), bp.data(),
+                     P.chunks.data(), bigd.data());
+  CGX_LAUNCH_CHECK();
+  if (tb) {
+    dbuf<int64_t> fd(tb, s), dd(tb, s);
+    hipLaunchKernelGGL(k_big_info, dim3(blocks(tb)), dim3(kBlock), 0, s, bigd.data(), off, tb, fd.data(), dd.data());
+    CGX_LAUNCH_CHECK();
+    P.big       = to_host(bigd.data(), (size_t)tb, s);
+    P.big_first = to_host(fd.data(), (size_t)tb, s);
+    P.big_deg   = to_host(dd.data(), (size_t)tb, s);
   }
-  close(nr);
-  P.nchunks = (int64_t)ch.size() / 2;
-  if (P.nchunks) {
-    P.chunks.resize(ch.size(), s);
-    to_device(P.chunks.data(), ch.data(), ch.size(), s);
-  }
-  for (int64_t r : big) {
-    P.big_first.push_back(oh[r]);
-    P.big_deg.push_back(oh[r + 1] - oh[r]);
-  }
-  P.big = big;
-  build_sort_coo(s, g, P, big_hash_enabled() ? plan_big_rows(s, oh, big, P) : big);
+  build_sort_coo(s, g, P, big_hash_enabled() ? plan_big_rows(s, P) : P.big);
   P.off  = off;
   P.hash = true;
 }
