@@ -125,3 +125,55 @@ def test_bfs_rmat24_all_bench_roots():
     del g, off, idx
     torch.cuda.synchronize()
     p.trim_device_cache()
+
+
+def test_louvain_bench_graph_modularity():
+    """Louvain on the bench graph (RMAT-23, fp32 [0,1) weights, bench.py louvain_leg):
+    the reported Q is the modularity of the returned partition, recomputed on the
+    device in fp64 from the library's own adjacency (compute_modularity,
+    common_methods.cuh:121-170): internal weight / m - sum_c a_c^2 / m^2."""
+    import torch
+    bench, p = _bench()
+    h = p.ResourceHandle()
+    g, _, _ = bench.build_rmat_graph(p, h, 23, weighted=True, transposed=False)
+    v, c, q = p.louvain(h, g, 100, 1.0, False)
+    off, idx, w = g.adjacency(h, transposed=False)
+    V = off.numel() - 1
+    c = c.to(torch.int64)
+    deg = (off[1:] - off[:-1]).to(torch.int64)
+    rows = torch.repeat_interleave(torch.arange(V, device=off.device), deg)
+    w64 = w.to(torch.float64)
+    m = w64.sum()
+    internal = torch.where(c[rows] == c[idx.to(torch.int64)], w64, torch.zeros_like(w64)).sum()
+    k = torch.zeros(V, dtype=torch.float64, device=off.device).index_add_(0, rows, w64)
+    a = torch.zeros(int(c.max()) + 1, dtype=torch.float64, device=off.device).index_add_(0, c, k)
+    Q = float(internal / m - (a * a).sum() / (m * m))
+    print(f"RMAT-23 Louvain: Q reported {q:.12f} recomputed {Q:.12f}, levels {h.last_louvain_levels()}, "
+          f"clusters {int(torch.unique(c).numel())}")
+    assert abs(Q - q) <= 1e-9 * abs(q)
+    assert q > 0.05
+    del g, off, idx, w, rows, w64
+    torch.cuda.synchronize()
+    p.trim_device_cache()
+
+
+def test_louvain_hash_equals_sort_rmat20(monkeypatch):
+    """RMAT-20 with integer weights: the LDS-hash local move (multi-segment heavy
+    rows, many buckets per row) and the sort local move give the same clustering."""
+    import torch
+    bench, p = _bench()
+    h = p.ResourceHandle()
+    n = 16 << 20
+    s, d = p.generators.generate_rmat_edgelist(h, 20, n, 0.57, 0.19, 0.19, 7, False, True)
+    w = torch.floor(p.generators.generate_edge_weights(h, n, 8) * 8.0) + 1.0
+    s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
+    props = p.GraphProperties(is_symmetric=True, is_multigraph=False)
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CGX_LOUVAIN_HASH", mode)
+        g = p.SGGraph(h, props, s, d, w, store_transposed=False, renumber=True)
+        v, c, q = p.louvain(h, g, 100, 1.0, False)
+        out.append((v.cpu().numpy(), c.cpu().numpy(), q, h.last_louvain_levels()))
+        del g
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] and out[0][3] == out[1][3]
