@@ -113,6 +113,7 @@ struct pr_push_t {
   int64_t nitems = 0;
   int64_t nwin   = 0;
   buffer tile_ctr;     // uint32 queue heads (128 B apart); zero between iterations
+  int64_t src_head = -1;  // source partition over the XCDs: head size (-1: not partitioned)
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

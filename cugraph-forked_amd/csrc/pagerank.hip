@@ -863,10 +863,191 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
   }
 }
 
+// ---- source partition over the XCDs (opt-in, see srcpart_enabled): entries of the 2^16..2^21
+// highest-ranked sources (the head; RMAT: most entries, ~2 MB of x~) are dealt to
+// any XCD, the tail sources are cut into 8 equal id ranges and range k's entries of
+// every window go to XCD k's queue -- each XCD's L2 then holds the head plus 1/8 of
+// the tail's x~ (offline LRU model, RMAT-24 / 8K windows: 12.9M -> 0.4M L2 misses
+// per iteration).
+constexpr int kSrcBinBits = 14;  // cut granularity: 16K sources
+constexpr int kSrcParts   = kQueues;
+
+// entries per 2^kSrcBinBits-source bin: thread per (window, bin), two binary searches
+__global__ void k_src_bin_counts(uint64_t const* keys, int64_t const* ws, int64_t nwin, int64_t nbins,
+                                 unsigned long long* cnt)
+{
+  int64_t const n = nwin * nbins;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const w = i / nbins, b = i % nbins;
+    int64_t const a = ws[w], e = ws[w + 1];
+    if (a == e) continue;
+    auto lb = [&](uint64_t key) {
+      int64_t lo = a, hi = e;
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < key) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
+    uint64_t const wk = (uint64_t)w << 32;
+    int64_t const c   = lb(wk | (uint64_t)((b + 1) << kSrcBinBits)) - lb(wk | (uint64_t)(b << kSrcBinBits));
+    if (c) atomicAdd(cnt + b, (unsigned long long)c);
+  }
+}
+
+// first position (entry stream; packed: the first jump of that entry) of every
+// window's first entry with source >= cut[c]; -1 when that is the window's start or end
+__global__ void k_src_cut_positions(uint64_t const* keys, int64_t const* ws, int64_t nwin, int64_t const* cut, int ncut,
+                                    unsigned long long const* cm, int64_t* pos)
+{
+  int64_t const n = nwin * ncut;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const w = i / ncut;
+    int64_t const a = ws[w], e = ws[w + 1];
+    uint64_t const key = ((uint64_t)w << 32) | (uint64_t)cut[i % ncut];
+    int64_t lo = a, hi = e;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    pos[i] = (lo == a || lo == e) ? -1 : (cm ? lo + (int64_t)cm[lo - 1] : lo);
+  }
+}
+
+__global__ void k_mark_positions(int64_t const* pos, int64_t n, uint32_t* flag)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (pos[i] >= 0) flag[pos[i]] = 1u;
+}
+
+// Off by default: measured on RMAT-24 it cut the push's FETCH_SIZE from 2.05 to
+// 1.44 GB per launch (L2 hits 11.7M -> 25.5M) but raised WRITE_SIZE from 174 to
+// 320 MB -- every window is flushed by ~9 items instead of ~1, each a near-full
+// 8K-slot set of global 64-bit atomics -- and the iteration went from 0.815 to
+// 0.866 ms (RMAT-22: 0.190 -> 0.313).  CGX_PR_SRCPART=1 turns it on (A/B, tests).
+inline bool srcpart_enabled()
+{
+  char const* e = std::getenv("CGX_PR_SRCPART");
+  return e && e[0] == '1';
+}
+
+// Head size and tail cuts from the per-bin entry counts: the smallest head (2^16 ..
+// 2^21 sources) for which no tail range holds more than 1/8 of the entries, so the
+// head items can level the queues.  Empty: no partition.
+inline std::vector<int64_t> plan_source_cuts(std::vector<unsigned long long> const& bins, int64_t n_cols, int64_t ne)
+{
+  std::vector<int64_t> none;
+  int64_t const nb = (int64_t)bins.size();
+  if (!srcpart_enabled() || n_cols < (int64_t)kSrcParts << (kSrcBinBits + 2)) return none;
+  std::vector<int64_t> pre(nb + 1, 0);
+  for (int64_t b = 0; b < nb; ++b) pre[b + 1] = pre[b] + (int64_t)bins[b];
+  for (int hb = 16; hb <= 21; ++hb) {
+    int64_t const H  = (int64_t)1 << hb;
+    int64_t const h0 = H >> kSrcBinBits;
+    if (h0 + kSrcParts > nb) break;
+    std::vector<int64_t> cut{H};
+    int64_t worst = 0;
+    int64_t prev  = h0;
+    for (int k = 1; k <= kSrcParts; ++k) {
+      int64_t const bk = k == kSrcParts ? nb : h0 + (nb - h0) * k / kSrcParts;
+      worst            = std::max(worst, pre[bk] - pre[prev]);
+      if (k < kSrcParts) cut.push_back(bk << kSrcBinBits);
+      prev = bk;
+    }
+    if (worst * kSrcParts <= ne * 49 / 50) return cut;  // 2 % slack for the head to level
+  }
+  return none;
+}
+
+inline void upload_items(hipStream_t s, pr_push_t& pp, std::vector<int64_t> const& item_u,
+                         std::vector<int64_t> const& queue, int64_t nitems)
+{
+  pp.items.set_stream(s);
+  pp.items.resize(item_u.size() * sizeof(int64_t));
+  to_device(pp.items.data<int64_t>(), item_u.data(), item_u.size(), s);
+  pp.queue.set_stream(s);
+  pp.queue.resize(std::max<size_t>(queue.size(), 1) * sizeof(int64_t));
+  to_device(pp.queue.data<int64_t>(), queue.data(), queue.size(), s);
+  pp.nitems = nitems;
+}
+
+// Source-partitioned items: a unit's part is the number of its window's cut
+// positions at or before it (0 = head, k + 1 = tail range k); an item is a run of a
+// window's units of one part, split in shares of about tg entries.  Tail items go to
+// queue k, head items (in window order) to the least-loaded queue.
+inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit const* units, int64_t nunits, int64_t ne,
+                                std::vector<int64_t> const& cutpos, int ncut)
+{
+  auto hu           = to_host(units, nunits, s);
+  int64_t const tg  = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * 4));
+  auto part_of      = [&](int64_t u) {
+    int p = 0;
+    for (int c = 0; c < ncut; ++c) {
+      int64_t const q = cutpos[hu[u].win * ncut + c];
+      if (q >= 0 && q <= hu[u].k0) p = c + 1;
+    }
+    return p;
+  };
+  std::vector<int64_t> item_u, item_e;
+  std::vector<int> item_p;
+  for (int64_t u0 = 0; u0 < nunits;) {
+    int const p0 = part_of(u0);
+    int64_t u1   = u0 + 1;
+    while (u1 < nunits && hu[u1].win == hu[u0].win && part_of(u1) == p0) ++u1;
+    int64_t const size = hu[u1 - 1].k1 - hu[u0].k0;
+    int64_t const n    = std::max<int64_t>(1, (size + tg / 2) / tg);
+    int64_t k          = 0;
+    for (int64_t u = u0; u < u1; ++u) {
+      int64_t const done = hu[u].k0 - hu[u0].k0;
+      if (u == u0 || (k < n && done * n >= k * size)) {
+        item_u.push_back(u);
+        item_e.push_back(0);
+        item_p.push_back(p0);
+        ++k;
+      }
+      item_e.back() += hu[u].k1 - hu[u].k0;
+    }
+    u0 = u1;
+  }
+  int64_t const nitems = (int64_t)item_u.size();
+  item_u.push_back(nunits);
+  std::vector<int> iq(nitems, 0);
+  int64_t load[kQueues] = {};
+  for (int64_t i = 0; i < nitems; ++i)
+    if (item_p[i] > 0) {
+      iq[i] = (item_p[i] - 1) % kQueues;
+      load[iq[i]] += item_e[i];
+    }
+  for (int64_t i = 0; i < nitems; ++i)
+    if (item_p[i] == 0) {
+      int best = 0;
+      for (int q = 1; q < kQueues; ++q)
+        if (load[q] < load[best]) best = q;
+      iq[i] = best;
+      load[best] += item_e[i];
+    }
+  std::vector<int64_t> queue;
+  queue.reserve(nitems);
+  for (int q = 0; q < kQueues; ++q) {
+    pp.qoff[q] = (int64_t)queue.size();
+    for (int64_t i = 0; i < nitems; ++i)
+      if (iq[i] == q) queue.push_back(i);
+  }
+  pp.qoff[kQueues] = (int64_t)queue.size();
+  upload_items(s, pp, item_u, queue, nitems);
+}
+
 // Items and queues over the units (host logic, once per graph)
-inline void build_items(hipStream_t s, pr_push_t& pp, push_unit const* units, int64_t nunits, bool xcd_queues_wanted)
+inline void build_items(hipStream_t s, pr_push_t& pp, push_unit const* units, int64_t nunits, bool xcd_queues_wanted,
+                        std::vector<int64_t> const& cutpos = {}, int ncut = 0)
 {
   int64_t const ne = nunits ? to_host(&units[nunits - 1].k1, 1, s)[0] : 0;
+  if (ncut > 0) {
+    build_items_srcpart(s, pp, units, nunits, ne, cutpos, ncut);
+    return;
+  }
   // Items and queues.  From 2^22 rows (8K windows): an item is a window's units,
   // or an equal share of a window of more than 1.5 tg entries; groups of
   // kGroupItems consecutive items are dealt to the 8 queues by longest-processing-
@@ -925,13 +1106,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit const* units, in
     for (int q = 1; q < kQueues; ++q) pp.qoff[q] = nitems;
   }
   pp.qoff[kQueues] = (int64_t)queue.size();
-  pp.items.set_stream(s);
-  pp.items.resize(item_u.size() * sizeof(int64_t));
-  to_device(pp.items.data<int64_t>(), item_u.data(), item_u.size(), s);
-  pp.queue.set_stream(s);
-  pp.queue.resize(std::max<size_t>(queue.size(), 1) * sizeof(int64_t));
-  to_device(pp.queue.data<int64_t>(), queue.data(), queue.size(), s);
-  pp.nitems = nitems;
+  upload_items(s, pp, item_u, queue, nitems);
 }
 
 // Push schedule of an edge list given as (row = destination, col = source) with
@@ -975,6 +1150,34 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
                      nwin, ws.data());
   CGX_LAUNCH_CHECK();
+  // source partition cuts (empty: window items only)
+  std::vector<int64_t> cuts;
+  pp.src_head = -1;
+  {
+    int64_t const nbins = (n_cols + (int64_t(1) << kSrcBinBits) - 1) >> kSrcBinBits;
+    if (n_cols >= (int64_t)kSrcParts << (kSrcBinBits + 2) && srcpart_enabled()) {
+      dbuf<unsigned long long> bc(nbins, s);
+      fill<unsigned long long>(bc.data(), nbins, 0ull, s);
+      hipLaunchKernelGGL(k_src_bin_counts, dim3(grid_for(nwin * nbins, kBlock, 16384)), dim3(kBlock), 0, s,
+                         keys_out.data(), ws.data(), nwin, nbins, bc.data());
+      CGX_LAUNCH_CHECK();
+      cuts = plan_source_cuts(to_host(bc.data(), nbins, s), n_cols, ne);
+      if (!cuts.empty()) pp.src_head = cuts[0];
+    }
+  }
+  int const ncut = (int)cuts.size();
+  dbuf<int64_t> cutd(std::max(ncut, 1), s), cutpos(std::max<int64_t>(nwin * ncut, 1), s);
+  if (ncut) to_device(cutd.data(), cuts.data(), ncut, s);
+  auto cut_positions = [&](unsigned long long const* cm, uint32_t* flag) {
+    if (!ncut) return std::vector<int64_t>{};
+    hipLaunchKernelGGL(k_src_cut_positions, dim3(grid_for(nwin * ncut, kBlock, 4096)), dim3(kBlock), 0, s,
+                       keys_out.data(), ws.data(), nwin, cutd.data(), ncut, cm, cutpos.data());
+    CGX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_mark_positions, dim3(grid_for(nwin * ncut, kBlock, 4096)), dim3(kBlock), 0, s, cutpos.data(),
+                       nwin * ncut, flag);
+    CGX_LAUNCH_CHECK();
+    return to_host(cutpos.data(), (size_t)(nwin * ncut), s);
+  };
   pp.packed = false;
   if (!w && packed_enabled()) {  // 16-bit entries unless the jumps would grow the entries by more than half
     uint32_t const dmax = (1u << (16 - wb)) - 2;  // coded deltas 0 .. dmax; dmax + 1 marks a jump
@@ -1005,6 +1208,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       hipLaunchKernelGGL(k_packed_mark_starts, dim3(grid_for(nwin, kBlock, 4096)), dim3(kBlock), 0, s, nws.data(),
                          nwin, total, pflag.data());
       CGX_LAUNCH_CHECK();
+      auto const cp = cut_positions(cm, pflag.data());
       fill<uint32_t>(pflag.data() + total, 1, 0u, s);
       exclusive_scan<uint32_t, uint32_t>(pflag.data(), puid.data(), total + 1, s);
       int64_t const nunits = (int64_t)to_host(puid.data() + total, 1, s)[0];
@@ -1024,7 +1228,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       CGX_LAUNCH_CHECK();
       pp.ent.release();
       pp.ew.release();
-      build_items(s, pp, units, nunits, wb == 13);
+      build_items(s, pp, units, nunits, wb == 13, cp, ncut);
       pp.nunits = nunits;
       HIP_CHECK(hipStreamSynchronize(s));
       return;
@@ -1034,6 +1238,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
                      ws.data(), sb, flag.data());
   CGX_LAUNCH_CHECK();
+  auto const cp = cut_positions(nullptr, flag.data());
   fill<uint32_t>(flag.data() + ne, 1, 0u, s);
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
   int64_t const nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
@@ -1059,7 +1264,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
                      w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
-  build_items(s, pp, units, nunits, wb == 13);
+  build_items(s, pp, units, nunits, wb == 13, cp, ncut);
   pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
 }

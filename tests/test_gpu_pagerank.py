@@ -211,3 +211,20 @@ def test_packed_entries_bitwise_equal_plain(scale, renumber, monkeypatch):
     r_plain = host(plc().pagerank(h2, G2, None, None, None, None, 0.85, 1e-6, 500, False)[1])
     assert h2.last_iterations() == it
     assert np.array_equal(r_packed, r_plain)
+
+
+@pytest.mark.parametrize("packed", ["1", "0"])
+def test_source_partition_bitwise_equal(packed, monkeypatch):
+    """The opt-in source partition of the push schedule (CGX_PR_SRCPART=1,
+    pagerank.hip build_items_srcpart: units cut at the head / tail source ranges,
+    tail range k on XCD queue k) adds the same fixed-point terms in another order:
+    the same bits as the window schedule, packed and 32-bit entries.  RMAT-20 has
+    enough sources (>= 2^19) for a partition."""
+    monkeypatch.setenv("CGX_PR_PACKED", packed)
+    s, d, _ = rmat_graph(20, False, True)
+    h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
+    r_win = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    monkeypatch.setenv("CGX_PR_SRCPART", "1")
+    h2, G2 = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
+    r_part = host(plc().pagerank(h2, G2, None, None, None, None, 0.85, 1e-6, 500, False)[1])
+    assert np.array_equal(r_win, r_part)
