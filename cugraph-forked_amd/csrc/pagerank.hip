@@ -408,6 +408,28 @@ __device__ __forceinline__ unsigned long long to_fixed(double v)
   return (unsigned long long)__double2ll_rn(v * kFixScale);
 }
 
+// The same value, round-to-nearest-even(x * 2^62), for an fp32 x in [0, 1) in fp32
+// arithmetic only: the fp64 sequence (cvt, 2 ldexp, rndne, floor, fma, 2 cvt) was
+// most of the push's VALU issue time (SQ_ACTIVE_INST_ANY at ~75 % of the waves'
+// cycles, RMAT-24).  y = x * 2^30 and its fraction are exact in fp32; the fraction's
+// significant bits then sit at 2^-32 .. 2^-62 of x, so rint(frac * 2^32) rounds
+// exactly where __double2ll_rn does and never reaches 2^32 (24-bit significands).
+__device__ __forceinline__ unsigned long long to_fixed_f32(float x)
+{
+  float const y     = x * 1073741824.0f;  // 2^30
+  uint32_t const hi = (uint32_t)y;
+  float const fr    = y - (float)hi;
+  uint32_t const lo = (uint32_t)__builtin_rintf(fr * 4294967296.0f);  // 2^32
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+template <typename R>
+__device__ __forceinline__ unsigned long long fixed_of(R x)
+{
+  if constexpr (std::is_same<R, float>::value) return to_fixed_f32(x);
+  else return to_fixed((double)x);
+}
+
 // add the LDS window to the global accumulators and clear it
 template <int WB, typename V, typename E, typename R>
 __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win)
@@ -489,9 +511,11 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
 #pragma unroll
       for (int j = 0; j < kPerThread; ++j) {
-        double v = (double)xv[j];
-        if constexpr (WEIGHTED) v *= (double)w[j];
-        atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed(v));
+        if constexpr (WEIGHTED) {
+          atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed((double)xv[j] * (double)w[j]));
+        } else {
+          atomicAdd(&acc[ent[j] & (kWin - 1)], fixed_of(xv[j]));
+        }
       }
 #pragma unroll
       for (int j = 0; j < kPerThread; ++j) {
@@ -617,7 +641,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       for (int j = 0; j < kRows; ++j) ent_n[j] = nt_load(sa.ent16 + k0n + wave * kSegEntries + j * 64 + lane);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
 #pragma unroll
-      for (int j = 0; j < kRows; ++j) atomicAdd(&acc[slot[j]], to_fixed((double)xv[j]));
+      for (int j = 0; j < kRows; ++j) atomicAdd(&acc[slot[j]], fixed_of(xv[j]));
 #pragma unroll
       for (int j = 0; j < kRows; ++j) ent[j] = ent_n[j];
       n    = nn;
