@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
+#include <stdexcept>
 
 namespace cgx {
 
@@ -51,6 +52,17 @@ __global__ void k_publish_ctr(bfs_ctr const* ctr, bfs_ctr* host)
   if (i < (int)(sizeof(bfs_ctr) / 8))
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(host) + i, reinterpret_cast<unsigned long long const*>(ctr)[i],
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the level counters, then seq (the host's poll word, pad[0]) behind a system fence
+__global__ void k_publish_seq(bfs_ctr const* ctr, bfs_ctr* host, unsigned long long seq)
+{
+  if (threadIdx.x != 0) return;
+  unsigned long long const* c = reinterpret_cast<unsigned long long const*>(ctr);
+  unsigned long long* hp      = reinterpret_cast<unsigned long long*>(host);
+  for (int i = 0; i < 5; ++i) __hip_atomic_store(hp + i, c[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename V>
@@ -634,11 +646,33 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   a.items = dir_opt ? adj.items.data<work_item>() : nullptr;
 
   // A/B (CGX_BFS_PUBLISH_KERNEL=1): counters published by k_publish_ctr instead of a
-  // D2H copy -- RMAT-24 1.168 vs 1.172 ms per traversal over 3 pairs, within noise
-  bool const ctr_memcpy = std::getenv("CGX_BFS_PUBLISH_KERNEL") == nullptr;
+  // D2H copy, both with a stream synchronize -- RMAT-24 1.168 vs 1.172 ms per
+  // traversal over 3 pairs, within noise
+  bool const ctr_memcpy = std::getenv("CGX_BFS_PUBLISH_KERNEL") != nullptr;
+  // Default: k_publish_seq into the handle's coherent block and a host spin on its
+  // sequence word -- no hipStreamSynchronize per level (CGX_BFS_SYNC=1: the
+  // memcpy + synchronize form, A/B)
+  bool const poll = std::getenv("CGX_BFS_SYNC") == nullptr && !ctr_memcpy;
+  bfs_ctr* pctr   = poll ? h.polled_as<bfs_ctr>() : nullptr;
   auto read_ctr = [&]() {
-    if (ctr_memcpy) HIP_CHECK(hipMemcpyAsync(hctr, ctr.data(), sizeof(bfs_ctr), hipMemcpyDeviceToHost, s));
-    else hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(64), 0, s, ctr.data(), hctr);
+    if (poll) {
+      unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
+      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq);
+      CGX_LAUNCH_CHECK();
+      for (unsigned long long n = 1; __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) != seq; ++n) {
+        __builtin_ia32_pause();
+        if ((n & 0xfffff) == 0) {  // ~every few ms: the stream must still be running, or done
+          hipError_t const q = hipStreamQuery(s);
+          if (q != hipSuccess && q != hipErrorNotReady) HIP_CHECK(q);
+          if (q == hipSuccess && __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) != seq)
+            throw std::runtime_error("BFS: level counters not published");
+        }
+      }
+      std::memcpy(hctr, pctr, sizeof(bfs_ctr));
+      return;
+    }
+    if (ctr_memcpy) hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(64), 0, s, ctr.data(), hctr);
+    else HIP_CHECK(hipMemcpyAsync(hctr, ctr.data(), sizeof(bfs_ctr), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
   };
   auto zero_ctr = [&]() { HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(bfs_ctr), s)); };

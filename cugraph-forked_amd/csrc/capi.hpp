@@ -14,6 +14,7 @@
 
 #include <memory>
 #include <string>
+#include <cstring>
 #include <vector>
 
 namespace cgx {
@@ -45,6 +46,19 @@ struct handle_t {
     if (!pinned) HIP_CHECK(hipHostMalloc(&pinned, kPinnedBytes, hipHostMallocDefault));
     return static_cast<T*>(pinned);
   }
+  // Coherent (fine-grained) pinned block the host polls while the stream runs on:
+  // a kernel publishes values and then a sequence number with system-scope stores.
+  void* polled = nullptr;
+  template <typename T>
+  T* polled_as()
+  {
+    static_assert(sizeof(T) <= kPinnedBytes, "polled scratch too small");
+    if (!polled) {
+      HIP_CHECK(hipHostMalloc(&polled, kPinnedBytes, hipHostMallocCoherent));
+      std::memset(polled, 0, kPinnedBytes);
+    }
+    return static_cast<T*>(polled);
+  }
   hipEvent_t event(size_t i)  // the i-th pooled event (created on first use)
   {
     while (events.size() <= i) {
@@ -58,6 +72,7 @@ struct handle_t {
   ~handle_t()
   {
     if (pinned) (void)hipHostFree(pinned);
+    if (polled) (void)hipHostFree(polled);
     for (auto e : events) (void)hipEventDestroy(e);
   }
 };
