@@ -54,13 +54,19 @@ __global__ void k_publish_ctr(bfs_ctr const* ctr, bfs_ctr* host)
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// the level counters, then seq (the host's poll word, pad[0]) behind a system fence
-__global__ void k_publish_seq(bfs_ctr const* ctr, bfs_ctr* host, unsigned long long seq)
+// the level counters (then zeroed for the next level: no memset launch per level)
+// and the source check flag (pad[1]), then seq (the host's poll word, pad[0]) behind
+// a system fence
+__global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr* host, unsigned long long seq, int const* bad)
 {
   if (threadIdx.x != 0) return;
-  unsigned long long const* c = reinterpret_cast<unsigned long long const*>(ctr);
-  unsigned long long* hp      = reinterpret_cast<unsigned long long*>(host);
-  for (int i = 0; i < 5; ++i) __hip_atomic_store(hp + i, c[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned long long* c  = reinterpret_cast<unsigned long long*>(ctr);
+  unsigned long long* hp = reinterpret_cast<unsigned long long*>(host);
+  for (int i = 0; i < 5; ++i) {
+    __hip_atomic_store(hp + i, c[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    c[i] = 0ull;
+  }
+  __hip_atomic_store(&host->pad[1], bad ? (unsigned long long)*bad : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();
   __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -654,10 +660,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // memcpy + synchronize form, A/B)
   bool const poll = std::getenv("CGX_BFS_SYNC") == nullptr && !ctr_memcpy;
   bfs_ctr* pctr   = poll ? h.polled_as<bfs_ctr>() : nullptr;
-  auto read_ctr = [&]() {
+  auto read_ctr = [&](int const* bad_flag = nullptr) {
     if (poll) {
       unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
-      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq);
+      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag);
       CGX_LAUNCH_CHECK();
       for (unsigned long long n = 1; __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) != seq; ++n) {
         __builtin_ia32_pause();
@@ -676,6 +682,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     HIP_CHECK(hipStreamSynchronize(s));
   };
   auto zero_ctr = [&]() { HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(bfs_ctr), s)); };
+  auto rezero_ctr = [&]() {  // after a read: k_publish_seq already zeroed the counters
+    if (!poll) zero_ctr();
+  };
 
   try {
     // sources -> distance 0, visited, frontier bitmap; then bitmap -> queues
@@ -686,13 +695,17 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     hipLaunchKernelGGL(k_sources_to_bitmap<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, dist, nv,
                        vis.data(), fr.data());
     CGX_LAUNCH_CHECK();
-    CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: sources have invalid vertex IDs.");
+    // poll mode: the source check comes back with the first counters (one host
+    // round trip fewer); invalid ids were skipped by k_bfs_init_sources
+    if (!poll)
+      CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: sources have invalid vertex IDs.");
     zero_ctr();
     for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
     hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, a,
                        fr.data(), nwords);
     CGX_LAUNCH_CHECK();
-    read_ctr();
+    read_ctr(bad.data());
+    if (poll) CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
     unsigned long long ncur[3] = {hctr->qlen[0], hctr->qlen[1], hctr->qlen[2]};
     unsigned long long n_f = ncur[0] + ncur[1] + ncur[2];
     unsigned long long m_f = hctr->next_m;
@@ -730,7 +743,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         else if (bottom_up && (double)n_f < (double)nv / beta_do) bottom_up = false;
       }
       a.depth = depth;
-      zero_ctr();
+      rezero_ctr();
       if (bottom_up) {
         if (!have_bitmap) {  // queues -> frontier bitmap
           HIP_CHECK(hipMemsetAsync(fr.data(), 0, nwords * 4, s));
@@ -765,7 +778,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           CGX_LAUNCH_CHECK();
           read_ctr();
           for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
-          zero_ctr();
+          rezero_ctr();
           have_queue = true;
         }
         for (int c = 0; c < 3; ++c) {

@@ -415,6 +415,30 @@ extern "C" bool_t cugraph_amd_graph_is_symmetric(const cugraph_graph_t* graph)
   return G(graph)->symmetric ? TRUE : FALSE;
 }
 
+extern "C" cugraph_error_code_t cugraph_amd_device_array_views_copy(
+  const cugraph_resource_handle_t* handle,
+  size_t n,
+  cugraph_type_erased_device_array_view_t* const* dst,
+  const cugraph_type_erased_device_array_view_t* const* src,
+  cugraph_error_t** error)
+{
+  *error = nullptr;
+  return guarded(error, [&] {
+    for (size_t i = 0; i < n; ++i) {
+      auto* d       = AV(dst[i]);
+      auto const* v = AV(src[i]);
+      CGX_INPUT(d->type == v->type, "Invalid input argument: type mismatch");
+      CGX_INPUT(d->size == v->size, "Invalid input argument: size mismatch");
+    }
+    for (size_t i = 0; i < n; ++i) {
+      auto* d       = AV(dst[i]);
+      auto const* v = AV(src[i]);
+      if (v->num_bytes) HIP_CHECK(hipMemcpyAsync(d->data, v->data, v->num_bytes, hipMemcpyDefault, H(handle)->stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(H(handle)->stream));
+  });
+}
+
 extern "C" cugraph_error_code_t cugraph_amd_graph_get_adjacency(const cugraph_resource_handle_t* handle,
                                                                cugraph_graph_t* graph,
                                                                bool_t transposed,

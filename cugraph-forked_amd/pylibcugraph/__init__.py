@@ -14,7 +14,8 @@ from __future__ import annotations
 import ctypes
 
 from . import _lib
-from ._arrays import DeviceArray, DeviceView, copy_view_to_tensor, optional_view, to_device_tensor, vptr
+from ._arrays import (DeviceArray, DeviceView, copy_view_to_tensor, copy_views_to_tensors, optional_view,
+                      to_device_tensor, vptr)
 
 from . import generators  # noqa: E402,F401  (MI355X build extensions)
 from . import comms  # noqa: E402,F401  (multi-GPU communicator contexts)
@@ -188,8 +189,8 @@ def _centrality(api, resource_handle, graph, *views_and_scalars):
     _lib.call(api, resource_handle.ptr, graph.c_graph_ptr, *views_and_scalars, ctypes.byref(res))
     h = resource_handle.ptr
     try:
-        v = copy_view_to_tensor(h, _lib.lib.cugraph_centrality_result_get_vertices(res))
-        x = copy_view_to_tensor(h, _lib.lib.cugraph_centrality_result_get_values(res))
+        v, x = copy_views_to_tensors(h, [_lib.lib.cugraph_centrality_result_get_vertices(res),
+                                         _lib.lib.cugraph_centrality_result_get_values(res)])
     finally:
         _lib.lib.cugraph_centrality_result_free(res)
     return v, x
@@ -226,9 +227,9 @@ def personalized_pagerank(resource_handle, graph, precomputed_vertex_out_weight_
 def _paths(resource_handle, res):
     h = resource_handle.ptr
     try:
-        v = copy_view_to_tensor(h, _lib.lib.cugraph_paths_result_get_vertices(res))
-        d = copy_view_to_tensor(h, _lib.lib.cugraph_paths_result_get_distances(res))
-        p = copy_view_to_tensor(h, _lib.lib.cugraph_paths_result_get_predecessors(res))
+        v, d, p = copy_views_to_tensors(h, [_lib.lib.cugraph_paths_result_get_vertices(res),
+                                            _lib.lib.cugraph_paths_result_get_distances(res),
+                                            _lib.lib.cugraph_paths_result_get_predecessors(res)])
     finally:
         _lib.lib.cugraph_paths_result_free(res)
     return v, d, p

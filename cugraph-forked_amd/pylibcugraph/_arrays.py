@@ -97,6 +97,32 @@ def copy_view_to_tensor(handle_ptr, view_ptr, free_view=True):
     return out
 
 
+def copy_views_to_tensors(handle_ptr, view_ptrs):
+    """copy_view_to_tensor for several result views with one C call (one stream
+    synchronize instead of one per array); the source views are freed."""
+    torch = _torch()
+    outs, dsts = [], []
+    try:
+        for v in view_ptrs:
+            c_type = _lib.lib.cugraph_type_erased_device_array_view_type(v)
+            n = _lib.lib.cugraph_type_erased_device_array_view_size(v)
+            out = torch.empty(n, dtype=_torch_dtype(c_type), device="cuda")
+            outs.append(out)
+            dsts.append(_lib.lib.cugraph_type_erased_device_array_view_create(ctypes.c_void_p(out.data_ptr()), n,
+                                                                               c_type))
+        k = len(view_ptrs)
+        dst_arr = (ctypes.c_void_p * k)(*dsts)
+        src_arr = (ctypes.c_void_p * k)(*view_ptrs)
+        _lib.call("cugraph_amd_device_array_views_copy", handle_ptr, k, ctypes.cast(dst_arr, ctypes.c_void_p),
+                  ctypes.cast(src_arr, ctypes.c_void_p))
+    finally:
+        for d in dsts:
+            _lib.lib.cugraph_type_erased_device_array_view_free(d)
+        for v in view_ptrs:
+            _lib.lib.cugraph_type_erased_device_array_view_free(v)
+    return outs
+
+
 def copy_view_to_numpy(handle_ptr, view_ptr):
     c_type = _lib.lib.cugraph_type_erased_device_array_view_type(view_ptr)
     n = _lib.lib.cugraph_type_erased_device_array_view_size(view_ptr)

@@ -79,6 +79,17 @@ cugraph_error_code_t cugraph_amd_graph_get_adjacency(const cugraph_resource_hand
                                                      cugraph_error_t** error);
 
 /*
+ * Copy n device array views (dst[i] <- src[i], same type and size) with one
+ * stream synchronize at the end: the batched form of
+ * cugraph_type_erased_device_array_view_copy (array.h) for result extraction.
+ */
+cugraph_error_code_t cugraph_amd_device_array_views_copy(const cugraph_resource_handle_t* handle,
+                                                         size_t n,
+                                                         cugraph_type_erased_device_array_view_t* const* dst,
+                                                         const cugraph_type_erased_device_array_view_t* const* src,
+                                                         cugraph_error_t** error);
+
+/*
  * Measurement hooks.  When profiling is on, algorithms record HIP events
  * around every launch of their dominant kernel (on the handle's stream) and
  * keep the total; stats are per handle and reset by each algorithm call.
