@@ -315,15 +315,18 @@ __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, u
   }
 }
 
-// bitmap -> class queues (bottom-up to top-down switch)
+// bitmap -> class queues (bottom-up to top-down switch).
+// The bitmap is cleared as it is read: while the frontier lives in queues the
+// bitmap stays all zero, so a later queues -> bitmap conversion needs no memset.
 template <typename V, typename E>
-__global__ __launch_bounds__(256) void k_bitmap_to_queues(bfs_args<V, E> a, uint32_t const* bm, int64_t nwords)
+__global__ __launch_bounds__(256) void k_bitmap_to_queues(bfs_args<V, E> a, uint32_t* bm, int64_t nwords)
 {
   CGX_WAVE_STAGE(V, st);
   unsigned long long my_m = 0;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += (int64_t)gridDim.x * blockDim.x) {
     int64_t w     = base + threadIdx.x;
     uint32_t word = w < nwords ? bm[w] : 0u;
+    if (word) bm[w] = 0u;
     // up to 32 rounds: every lane walks its word's set bits
     for (int r = 0; r < 32; ++r) {
       bool take = word != 0;
@@ -568,11 +571,16 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
   flush_counts(a.ctr, my_n, my_m);
 }
 
+// unreached -> -1, reached -> the external id of the predecessor (nmap: the
+// graph's number map, nullptr when not renumbered), one pass
 template <typename V>
-__global__ void k_finish_pred(V* pred, size_t n, V none)
+__global__ void k_finish_pred(V* pred, size_t n, V none, V const* nmap)
 {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    if (pred[i] == none) pred[i] = (V)-1;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    V const p = pred[i];
+    if (p == none) pred[i] = (V)-1;
+    else if (nmap) pred[i] = nmap[p];
+  }
 }
 
 // dist / pred = INF and the three bitmaps cleared in one launch (was 2 fills + 3 memsets)
@@ -620,7 +628,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
             "Invalid input argument: input graph should be symmetric for direction optimizing BFS.");
   (void)expensive;
   // sources: external -> internal, in place (c_api/bfs.cpp:96-114)
-  renumber_ext_to_int(h, g, sources->data, sources->size, true);
+  // ids not in the graph become -1 and are reported by k_bfs_sources' range check
+  // (no host round trip here)
+  if (g.renumbered) renumber_ext_to_int_unchecked(h, g, sources->data, sources->size);
   V const INF = std::numeric_limits<V>::max();
   res.vertices  = number_map_copy(h, g);
   res.distances = std::make_unique<device_array_t>((size_t)nv, dtype_of<V>(), s);
@@ -718,7 +728,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     unsigned long long m_u = (unsigned long long)g.num_edges - m_f;
     bool bottom_up  = false;
     bool have_queue = true;  // frontier available as queues (qa); else as bitmap fr
-    bool have_bitmap = true; // frontier bitmap fr valid
+    bool have_bitmap = false; // frontier bitmap fr valid (else fr is all zero: k_bitmap_to_queues clears it)
     V depth = 0;
     V limit = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
                                               (unsigned long long)std::numeric_limits<V>::max());
@@ -751,8 +761,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       a.depth = depth;
       rezero_ctr();
       if (bottom_up) {
-        if (!have_bitmap) {  // queues -> frontier bitmap
-          HIP_CHECK(hipMemsetAsync(fr.data(), 0, nwords * 4, s));
+        if (!have_bitmap) {  // queues -> frontier bitmap (fr is all zero here)
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
                              ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), fr.data());
           CGX_LAUNCH_CHECK();
@@ -831,9 +840,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     throw;
   }
   if (pred) {
-    hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF);
+    hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF,
+                       g.renumbered ? g.number_map.data<V>() : (V const*)nullptr);
     CGX_LAUNCH_CHECK();
-    unrenumber_int_to_ext(h, g, pred, (size_t)nv);
   }
 }
 

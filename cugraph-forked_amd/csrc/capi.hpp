@@ -249,6 +249,9 @@ adjacency_t& ensure_adjacency(handle_t& h, graph_t& g, bool transposed);  // bui
 void ensure_schedule(handle_t& h, graph_t& g, adjacency_t& adj);
 // external ids (device, graph vertex type) -> internal ids, in place; throws on unknown ids
 void renumber_ext_to_int(handle_t& h, graph_t& g, void* ids, size_t n, bool check);
+// the same lookup with no check and no host sync: ids not in the graph become -1,
+// for callers that range-check the internal ids on the device anyway (BFS sources)
+void renumber_ext_to_int_unchecked(handle_t& h, graph_t& g, void* ids, size_t n);
 // sorted external ids + their internal ids (g.ext_sorted / g.ext_internal), renumbered graphs
 void ensure_ext_lookup(handle_t& h, graph_t& g);
 // internal ids -> external ids (values < 0 or >= V are left untouched), in place

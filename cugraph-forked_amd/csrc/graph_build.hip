@@ -185,7 +185,7 @@ __global__ void k_ext_to_int(V* ids, size_t n, V const* sorted_ext, V const* int
     if (lo < nv && sorted_ext[lo] == x) ids[i] = internal[lo];
     else {
       ids[i] = static_cast<V>(-1);
-      atomicAdd(bad, 1);
+      if (bad) atomicAdd(bad, 1);
     }
   }
 }
@@ -576,6 +576,21 @@ void renumber_ext_to_int(handle_t& h, graph_t& g, void* ids, size_t n, bool /*ch
   if (g.vertex_type == INT32) run(int32_t{});
   else run(int64_t{});
   CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: vertex id not in the graph.");
+}
+
+void renumber_ext_to_int_unchecked(handle_t& h, graph_t& g, void* ids, size_t n)
+{
+  if (!n || !g.renumbered) return;
+  hipStream_t s = h.stream;
+  auto run      = [&](auto vtag) {
+    using V = decltype(vtag);
+    if (!g.ext_lookup_valid) ext_lookup_impl<V>(h, g);
+    hipLaunchKernelGGL(k_ext_to_int<V>, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, static_cast<V*>(ids), n,
+                       g.ext_sorted.data<V>(), g.ext_internal.data<V>(), (size_t)g.num_vertices, nullptr);
+    CGX_LAUNCH_CHECK();
+  };
+  if (g.vertex_type == INT32) run(int32_t{});
+  else run(int64_t{});
 }
 
 void ensure_ext_lookup(handle_t& h, graph_t& g)

@@ -72,7 +72,47 @@ struct pr_args {
   double* partials;
   pr_state* st;
   double* mg_sums;  // multi-GPU: (diff, dangling) of this rank, allreduced before k_mg_finish
+  int enc;          // x~ stored as fixed-point words (enc_fixed; single-GPU fp32 packed push only)
 };
+
+// x~ as the push consumes it: the 64-bit fixed-point value RNE(x * 2^62) of an fp32
+// x in [0, 1] written as one 32-bit word, significand M (24 bits) | shift s << 24,
+// value = M << s.  x = M * 2^(eb - 150) for the biased exponent eb, so s = eb - 88
+// for x >= 2^-39 (exact); smaller x are rounded to nearest-even here, once per
+// vertex, and stored with s = 0.  The push then converts with an and, a shift and
+// a 64-bit shift instead of the 7-op fp32 sequence per entry (to_fixed_f32), with
+// the same bits.
+__device__ __forceinline__ uint32_t enc_fixed(float x)
+{
+  uint32_t const b  = __float_as_uint(x);
+  uint32_t const eb = b >> 23;  // x >= 0
+  uint32_t const m  = (b & 0x7fffffu) | 0x800000u;
+  if (eb >= 88u) return ((eb - 88u) << 24) | m;
+  if (eb == 0u) return 0u;  // denormal or zero: below 2^-126, rounds to 0
+  uint32_t const k = 88u - eb;
+  if (k > 24u) return 0u;  // m / 2^k < 1/2
+  uint32_t const q    = m >> k;
+  uint32_t const r    = m & ((1u << k) - 1u);
+  uint32_t const half = 1u << (k - 1u);
+  return q + ((r > half || (r == half && (q & 1u))) ? 1u : 0u);
+}
+
+__device__ __forceinline__ unsigned long long dec_fixed(uint32_t w)
+{
+  return (unsigned long long)(w & 0xffffffu) << (w >> 24);
+}
+
+template <typename R>
+__device__ __forceinline__ void store_x(R* x, int64_t v, R val, int enc)
+{
+  if constexpr (std::is_same<R, float>::value) {
+    if (enc) {
+      reinterpret_cast<uint32_t*>(x)[v] = enc_fixed(val);
+      return;
+    }
+  }
+  x[v] = val;
+}
 
 // Iterations to enqueue before the host next reads the state.  The L1 difference
 // of the power iteration falls geometrically (ratio ~ alpha times the second
@@ -169,9 +209,9 @@ __global__ __launch_bounds__(256) void k_pr_init(pr_args<V, E, R> a)
     R ow = a.outw[v];
     if (ow == R(0)) {
       dang += (double)p;
-      a.x_out[v] = R(0);
+      store_x<R>(a.x_out, v, R(0), a.enc);
     } else {
-      a.x_out[v] = (R)((double)p / (double)ow);
+      store_x<R>(a.x_out, v, (R)((double)p / (double)ow), a.enc);
     }
   }
   finish_iteration<V, E, R>(a, 0.0, dang, false);
@@ -243,7 +283,7 @@ __device__ __forceinline__ void vertex_update_from(pr_args<V, E, R> const& a, V 
   R xv = R(0);
   if (ow == R(0)) my_dang += (double)nr;
   else xv = (R)((double)nr / (double)ow);
-  a.x_out[v] = xv;
+  store_x<R>(a.x_out, v, xv, a.enc);
 }
 
 template <typename V, typename E, typename R>
@@ -260,7 +300,7 @@ __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, do
   R xv = R(0);
   if (ow == R(0)) my_dang += (double)nr;
   else xv = (R)((double)nr / (double)ow);
-  a.x_out[v] = xv;
+  store_x<R>(a.x_out, v, xv, a.enc);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -368,6 +408,12 @@ inline int push_win_bits(int64_t n_rows)
 
 // 16-bit packed entries for unweighted graphs (push_body16); CGX_PR_PACKED=0 keeps
 // the 32-bit format (measurement / A-B only)
+inline bool env_is(char const* name, char const* value)
+{
+  char const* e = std::getenv(name);
+  return e && std::string(e) == value;
+}
+
 inline bool packed_enabled()
 {
   char const* e = std::getenv("CGX_PR_PACKED");
@@ -591,9 +637,11 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
   for (int j = 0; j < N; ++j) v[j] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x143, 0xc, 0xf, false);
 }
 
-template <int WB, typename V, typename E, typename R>
+template <int WB, typename V, typename E, typename R, bool ENC>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
+  // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed
+  using xw_t = typename std::conditional<ENC, uint32_t, R>::type;
   constexpr int kWin        = 1 << WB;
   constexpr uint32_t kJump  = (1u << (16 - WB)) - 1;  // delta code of a jump entry
   constexpr uint32_t kLow   = (1u << WB) - 1;
@@ -604,11 +652,11 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   if (sa.a.st->done) return;
   int const tid  = threadIdx.x;
   int const lane = tid & 63;
-  int const wave = tid >> 6;
+  int const wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
   using cunit_t        = __attribute__((address_space(4))) push_unit const;
   cunit_t* const units = (cunit_t*)sa.units;
-  R const* const x     = sa.a.x_in;
+  xw_t const* const x  = reinterpret_cast<xw_t const*>(sa.a.x_in);
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
     if (tid == 0) {
@@ -626,32 +674,37 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     int64_t const ua = sa.items[it], ub = sa.items[it + 1];
     int64_t const win = units[ua].win;
     int64_t k0 = units[ua].k0;
-    int n      = (int)(units[ua].k1 - k0) - wave * kSegEntries;  // entries of this wave's segment (may be <= 0)
+    // entries of this wave's segment: a multiple of kSegEntries (windows are padded
+    // to whole segments), <= 0 for the waves past the end of a window's last unit
+    int n      = (int)(units[ua].k1 - k0) - wave * kSegEntries;
     uint32_t base = __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]);
     uint16_t ent[kRows];
 #pragma unroll
     for (int j = 0; j < kRows; ++j) ent[j] = nt_load(sa.ent16 + k0 + wave * kSegEntries + j * 64 + lane);  // padded
     for (int64_t un = ua; un < ub; ++un) {
-      uint32_t sc[kRows], slot[kRows];
-      bool live[kRows];
+      bool const active = n > 0;  // wave-uniform
+      uint32_t slot[kRows];
+      xw_t xv[kRows];
+      if (active) {
+        uint32_t sc[kRows];
+        bool live[kRows];
 #pragma unroll
-      for (int j = 0; j < kRows; ++j) {
-        bool const ok   = j * 64 + lane < n;
-        uint32_t const e = ok ? (uint32_t)ent[j] : (kJump << WB);  // past the end: a jump of 0
-        bool const jump = (e >> WB) == kJump;
-        live[j]         = !jump;
-        slot[j]         = e & kLow;
-        sc[j]           = jump ? (e & kLow) : (e >> WB);
-      }
-      wave_incl_scan_rows<kRows>(sc);
-      R xv[kRows];
-      uint32_t run = base;
+        for (int j = 0; j < kRows; ++j) {
+          uint32_t const e = (uint32_t)ent[j];
+          bool const jump  = (e >> WB) == kJump;
+          live[j]          = !jump;
+          slot[j]          = e & kLow;
+          sc[j]            = jump ? (e & kLow) : (e >> WB);
+        }
+        wave_incl_scan_rows<kRows>(sc);
+        uint32_t run = base;
 #pragma unroll
-      for (int j = 0; j < kRows; ++j) {
-        uint32_t const src = run + sc[j];
-        run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-        xv[j] = x[src];  // every lane loads (jumps and the tail read a valid source id)
-        xv[j] = live[j] ? xv[j] : R(0);
+        for (int j = 0; j < kRows; ++j) {
+          uint32_t const src = run + sc[j];
+          run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
+          xv[j] = x[src];  // every lane loads (jumps and padding read a valid source id)
+          xv[j] = live[j] ? xv[j] : xw_t(0);
+        }
       }
       int64_t const nx  = un + 1 < ub ? un + 1 : un;
       int64_t const k0n = units[nx].k0;
@@ -661,8 +714,13 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 #pragma unroll
       for (int j = 0; j < kRows; ++j) ent_n[j] = nt_load(sa.ent16 + k0n + wave * kSegEntries + j * 64 + lane);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
+      if (active) {
 #pragma unroll
-      for (int j = 0; j < kRows; ++j) atomicAdd(&acc[slot[j]], fixed_of(xv[j]));
+        for (int j = 0; j < kRows; ++j) {
+          if constexpr (ENC) atomicAdd(&acc[slot[j]], dec_fixed(xv[j]));
+          else atomicAdd(&acc[slot[j]], fixed_of(xv[j]));
+        }
+      }
 #pragma unroll
       for (int j = 0; j < kRows; ++j) ent[j] = ent_n[j];
       n    = nn;
@@ -672,10 +730,10 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   }
 }
 
-template <int WB, typename V, typename E, typename R>
+template <int WB, typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
 {
-  push_body16<WB, V, E, R>(sa);
+  push_body16<WB, V, E, R, ENC>(sa);
 }
 
 template <typename V, typename E, typename R>
@@ -822,8 +880,8 @@ __global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* w
 // real entry k at k + cm[k] (cm = inclusive prefix of the jump counts), its jumps
 // right before it
 __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, int64_t ne,
-                         int64_t const* ws, uint32_t const* mj, unsigned long long const* cm, int wb, uint32_t pmax,
-                         uint16_t* ent16)
+                         int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
+                         unsigned long long const* pb, int wb, uint32_t pmax, uint16_t* ent16)
 {
   uint32_t const jump = (1u << (16 - wb)) - 1, low = (1u << wb) - 1;
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
@@ -831,7 +889,7 @@ __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t co
     uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
     uint32_t const D    = (uint32_t)keys[k] - prev;
     uint32_t const m    = mj[k];
-    int64_t const pos   = k + (int64_t)cm[k];
+    int64_t const pos   = k + (int64_t)cm[k] + (int64_t)pb[w];
     uint32_t const slot = rows[vals[k]] & low;
     if (m == 0) {
       ent16[pos] = (uint16_t)((D << wb) | slot);
@@ -845,23 +903,37 @@ __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t co
   }
 }
 
-// window starts in packed positions (nws[nwin] = total)
-__global__ void k_packed_win_starts(int64_t const* ws, unsigned long long const* cm, int64_t nwin, int64_t total, int64_t* nws)
+// Every window's packed stream starts at a multiple of kSegEntries and is padded
+// with jumps of 0 (no edge) to a multiple of it, so every wave segment of a unit
+// is whole and the push needs no per-entry bound check.
+// unpadded packed start of window w (w == nwin: total)
+__device__ __forceinline__ int64_t packed_start(int64_t const* ws, unsigned long long const* cm, int64_t w,
+                                                int64_t nwin, int64_t total)
+{
+  return w == nwin ? total : ws[w] + (ws[w] > 0 ? (int64_t)cm[ws[w] - 1] : 0);
+}
+// padding after every window (pad[nwin] = 0)
+__global__ void k_packed_pads(int64_t const* ws, unsigned long long const* cm, int64_t nwin, int64_t total,
+                              unsigned long long* pad)
+{
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const len = w == nwin ? 0 : packed_start(ws, cm, w + 1, nwin, total) - packed_start(ws, cm, w, nwin, total);
+    pad[w]            = (unsigned long long)((kSegEntries - len % kSegEntries) % kSegEntries);
+  }
+}
+// padded window starts (pb = exclusive prefix of the pads; nws[nwin] = padded total)
+__global__ void k_packed_win_starts(int64_t const* ws, unsigned long long const* cm, unsigned long long const* pb,
+                                    int64_t nwin, int64_t total, int64_t* nws)
 {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x)
-    nws[w] = w == nwin ? total : ws[w] + (ws[w] > 0 ? (int64_t)cm[ws[w] - 1] : 0);
+    nws[w] = packed_start(ws, cm, w, nwin, total) + (int64_t)pb[w];
 }
 
-// unit heads over packed positions: window starts and multiples of kPushUnit
-__global__ void k_packed_unit_flags(int64_t total, uint32_t* flag)
-{
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x)
-    flag[p] = p % kPushUnit == 0 ? 1u : 0u;
-}
-__global__ void k_packed_mark_starts(int64_t const* nws, int64_t nwin, int64_t total, uint32_t* flag)
+// unit heads: every window start and every kPushUnit entries into a window
+__global__ void k_packed_unit_marks(int64_t const* nws, int64_t nwin, uint32_t* flag)
 {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwin; w += (int64_t)gridDim.x * blockDim.x)
-    if (nws[w] < total) flag[nws[w]] = 1u;
+    for (int64_t p = nws[w]; p < nws[w + 1]; p += kPushUnit) flag[p] = 1u;
 }
 __global__ void k_packed_unit_heads(uint32_t const* flag, uint32_t const* uid, int64_t total, int64_t const* nws,
                                     int64_t nwin, push_unit* units)
@@ -880,25 +952,25 @@ __global__ void k_packed_unit_heads(uint32_t const* flag, uint32_t const* uid, i
 
 // running source before the first entry of every (unit, wave segment)
 __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t const* keys, int64_t ne,
-                            int64_t const* ws, uint32_t const* mj, unsigned long long const* cm, uint32_t dmax,
-                            uint32_t pmax, uint32_t* seg_base)
+                            int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
+                            unsigned long long const* pb, uint32_t dmax, uint32_t pmax, uint32_t* seg_base)
 {
   int64_t const n = nunits * kSegsPerUnit;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     push_unit const u = units[i / kSegsPerUnit];
     int64_t const p   = u.k0 + (i % kSegsPerUnit) * kSegEntries;
     uint32_t base     = 0;
-    if (p < u.k1) {
-      int64_t lo = 0, hi = ne - 1;  // first real entry with k + cm[k] >= p
+    if (p < u.k1) {  // a segment never starts in a window's padding
+      int64_t lo = 0, hi = ne - 1;  // first real entry at a packed position >= p
       while (lo < hi) {
         int64_t mid = (lo + hi) >> 1;
-        if (mid + (int64_t)cm[mid] < p) lo = mid + 1;
+        if (mid + (int64_t)cm[mid] + (int64_t)pb[keys[mid] >> 32] < p) lo = mid + 1;
         else hi = mid;
       }
       int64_t const k     = lo;
       uint32_t const m    = mj[k];
-      int64_t const j     = p - (k + (int64_t)cm[k] - m);
       int64_t const w     = (int64_t)(keys[k] >> 32);
+      int64_t const j     = p - (k + (int64_t)cm[k] + (int64_t)pb[w] - m);
       uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
       uint32_t const src  = (uint32_t)keys[k];
       uint32_t const D    = src - prev;
@@ -1200,7 +1272,8 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.src_head = -1;
   {
     int64_t const nbins = (n_cols + (int64_t(1) << kSrcBinBits) - 1) >> kSrcBinBits;
-    if (n_cols >= (int64_t)kSrcParts << (kSrcBinBits + 2) && srcpart_enabled()) {
+    // (32-bit entries only: its cuts would break the packed format's whole segments)
+    if (n_cols >= (int64_t)kSrcParts << (kSrcBinBits + 2) && srcpart_enabled() && (w || !packed_enabled())) {
       dbuf<unsigned long long> bc(nbins, s);
       fill<unsigned long long>(bc.data(), nbins, 0ull, s);
       hipLaunchKernelGGL(k_src_bin_counts, dim3(grid_for(nwin * nbins, kBlock, 16384)), dim3(kBlock), 0, s,
@@ -1234,27 +1307,34 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     CGX_LAUNCH_CHECK();
     fill<uint32_t>(mj.data() + ne, 1, 0u, s);
     exclusive_scan<uint32_t, unsigned long long>(mj.data(), ex.data(), ne + 1, s);
-    int64_t const total = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
+    int64_t const total0 = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
     unsigned long long const* cm = ex.data() + 1;  // inclusive prefix
+    // windows padded to whole wave segments (k_packed_pads)
+    dbuf<unsigned long long> pad(nwin + 1, s), pb(nwin + 1, s);
+    hipLaunchKernelGGL(k_packed_pads, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nwin,
+                       total0, pad.data());
+    CGX_LAUNCH_CHECK();
+    exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nwin + 1, s);
+    int64_t const total = total0 + (int64_t)to_host(pb.data() + nwin, 1, s)[0];
     if (total <= ne + ne / 2 && (uint64_t)total < (1ull << 32)) {
+      uint16_t const pad_code = (uint16_t)(((1u << (16 - wb)) - 1) << wb);  // a jump of 0: no edge
       pp.packed = true;
       pp.ent16.set_stream(s);
-      pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // padded: the kernel loads whole units
-      HIP_CHECK(hipMemsetAsync(pp.ent16.data<uint16_t>() + total, 0, kPushUnit * sizeof(uint16_t), s));
+      pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // + a unit: the kernel prefetches whole units
+      fill<uint16_t>(pp.ent16.data<uint16_t>(), (size_t)(total + kPushUnit), pad_code, s);
       hipLaunchKernelGGL(k_pack16, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                         vals_out.data(), rows, ne, ws.data(), mj.data(), cm, wb, pmax, pp.ent16.data<uint16_t>());
+                         vals_out.data(), rows, ne, ws.data(), mj.data(), cm, pb.data(), wb, pmax,
+                         pp.ent16.data<uint16_t>());
       CGX_LAUNCH_CHECK();
       dbuf<int64_t> nws(nwin + 1, s);
       hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
-                         cm, nwin, total, nws.data());
+                         cm, pb.data(), nwin, total0, nws.data());
       dbuf<uint32_t> pflag(total + 1, s), puid(total + 1, s);
-      hipLaunchKernelGGL(k_packed_unit_flags, dim3(grid_for(total, kBlock, 16384)), dim3(kBlock), 0, s, total,
+      fill<uint32_t>(pflag.data(), (size_t)(total + 1), 0u, s);
+      hipLaunchKernelGGL(k_packed_unit_marks, dim3(grid_for(nwin, 64, 4096)), dim3(64), 0, s, nws.data(), nwin,
                          pflag.data());
-      hipLaunchKernelGGL(k_packed_mark_starts, dim3(grid_for(nwin, kBlock, 4096)), dim3(kBlock), 0, s, nws.data(),
-                         nwin, total, pflag.data());
       CGX_LAUNCH_CHECK();
-      auto const cp = cut_positions(cm, pflag.data());
-      fill<uint32_t>(pflag.data() + total, 1, 0u, s);
+      std::vector<int64_t> const cp;  // no source partition with packed entries
       exclusive_scan<uint32_t, uint32_t>(pflag.data(), puid.data(), total + 1, s);
       int64_t const nunits = (int64_t)to_host(puid.data() + total, 1, s)[0];
       pp.units.set_stream(s);
@@ -1268,7 +1348,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       pp.seg_base.set_stream(s);
       pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
       hipLaunchKernelGGL(k_seg_bases, dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0, s, units,
-                         nunits, keys_out.data(), ne, ws.data(), mj.data(), cm, dmax, pmax,
+                         nunits, keys_out.data(), ne, ws.data(), mj.data(), cm, pb.data(), dmax, pmax,
                          pp.seg_base.data<uint32_t>());
       CGX_LAUNCH_CHECK();
       pp.ent.release();
@@ -1389,9 +1469,12 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 
 // the push kernel for the schedule's window bits and entry format
 template <typename V, typename E, typename R>
-auto push_kernel(pr_push_t const& pp, bool weighted)
+auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
-  if (pp.packed) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R> : k_pr_push16<12, V, E, R>;
+  if (pp.packed) {
+    if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true> : k_pr_push16<12, V, E, R, true>;
+    return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false> : k_pr_push16<12, V, E, R, false>;
+  }
   constexpr bool wide = sizeof(R) == 8;  // fp64 weights: no 8-waves bound (see k_pr_push_q_wide)
   if (pp.win_bits == 13)
     return weighted ? (wide ? k_pr_push_q_wide<13, V, E, R, true> : k_pr_push_q<13, V, E, R, true>)
@@ -1511,19 +1594,22 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   a.st       = st.data();
   a.x_in     = nullptr;
   a.x_out    = xa.data();
+
+  // windowed push (our own out-weight sums keep every fixed-point sum <= 1; user
+  // precomputed out-weights may not: generic pull kernel then)
+  bool push = pow_v == nullptr && max_iter > 0;
+  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj);
+  push = push && adj.pr.ok;
+  // fp32 packed push: x~ as enc_fixed words (CGX_PR_ENC=0: plain floats, A/B)
+  a.enc = push && adj.pr.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
 
   if (max_iter == 0) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
 
-  // windowed push (our own out-weight sums keep every fixed-point sum <= 1; user
-  // precomputed out-weights may not: generic pull kernel then)
-  bool push = pow_v == nullptr;
-  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj);
-  push = push && adj.pr.ok;
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  auto pkernel = push_kernel<V, E, R>(adj.pr, g.weighted);
+  auto pkernel = push_kernel<V, E, R>(adj.pr, g.weighted, a.enc != 0);
   if (push) {
     set_queue_args(sa, adj.pr, s);
     nblk_push  = sa.nitems ? kPushBlocks : 0;
