@@ -389,18 +389,21 @@ def test_mg_rank_without_edges(algo, monkeypatch):
         tmp.spawn(_worker, args=(3, port, 3, 10, False, algo), nprocs=3, join=True)
 
 
-# The reference's 8-GPU grid (mg_utilities.cpp:60-66: R = 2 x C = 4) rehearsed with 8
-# ranks on the one test GPU over torch.distributed/gloo: the same partition, id
-# routing and per-level / per-iteration collectives an 8 x MI355X node runs over
-# RCCL (performance unmeasured here).
+# The reference's 8-GPU grid (mg_utilities.cpp:59-62: row communicator size = the
+# largest divisor of 8 not above sqrt(8) = 2, so R x C = 4 x 2 -- bench.py's default at
+# N = 8) and its transpose 2 x 4, rehearsed with 8 ranks on the one test GPU over
+# torch.distributed/gloo: the same partition, id routing and per-level /
+# per-iteration collectives an 8 x MI355X node runs over RCCL (performance
+# unmeasured here).
+@pytest.mark.parametrize("C", [2, 4])
 @pytest.mark.parametrize("algo", ["pagerank", "bfs_do", "bfs", "louvain"])
-def test_mg_world8_reference_grid(algo):
+def test_mg_world8_reference_grid(algo, C):
     import torch.multiprocessing as tmp
     port = _free_port()
     if algo == "louvain":
-        tmp.spawn(_louvain_worker, args=(8, port, 4, 10, True), nprocs=8, join=True)
+        tmp.spawn(_louvain_worker, args=(8, port, C, 10, True), nprocs=8, join=True)
     else:
-        tmp.spawn(_worker, args=(8, port, 4, 11, False, algo), nprocs=8, join=True)
+        tmp.spawn(_worker, args=(8, port, C, 11, False, algo), nprocs=8, join=True)
 
 
 def _dask_worker(rank, world, port, C):
