@@ -15,7 +15,8 @@
 //    scans its sorted adjacency in lane groups (degree-binned schedule, as the
 //    PageRank kernel) and stops at the first neighbour in the frontier bitmap
 //    (the bitmap is V/8 bytes: L2/Infinity-Cache resident).
-//  * Beamer switching (alpha = 14, beta = 24) from per-level counters.
+//  * Beamer switching from per-level counters, alpha = 40 / beta = 64 (measured on
+//    RMAT-24, see bfs_impl; mg_bfs.hip keeps Beamer's 14 / 24).
 //  * predecessor = the frontier neighbour with the smallest internal id in both
 //    directions (atomicMin top-down, first hit in the sorted list bottom-up), so
 //    results are deterministic and independent of the direction schedule.
@@ -469,7 +470,13 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
 #endif
 constexpr int kProbe = CGX_BFS_PROBE;
 
-template <typename V, typename E>
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+// VEC: a lane's first 8 neighbours from three 16-byte loads of the aligned
+// 12-entry span around them (adjacency arrays are padded by 16 entries) instead of
+// 8 dword gathers: consecutive lanes' lists are adjacent, so each load instruction
+// touches about as many cache lines as one dword gather did.
+template <typename V, typename E, bool VEC>
 __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
 {
   V const nd    = (V)(a.depth + 1);
@@ -492,8 +499,23 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
     V par    = 0;
     if (deg > 0) {
       V u[kProbe];
+      if constexpr (VEC && sizeof(V) == 4 && kProbe == 8) {
+        E const a0   = beg & ~E(3);
+        int const sh = (int)(beg - a0);
+        v4i_t const* p = reinterpret_cast<v4i_t const*>(a.idx + a0);
+        v4i_t const c0 = p[0], c1 = p[1], c2 = p[2];
+        int const wv[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
 #pragma unroll
-      for (int t = 0; t < kProbe; ++t) u[t] = a.idx[beg + (t < deg ? t : 0)];
+        for (int t = 0; t < kProbe; ++t) {
+          int const x = sh == 0 ? wv[t] : sh == 1 ? wv[t + 1] : sh == 2 ? wv[t + 2] : wv[t + 3];
+          u[t]        = (V)x;
+        }
+#pragma unroll
+        for (int t = 1; t < kProbe; ++t) u[t] = t < deg ? u[t] : u[0];  // past the list: another list or padding
+      } else {
+#pragma unroll
+        for (int t = 0; t < kProbe; ++t) u[t] = a.idx[beg + (t < deg ? t : 0)];
+      }
       uint32_t fw[kProbe];  // all frontier words first: the loads issue back to back
 #pragma unroll
       for (int t = 0; t < kProbe; ++t) fw[t] = a.fr[u[t] >> 5];
@@ -735,6 +757,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     size_t levels = 0, bu_steps = 0;
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
     bool const one_pass_bu = std::getenv("CGX_BFS_ONE_PASS_BU") != nullptr;  // A/B: the one-pass bottom-up
+    // probe neighbours by 16-byte loads (needs the padded adjacency, int32 ids)
+    bool const probe_vec = adj.idx_padded && std::getenv("CGX_BFS_PROBE_VEC") != nullptr;
     // Grid sizes: every block ends with same-address atomics on the level counters,
     // which serialise at the memory side (≈8 ns each): RMAT-24 MTEPS with the probe
     // on 512 / 1024 / 2048 / 8192 / 32768 blocks: 166K / 173K / 168K / 148K / 101K
@@ -770,8 +794,12 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         bool const probe_path = a.order == nullptr && !one_pass_bu;
         if (!probe_path) HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));  // the probe writes every word
         if (probe_path) {  // probe + residual (identity order)
-          hipLaunchKernelGGL((k_bu_probe<V, E>), dim3(grid_for((nv + 63) / 64, kBlock / 64, probe_grid)), dim3(kBlock),
-                             0, s, a, qb[0].data());
+          if (probe_vec)
+            hipLaunchKernelGGL((k_bu_probe<V, E, true>), dim3(grid_for((nv + 63) / 64, kBlock / 64, probe_grid)),
+                               dim3(kBlock), 0, s, a, qb[0].data());
+          else
+            hipLaunchKernelGGL((k_bu_probe<V, E, false>), dim3(grid_for((nv + 63) / 64, kBlock / 64, probe_grid)),
+                               dim3(kBlock), 0, s, a, qb[0].data());
           CGX_LAUNCH_CHECK();
           hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, a, qb[0].data());
         } else {

@@ -132,10 +132,13 @@ struct pr_push_t {
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).
+constexpr int64_t kIdxPad = 16;  // entries past the end of adjacency_t::indices (vector loads)
+
 struct adjacency_t {
   buffer offsets;  // edge_t[V+1]
-  buffer indices;  // vertex_t[E], ascending within each row
+  buffer indices;  // vertex_t[E], ascending within each row (+ kIdxPad entries when idx_padded)
   buffer weights;  // weight_t[E] or empty
+  bool idx_padded = false;
   // degree-binned schedule (built on first use, see schedule.hpp)
   bool degree_sorted = false;  // majors already in descending-degree order (renumbered build)
   bool sched_valid   = false;

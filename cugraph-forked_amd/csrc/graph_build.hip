@@ -255,7 +255,8 @@ void compress(hipStream_t s, int64_t nv, V const* majors, V const* minors, W con
   key.b.release();
   dbuf<V> smaj(n, s);
   adj.indices.set_stream(s);
-  adj.indices.resize(n * sizeof(V));
+  adj.indices.resize((n + kIdxPad) * sizeof(V));  // padded: vector loads may read past the last list
+  adj.idx_padded = true;
   if (n) {
     hipLaunchKernelGGL(k_split_key<V>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, key_sorted.data(), n, b,
                        smaj.data(), adj.indices.data<V>());

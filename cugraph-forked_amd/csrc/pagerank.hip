@@ -637,10 +637,15 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
   for (int j = 0; j < N; ++j) v[j] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x143, 0xc, 0xf, false);
 }
 
+// Rows are 64 consecutive entries, so one gather instruction spans a short source
+// range.  (Measured: lane-major segments -- a lane's 8 consecutive entries from one
+// 16-byte load, sources as a running sum plus one wave scan, 6 DPP adds per 8
+// entries instead of 48 -- were 20 % slower: each gather then spans the whole
+// 512-entry segment, and the gathers' cost follows the distinct lines each touches.)
 template <int WB, typename V, typename E, typename R, bool ENC>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
-  // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed
+  // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
   using xw_t = typename std::conditional<ENC, uint32_t, R>::type;
   constexpr int kWin        = 1 << WB;
   constexpr uint32_t kJump  = (1u << (16 - WB)) - 1;  // delta code of a jump entry
@@ -690,7 +695,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         bool live[kRows];
 #pragma unroll
         for (int j = 0; j < kRows; ++j) {
-          uint32_t const e = (uint32_t)ent[j];
+          uint32_t const e = ent[j];
           bool const jump  = (e >> WB) == kJump;
           live[j]          = !jump;
           slot[j]          = e & kLow;

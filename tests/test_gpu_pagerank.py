@@ -266,3 +266,4 @@ def test_encoded_x_bitwise_equal_float(graph, monkeypatch):
         got = by_ext(v, pr)
         ref = opr.pagerank(nv, s, d, None, 0.85, 1e-6, 500)
         assert (np.abs(got[:nv] - ref) / ref).max() < REL
+
