@@ -598,10 +598,21 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
 template <typename V>
 __global__ void k_finish_pred(V* pred, size_t n, V none, V const* nmap)
 {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    V const p = pred[i];
-    if (p == none) pred[i] = (V)-1;
-    else if (nmap) pred[i] = nmap[p];
+  constexpr int kB    = 4;  // elements per thread, loads (and number-map gathers) issued first
+  size_t const stride = (size_t)gridDim.x * blockDim.x;
+  size_t i            = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i + (kB - 1) * stride < n; i += kB * stride) {
+    V p[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) p[j] = pred[i + j * stride];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) p[j] = p[j] == none ? (V)-1 : (nmap ? nmap[p[j]] : p[j]);
+#pragma unroll
+    for (int j = 0; j < kB; ++j) pred[i + j * stride] = p[j];
+  }
+  for (; i < n; i += stride) {
+    V const q = pred[i];
+    pred[i]   = q == none ? (V)-1 : (nmap ? nmap[q] : q);
   }
 }
 
@@ -757,8 +768,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     size_t levels = 0, bu_steps = 0;
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
     bool const one_pass_bu = std::getenv("CGX_BFS_ONE_PASS_BU") != nullptr;  // A/B: the one-pass bottom-up
-    // probe neighbours by 16-byte loads (needs the padded adjacency, int32 ids)
-    bool const probe_vec = adj.idx_padded && std::getenv("CGX_BFS_PROBE_VEC") != nullptr;
+    // probe neighbours by 16-byte loads (needs the padded adjacency, int32 ids; RMAT-24
+    // k_bu_probe 133.6 -> 129.5 us average; CGX_BFS_PROBE_VEC=0: dword gathers, A/B)
+    char const* pv       = std::getenv("CGX_BFS_PROBE_VEC");
+    bool const probe_vec = adj.idx_padded && !(pv && std::string(pv) == "0");
     // Grid sizes: every block ends with same-address atomics on the level counters,
     // which serialise at the memory side (≈8 ns each): RMAT-24 MTEPS with the probe
     // on 512 / 1024 / 2048 / 8192 / 32768 blocks: 166K / 173K / 168K / 148K / 101K
@@ -868,7 +881,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     throw;
   }
   if (pred) {
-    hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF,
+    hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for((nv + 3) / 4, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF,
                        g.renumbered ? g.number_map.data<V>() : (V const*)nullptr);
     CGX_LAUNCH_CHECK();
   }

@@ -150,14 +150,16 @@ def test_extract_paths_rmat_renumbered():
 @pytest.mark.parametrize("scale", [14, 18])
 def test_probe_vector_loads_same_result(scale, monkeypatch):
     """The bottom-up probe reading a vertex's first 8 neighbours by 16-byte loads
-    (CGX_BFS_PROBE_VEC=1, bfs.hip k_bu_probe<VEC>: aligned 12-entry span, padded
-    adjacency) gives the same distances and predecessors as the dword gathers."""
+    (the default, bfs.hip k_bu_probe<VEC>: aligned 12-entry span, padded adjacency)
+    gives the same distances and predecessors as the dword gathers
+    (CGX_BFS_PROBE_VEC=0)."""
     s, d = rmat_sym(scale)
     h, G = make_graph(s, d, None, renumber=True, symmetric=True)
     deg = np.bincount(s)
     srcs = [int(np.argmax(deg)), int(s[len(s) // 3]), int(d[-1])]
+    monkeypatch.setenv("CGX_BFS_PROBE_VEC", "0")
     base = [run(h, G, [x], True) for x in srcs]
-    monkeypatch.setenv("CGX_BFS_PROBE_VEC", "1")
+    monkeypatch.delenv("CGX_BFS_PROBE_VEC")
     for x, (v0, d0, p0) in zip(srcs, base):
         v, dist, pred = run(h, G, [x], True)
         assert h.last_bfs_bottom_up_steps() > 0
