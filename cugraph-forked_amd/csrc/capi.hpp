@@ -128,6 +128,7 @@ struct pr_push_t {
   int64_t nitems = 0;
   int64_t nwin   = 0;
   buffer tile_ctr;     // uint32 queue heads (128 B apart); zero between iterations
+  buffer win_multi;    // uint8[nwin]: 1 = window summed by several items (flushes add), 0 = one item stores it
   int64_t src_head = -1;  // source partition over the XCDs: head size (-1: not partitioned)
 };
 

@@ -441,6 +441,9 @@ struct push_args {
   int64_t qoff[kQueues + 1];
   int64_t nitems;
   unsigned int* tile_ctr;   // queue heads, kCtrStride apart (k_pr_apply resets them)
+  uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
+                            // its sums), 0 = stored whole; nullptr: clear every sum
+  int win_bits;
 };
 
 template <typename T>
@@ -476,17 +479,31 @@ __device__ __forceinline__ unsigned long long fixed_of(R x)
   else return to_fixed((double)x);
 }
 
-// add the LDS window to the global accumulators and clear it
+// push_unit::win of an item's first unit carries kWholeItem when the item is all of
+// its window's units: that window's sums are then stored, not added, and k_pr_apply
+// need not clear them (win_multi)
+constexpr int64_t kWholeItem = int64_t(1) << 40;
+constexpr int64_t kWinMask   = kWholeItem - 1;
+
+// add the LDS window to the global accumulators (or store it: the item is the
+// whole window) and clear it
 template <int WB, typename V, typename E, typename R>
-__device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win)
+__device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
 {
   __syncthreads();
-  unsigned long long* g = sa.acc + (win << WB);
-  for (int i = threadIdx.x; i < (1 << WB); i += kPushThreads) {
-    unsigned long long v = acc[i];
-    if (v) {
-      atomicAdd(g + i, v);
+  unsigned long long* g = sa.acc + ((win_w & kWinMask) << WB);
+  if (win_w & kWholeItem) {
+    for (int i = threadIdx.x; i < (1 << WB); i += kPushThreads) {
+      g[i]   = acc[i];
       acc[i] = 0ull;
+    }
+  } else {
+    for (int i = threadIdx.x; i < (1 << WB); i += kPushThreads) {
+      unsigned long long v = acc[i];
+      if (v) {
+        atomicAdd(g + i, v);
+        acc[i] = 0ull;
+      }
     }
   }
   __syncthreads();
@@ -766,14 +783,14 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
     }
 #pragma unroll
     for (int j = 0; j < kApplyBatch; ++j) {
-      if (f[j]) sa.acc[v + j * stride] = 0ull;
+      if (f[j] && (!sa.win_multi || sa.win_multi[(v + j * stride) >> sa.win_bits])) sa.acc[v + j * stride] = 0ull;
       vertex_update_from<V, E, R>(a, (V)(v + j * stride), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base,
                                   pf, my_diff, my_dang);
     }
   }
   for (; v < a.nv; v += stride) {
     unsigned long long f = sa.acc[v];
-    if (f) sa.acc[v] = 0ull;
+    if (f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
     vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
@@ -1083,6 +1100,28 @@ inline std::vector<int64_t> plan_source_cuts(std::vector<unsigned long long> con
   return none;
 }
 
+// Whole items (all of a window's units): kWholeItem on the item's first unit (the
+// push stores that window's sums), 0 in win_multi (k_pr_apply leaves them)
+inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std::vector<push_unit>& hu,
+                             std::vector<int64_t> const& item_u, int64_t nitems)
+{
+  int64_t const nunits = (int64_t)hu.size();
+  bool const no_whole  = env_is("CGX_PR_WHOLE", "0");  // A/B: every flush adds, the apply clears every sum
+  std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.nwin, 1), 0);
+  for (int64_t i = 0; i < nitems; ++i) {
+    int64_t const u = item_u[i], last = item_u[i + 1] - 1;
+    bool const whole = !no_whole && (u == 0 || hu[u - 1].win != hu[u].win) &&
+                       (last + 1 >= nunits || hu[last + 1].win != hu[u].win);
+    if (whole) hu[u].win |= kWholeItem;
+    else multi[hu[u].win] = 1;
+  }
+  to_device(units, hu.data(), (size_t)nunits, s);
+  pp.win_multi.set_stream(s);
+  pp.win_multi.resize(multi.size());
+  to_device(pp.win_multi.data<uint8_t>(), multi.data(), multi.size(), s);
+  HIP_CHECK(hipStreamSynchronize(s));  // the host vectors go out of scope
+}
+
 inline void upload_items(hipStream_t s, pr_push_t& pp, std::vector<int64_t> const& item_u,
                          std::vector<int64_t> const& queue, int64_t nitems)
 {
@@ -1099,7 +1138,7 @@ inline void upload_items(hipStream_t s, pr_push_t& pp, std::vector<int64_t> cons
 // positions at or before it (0 = head, k + 1 = tail range k); an item is a run of a
 // window's units of one part, split in shares of about tg entries.  Tail items go to
 // queue k, head items (in window order) to the least-loaded queue.
-inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit const* units, int64_t nunits, int64_t ne,
+inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, int64_t ne,
                                 std::vector<int64_t> const& cutpos, int ncut)
 {
   auto hu           = to_host(units, nunits, s);
@@ -1158,11 +1197,12 @@ inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit const* u
       if (iq[i] == q) queue.push_back(i);
   }
   pp.qoff[kQueues] = (int64_t)queue.size();
+  mark_whole_items(s, pp, units, hu, item_u, nitems);
   upload_items(s, pp, item_u, queue, nitems);
 }
 
 // Items and queues over the units (host logic, once per graph)
-inline void build_items(hipStream_t s, pr_push_t& pp, push_unit const* units, int64_t nunits, bool xcd_queues_wanted,
+inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, bool xcd_queues_wanted,
                         std::vector<int64_t> const& cutpos = {}, int ncut = 0)
 {
   int64_t const ne = nunits ? to_host(&units[nunits - 1].k1, 1, s)[0] : 0;
@@ -1228,6 +1268,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit const* units, in
     for (int q = 1; q < kQueues; ++q) pp.qoff[q] = nitems;
   }
   pp.qoff[kQueues] = (int64_t)queue.size();
+  mark_whole_items(s, pp, units, hu, item_u, nitems);
   upload_items(s, pp, item_u, queue, nitems);
 }
 
@@ -1617,6 +1658,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   auto pkernel = push_kernel<V, E, R>(adj.pr, g.weighted, a.enc != 0);
   if (push) {
     set_queue_args(sa, adj.pr, s);
+    sa.win_multi = adj.pr.win_multi.data<uint8_t>();  // single GPU: stored windows are not cleared
+    sa.win_bits  = adj.pr.win_bits;
     nblk_push  = sa.nitems ? kPushBlocks : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
