@@ -15,7 +15,7 @@ import ctypes
 
 from . import _lib
 from ._arrays import (DeviceArray, DeviceView, copy_view_to_tensor, copy_views_to_tensors, optional_view,
-                      to_device_tensor, vptr)
+                      to_device_tensor, views_to_tensors_owned, vptr)
 
 from . import generators  # noqa: E402,F401  (MI355X build extensions)
 from . import comms  # noqa: E402,F401  (multi-GPU communicator contexts)
@@ -187,12 +187,9 @@ class MGGraph(_GPUGraph):
 def _centrality(api, resource_handle, graph, *views_and_scalars):
     res = ctypes.c_void_p()
     _lib.call(api, resource_handle.ptr, graph.c_graph_ptr, *views_and_scalars, ctypes.byref(res))
-    h = resource_handle.ptr
-    try:
-        v, x = copy_views_to_tensors(h, [_lib.lib.cugraph_centrality_result_get_vertices(res),
-                                         _lib.lib.cugraph_centrality_result_get_values(res)])
-    finally:
-        _lib.lib.cugraph_centrality_result_free(res)
+    v, x = views_to_tensors_owned(resource_handle.ptr, [_lib.lib.cugraph_centrality_result_get_vertices(res),
+                                                        _lib.lib.cugraph_centrality_result_get_values(res)],
+                                  res, _lib.lib.cugraph_centrality_result_free)
     return v, x
 
 
@@ -225,13 +222,10 @@ def personalized_pagerank(resource_handle, graph, precomputed_vertex_out_weight_
 
 
 def _paths(resource_handle, res):
-    h = resource_handle.ptr
-    try:
-        v, d, p = copy_views_to_tensors(h, [_lib.lib.cugraph_paths_result_get_vertices(res),
-                                            _lib.lib.cugraph_paths_result_get_distances(res),
-                                            _lib.lib.cugraph_paths_result_get_predecessors(res)])
-    finally:
-        _lib.lib.cugraph_paths_result_free(res)
+    v, d, p = views_to_tensors_owned(resource_handle.ptr, [_lib.lib.cugraph_paths_result_get_vertices(res),
+                                                           _lib.lib.cugraph_paths_result_get_distances(res),
+                                                           _lib.lib.cugraph_paths_result_get_predecessors(res)],
+                                     res, _lib.lib.cugraph_paths_result_free)
     return v, d, p
 
 

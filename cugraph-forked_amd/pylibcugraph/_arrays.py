@@ -123,6 +123,62 @@ def copy_views_to_tensors(handle_ptr, view_ptrs):
     return outs
 
 
+_TYPESTR = {_lib.INT32: "<i4", _lib.INT64: "<i8", _lib.FLOAT32: "<f4", _lib.FLOAT64: "<f8"}
+
+
+class ResultOwner:
+    """Keeps a libcugraph_c result -- and the device arrays it owns -- alive while
+    tensors view its arrays; frees it when the last of them is gone.  The free
+    returns the memory to the library's stream-ordered cache, so the caller's
+    stream is synchronised first: no reader on it can still be running when the
+    library reuses the block."""
+
+    def __init__(self, ptr, free_fn):
+        self.ptr = ptr
+        self._free = free_fn
+
+    def __del__(self, _sd=_lib.SHUTDOWN):
+        if getattr(self, "ptr", None) and not _sd[0]:
+            try:
+                _torch().cuda.current_stream().synchronize()
+            finally:
+                self._free(self.ptr)
+                self.ptr = None
+
+
+class _OwnedDeviceArray:
+    """``__cuda_array_interface__`` over one result array; holds the owner."""
+
+    def __init__(self, owner, ptr, n, c_type):
+        self._owner = owner
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": _TYPESTR[c_type], "data": (ptr, False),
+                                         "strides": None, "version": 3}
+
+
+def views_to_tensors_owned(handle_ptr, view_ptrs, res_ptr, free_fn):
+    """Result views -> GPU torch tensors WITHOUT a copy (the reference's
+    copy_to_cupy_array copies; here the tensors view the library's result arrays and
+    keep the result alive through a ResultOwner).  One stream synchronize; the
+    views are freed, the result is freed when the tensors are."""
+    torch = _torch()
+    owner = ResultOwner(res_ptr, free_fn)
+    outs = []
+    try:
+        _lib.call("cugraph_amd_device_array_views_copy", handle_ptr, 0, None, None)  # handle stream synchronize
+        for v in view_ptrs:
+            c_type = _lib.lib.cugraph_type_erased_device_array_view_type(v)
+            n = _lib.lib.cugraph_type_erased_device_array_view_size(v)
+            ptr = _lib.lib.cugraph_type_erased_device_array_view_pointer(v)
+            if n == 0 or not ptr:
+                outs.append(torch.empty(0, dtype=_torch_dtype(c_type), device="cuda"))
+            else:
+                outs.append(torch.as_tensor(_OwnedDeviceArray(owner, ptr, n, c_type), device="cuda"))
+    finally:
+        for v in view_ptrs:
+            _lib.lib.cugraph_type_erased_device_array_view_free(v)
+    return outs
+
+
 def copy_view_to_numpy(handle_ptr, view_ptr):
     c_type = _lib.lib.cugraph_type_erased_device_array_view_type(view_ptr)
     n = _lib.lib.cugraph_type_erased_device_array_view_size(view_ptr)

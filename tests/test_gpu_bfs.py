@@ -166,3 +166,24 @@ def test_probe_vector_loads_same_result(scale, monkeypatch):
         assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0)
         if scale == 14:
             check_vs_oracle(s, d, v, dist, pred, [x])
+
+
+def test_result_tensors_own_library_memory():
+    """Result tensors view the library's result arrays without a copy
+    (pylibcugraph._arrays.views_to_tensors_owned): they must stay intact across
+    later calls (which allocate from the same cache) and after a derived tensor
+    outlives the original ones."""
+    import gc
+    s, d = rmat_sym(12)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    dist, pred, verts = plc().bfs(h, G, np.asarray([int(s[0])], np.int32), True, 0, True, False)
+    snap = (host(dist).copy(), host(pred).copy(), host(verts).copy())
+    view = dist[1:]  # shares the storage
+    del dist
+    gc.collect()
+    for x in (int(s[5]), int(d[7]), int(s[-1])):
+        plc().bfs(h, G, np.asarray([x], np.int32), True, 0, True, False)
+        plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 100, False)
+    gc.collect()
+    assert np.array_equal(host(view), snap[0][1:])
+    assert np.array_equal(host(pred), snap[1]) and np.array_equal(host(verts), snap[2])
