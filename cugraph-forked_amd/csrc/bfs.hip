@@ -789,6 +789,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // Env overrides are measurement only.
     double const alpha_do = std::getenv("CGX_BFS_ALPHA") ? std::atof(std::getenv("CGX_BFS_ALPHA")) : 40.0;
     double const beta_do  = std::getenv("CGX_BFS_BETA") ? std::atof(std::getenv("CGX_BFS_BETA")) : 64.0;
+    // A/B: mark the visited bits after every top-down level, as before (CGX_BFS_MARK_ALL=1)
+    bool const mark_all = std::getenv("CGX_BFS_MARK_ALL") != nullptr;
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
@@ -859,7 +861,13 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
         n_f = ncur[0] + ncur[1] + ncur[2];
         m_f = hctr->next_m;
-        if (n_f) {
+        // The new frontier's visited bits are needed only by a next top-down level: a
+        // next bottom-up level marks them with its frontier bitmap (queues -> bitmap
+        // above), and after the last level nothing reads them
+        unsigned long long const m_u_next = m_u > m_f ? m_u - m_f : 0;
+        bool const next_bu   = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
+        bool const last      = n_f == 0 || depth + 1 >= limit;
+        if (mark_all ? n_f > 0 : (!last && !next_bu)) {
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
                              ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], vis.data(), nullptr);
           CGX_LAUNCH_CHECK();
