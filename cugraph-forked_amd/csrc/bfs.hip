@@ -39,7 +39,7 @@ constexpr int kMidDeg   = 1024;  // one wave; above: edge chunks over blocks
 constexpr int kChunk    = 2048;  // edges per large-class chunk
 
 struct bfs_ctr {
-  unsigned long long qlen[3];  // next queues: small / mid / large
+  unsigned long long qlen[3];  // next queues: small / mid / large (first: bfs_args::ncur_dev points here)
   unsigned long long next_n;   // vertices discovered this level
   unsigned long long next_m;   // sum of their degrees
   unsigned long long pad[3];
@@ -116,6 +116,7 @@ struct bfs_args {
   uint32_t* nxt;  // bottom-up: next frontier bitmap
   V const* qcur[3];
   unsigned long long ncur[3];
+  unsigned long long const* ncur_dev;  // if set: the current queue lengths, read on the device (ncur: bounds)
   V* qnext[3];
   bfs_ctr* ctr;
   V depth;  // distance of the current frontier
@@ -235,6 +236,9 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
   unsigned long long my_m = 0, my_n = 0;
   long long b = blockIdx.x;
   int tid     = threadIdx.x;
+  unsigned long long const n0 = a.ncur_dev ? a.ncur_dev[0] : a.ncur[0];
+  unsigned long long const n1 = a.ncur_dev ? a.ncur_dev[1] : a.ncur[1];
+  unsigned long long const n2 = a.ncur_dev ? a.ncur_dev[2] : a.ncur[2];
   if (b < a.blk_mid_start) {
     // large class, edge-parallel: every vertex's row is cut into kChunk-edge chunks
     // and the blocks stride over the global chunk index (a root of degree 4e5 would
@@ -244,7 +248,7 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
     for (long long c = b;; c += nb) {
       V u = 0;
       E beg = 0, end = 0;
-      while (i < (long long)a.ncur[2]) {
+      while (i < (long long)n2) {
         u   = a.qcur[2][i];
         beg = a.off[u];
         end = a.off[u + 1];
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
         chunk_base += nch;
         ++i;
       }
-      if (i >= (long long)a.ncur[2]) break;
+      if (i >= (long long)n2) break;
       E cb = beg + (E)((c - chunk_base) * kChunk);
       E ce = cb + (E)kChunk < end ? cb + (E)kChunk : end;
       for (E base = cb; base < ce; base += 256) {
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
     long long nb   = a.blk_small_start - a.blk_mid_start;
     long long widx = (b - a.blk_mid_start) * 4 + (tid >> 6);
     int lane       = tid & 63;
-    for (long long i = widx; i < (long long)a.ncur[1]; i += nb * 4) {
+    for (long long i = widx; i < (long long)n1; i += nb * 4) {
       V u   = a.qcur[1][i];
       E beg = a.off[u], end = a.off[u + 1];
       for (E base = beg; base < end; base += 64) {
@@ -282,9 +286,9 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
     long long g   = (b - a.blk_small_start) * 64 + (tid >> 2);
     int lane      = tid & 3;
     // all 4 lanes of a group share u; lanes of a wave run the same trip count (<= 4 rounds)
-    for (long long i0 = (b - a.blk_small_start) * 64; i0 < (long long)a.ncur[0]; i0 += nb * 64) {
+    for (long long i0 = (b - a.blk_small_start) * 64; i0 < (long long)n0; i0 += nb * 64) {
       long long i = i0 + (tid >> 2);
-      bool have   = i < (long long)a.ncur[0];
+      bool have   = i < (long long)n0;
       V u         = have ? a.qcur[0][i] : V(0);
       E beg = have ? a.off[u] : E(0), end = have ? a.off[u + 1] : E(0);
       for (int r = 0; r < kSmallDeg / 4; ++r) {
@@ -688,7 +692,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     qa[c].resize(nv, s);
     qb[c].resize(nv, s);
   }
-  dbuf<bfs_ctr> ctr(1, s);
+  dbuf<bfs_ctr> ctr(1, s), ctr2(1, s);  // ctr2: queue lengths of a bitmap -> queues conversion
   bfs_ctr* hctr = h.pinned_as<bfs_ctr>();
 
   bfs_args<V, E> a{};
@@ -791,6 +795,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     double const beta_do  = std::getenv("CGX_BFS_BETA") ? std::atof(std::getenv("CGX_BFS_BETA")) : 64.0;
     // A/B: mark the visited bits after every top-down level, as before (CGX_BFS_MARK_ALL=1)
     bool const mark_all = std::getenv("CGX_BFS_MARK_ALL") != nullptr;
+    // A/B: read the queue lengths of a bitmap -> queues conversion on the host (CGX_BFS_CONV_SYNC=1)
+    bool const conv_sync = std::getenv("CGX_BFS_CONV_SYNC") != nullptr;
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
@@ -829,7 +835,21 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         m_f = hctr->next_m;
         ++bu_steps;
       } else {
-        if (!have_queue) {  // frontier bitmap -> queues
+        if (!have_queue && poll && !conv_sync) {
+          // frontier bitmap -> queues with no host round trip: the conversion counts
+          // into ctr2, k_topdown reads the queue lengths from there and the grid is
+          // sized for all n_f frontier vertices in every degree class
+          for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
+          HIP_CHECK(hipMemsetAsync(ctr2.data(), 0, sizeof(bfs_ctr), s));
+          bfs_args<V, E> ac = a;
+          ac.ctr            = ctr2.data();
+          hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s,
+                             ac, fr.data(), nwords);
+          CGX_LAUNCH_CHECK();
+          for (int c = 0; c < 3; ++c) ncur[c] = n_f;
+          a.ncur_dev = reinterpret_cast<unsigned long long const*>(ctr2.data());  // bfs_ctr::qlen, offset 0
+          have_queue = true;
+        } else if (!have_queue) {  // frontier bitmap -> queues
           for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
           hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s,
                              a, fr.data(), nwords);
@@ -857,6 +877,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           hipLaunchKernelGGL((k_topdown<V, E>), dim3(grid), dim3(kBlock), 0, s, a);
           CGX_LAUNCH_CHECK();
         }
+        a.ncur_dev = nullptr;
         read_ctr();
         for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
         n_f = ncur[0] + ncur[1] + ncur[2];
