@@ -414,6 +414,15 @@ inline bool env_is(char const* name, char const* value)
   return e && std::string(e) == value;
 }
 
+// items per push block on average (a window larger than 1.5 x E / (kPushBlocks x this)
+// is cut into shares); CGX_PR_SHARE_DIV overrides (measurement only)
+inline int64_t item_share_div()
+{
+  char const* e = std::getenv("CGX_PR_SHARE_DIV");
+  int64_t const d = e ? std::atoll(e) : 0;
+  return d > 0 ? d : 4;
+}
+
 inline bool packed_enabled()
 {
   char const* e = std::getenv("CGX_PR_PACKED");
@@ -1218,7 +1227,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   // measured 0.199 -> 0.216, the last groups' imbalance outweighing the L2 hits).
   auto hu = to_host(units, nunits, s);
   bool const xcd_queues = xcd_queues_wanted;
-  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * 4));
+  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * item_share_div()));
   std::vector<int64_t> item_u, item_e;
   for (int64_t u0 = 0; u0 < nunits;) {
     int64_t u1 = u0;
