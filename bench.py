@@ -131,13 +131,18 @@ def omp_threads():
 # ----------------------------------------------------------------------------- graphs
 def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want_roots=0, mg=None):
     """Device R-MAT -> symmetrise + dedup (cugraph.Graph preprocessing) -> graph.
+    weighted: False (no weights at the C ABI), True (uniform [0, 1) fp32, seed + 1) or
+    "ones" (all-ones fp32, the reference Python path's unweighted graph).
     mg = (rank, world): every rank makes the same edge list and passes its slice to
     the collective MGGraph build."""
     import numpy as np
     import torch
     n = 16 << scale
     s, d = p.generators.generate_rmat_edgelist(h, scale, n, 0.57, 0.19, 0.19, seed, False, True)
-    w = p.generators.generate_edge_weights(h, n, seed + 1) if weighted else None
+    if weighted == "ones":  # what cugraph.Graph attaches to an unweighted edge list (simpleGraph.py:840-843)
+        w = torch.ones(n, dtype=torch.float32, device=s.device)
+    else:
+        w = p.generators.generate_edge_weights(h, n, seed + 1) if weighted else None
     s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
     props = p.GraphProperties(is_symmetric=True, is_multigraph=False)
     roots, deg = None, None
@@ -348,7 +353,7 @@ def bfs_leg(p, args, child=False):
     if deg is None:  # SG: degrees from the CSR (internal order == result order)
         off, _, _ = g.adjacency(h, transposed=False)
         deg_int = (off[1:] - off[:-1]).to(torch.int64)
-    rates, stored, levels, bu, times, bytes_alg = [], [], [], [], [], []
+    rates, stored, levels, bu, times, bytes_alg, spread = [], [], [], [], [], [], []
     number_map = None
     for r in roots:
         mine = [int(r)] if args.rank == 0 else []
@@ -357,13 +362,19 @@ def bfs_leg(p, args, child=False):
             p.bfs(h, g, src.clone(), True, 0, True, False)
             continue
         p.bfs(h, g, src.clone(), True, 0, True, False)  # warm
-        torch.cuda.synchronize()
-        barrier(args)
-        t0 = time.perf_counter()
-        dist, pred, verts = p.bfs(h, g, src.clone(), True, 0, True, False)
-        torch.cuda.synchronize()
-        barrier(args)
-        t = max_over_ranks(args, time.perf_counter() - t0)
+        samples, res = [], None
+        for _ in range(args.bfs_reps):
+            res = None  # the previous result's free (a device synchronize) stays off the clock
+            s_in = src.clone()
+            torch.cuda.synchronize()
+            barrier(args)
+            t0 = time.perf_counter()
+            res = p.bfs(h, g, s_in, True, 0, True, False)
+            torch.cuda.synchronize()
+            barrier(args)
+            samples.append(max_over_ranks(args, time.perf_counter() - t0))
+        dist, pred, verts = res
+        t = sorted(samples)[len(samples) // 2]  # median of the root's traversals
         reached = dist < 2**31 - 1
         # Graph500 TEPS: undirected edges of the source's component = stored directed edges / 2
         if deg is None:
@@ -375,6 +386,7 @@ def bfs_leg(p, args, child=False):
         if number_map is None and deg is None:
             number_map = verts.cpu().numpy()  # internal id -> external id (SG)
         times.append(t)
+        spread.append((min(samples), max(samples)))
         levels.append(h.last_bfs_levels())
         bu.append(h.last_bfs_bottom_up_steps())
         rates.append((e_cc / 2) / t / 1e6)
@@ -388,7 +400,12 @@ def bfs_leg(p, args, child=False):
     out = {"scale": scale, "vertices": V, "edges": E, "roots": len(rates),
            "mteps_harmonic_mean": hm, "mteps_min": min(rates), "mteps_max": max(rates),
            "stored_edge_mteps_harmonic_mean": hm_stored,
-           "ms_mean": 1e3 * sum(times) / len(times), "levels": levels, "bottom_up_steps": bu,
+           "ms_mean": 1e3 * sum(times) / len(times), "ms_per_root_median": [round(1e3 * x, 4) for x in times],
+           "ms_per_root_min_max": [[round(1e3 * a, 4), round(1e3 * b, 4)] for a, b in spread],
+           "reps_per_root": args.bfs_reps,
+           "timing": "median of reps_per_root timed traversals per root (after one warm traversal); MTEPS per root "
+                     "from its median, harmonic mean over the roots",
+           "levels": levels, "bottom_up_steps": bu,
            "direction_optimizing": True, "n_gpus": args.world,
            "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)",
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -460,6 +477,30 @@ def grid_name(args, C):
             f"{'RCCL' if args.comm == 'rccl' else 'torch.distributed/gloo'}")
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_command(n, argv, port):
+    """The torch.distributed.run command line of an N-rank run of this script."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """Start N ranks as a child process group (never exec: the parent has not
+    touched the GPU, but a child keeps that true by construction); rank 0's JSON
+    line reaches our stdout through the inherited descriptor."""
+    cmd = launch_command(n, argv, free_port())
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -475,6 +516,7 @@ def main():
     ap.add_argument("--no-bfs", dest="bfs", action="store_false")
     ap.add_argument("--bfs-scale", type=int, default=24)
     ap.add_argument("--bfs-roots", type=int, default=8)
+    ap.add_argument("--bfs-reps", type=int, default=5, help="timed traversals per root (median reported)")
     ap.add_argument("--louvain", dest="louvain", action="store_true", default=True)
     ap.add_argument("--no-louvain", dest="louvain", action="store_false")
     ap.add_argument("--louvain-scale", type=int, default=None, help="default 23 + log2(N): RMAT-26 at 8 GPUs")
@@ -493,7 +535,14 @@ def main():
     ap.add_argument("--louvain-only", action="store_true", help="A/B aid: only the Louvain leg, its dict on stdout")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one command, N ranks (benchmarks/python_e2e/main.py:72-79 starts one worker
+        # per GPU itself): run torch.distributed.run as a CHILD before anything here
+        # touches the GPU, relay its output and exit code
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     grow = int(round(math.log2(max(world, 1))))
     if args.louvain_scale is None:

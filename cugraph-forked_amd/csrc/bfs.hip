@@ -57,8 +57,11 @@ __global__ void k_publish_ctr(bfs_ctr const* ctr, bfs_ctr* host)
 
 // the level counters (then zeroed for the next level: no memset launch per level)
 // and the source check flag (pad[1]), then seq (the host's poll word, pad[0]) behind
-// a system fence
-__global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr* host, unsigned long long seq, int const* bad)
+// a system fence.  ctr_b: a second level's counters (a speculative top-down level)
+// -> host[1], also zeroed; src_m: the sources' edge count of a conversion the host
+// did not read (bfs_ctr::next_m of that block) -> pad[2]
+__global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr* host, unsigned long long seq, int const* bad, bfs_ctr* ctr_b,
+                              bfs_ctr const* src_m)
 {
   if (threadIdx.x != 0) return;
   unsigned long long* c  = reinterpret_cast<unsigned long long*>(ctr);
@@ -67,6 +70,15 @@ __global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr* host, unsigned long long se
     __hip_atomic_store(hp + i, c[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     c[i] = 0ull;
   }
+  if (ctr_b) {
+    unsigned long long* cb = reinterpret_cast<unsigned long long*>(ctr_b);
+    unsigned long long* hb = reinterpret_cast<unsigned long long*>(host + 1);
+    for (int i = 0; i < 5; ++i) {
+      __hip_atomic_store(hb + i, cb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      cb[i] = 0ull;
+    }
+  }
+  __hip_atomic_store(&host->pad[2], src_m ? src_m->next_m : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&host->pad[1], bad ? (unsigned long long)*bad : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();
   __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -305,11 +317,17 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
   flush_counts(a.ctr, 0, my_m);
 }
 
-// mark the next queues as visited (their distances were set by the claim)
+// mark the next queues as visited (their distances were set by the claim);
+// cdev: read the queue lengths on the device (a level the host has not read yet)
 template <typename V>
 __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, unsigned long long n1, V const* q2,
-                              unsigned long long n2, uint32_t* vis, uint32_t* fr)
+                              unsigned long long n2, uint32_t* vis, uint32_t* fr, bfs_ctr const* cdev = nullptr)
 {
+  if (cdev) {
+    n0 = cdev->qlen[0];
+    n1 = cdev->qlen[1];
+    n2 = cdev->qlen[2];
+  }
   unsigned long long tot = n0 + n1 + n2;
   for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < tot;
        i += (unsigned long long)gridDim.x * blockDim.x) {
@@ -620,6 +638,30 @@ __global__ void k_finish_pred(V* pred, size_t n, V none, V const* nmap)
   }
 }
 
+// 4-byte ids: four predecessors per lane through one 16-byte load and store
+// (RMAT-24: 8.9M predecessors, 35 MB each way plus the number-map gathers)
+__global__ __launch_bounds__(256) void k_finish_pred4(int* pred, size_t n, int none, int const* nmap)
+{
+  typedef int v4_t __attribute__((ext_vector_type(4)));
+  size_t const nq     = n / 4;
+  size_t const stride = (size_t)gridDim.x * blockDim.x;
+  v4_t* p4            = reinterpret_cast<v4_t*>(pred);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nq; i += stride) {
+    v4_t p = __builtin_nontemporal_load(p4 + i);
+    int const q0 = p.x == none ? -1 : (nmap ? nmap[p.x] : p.x);
+    int const q1 = p.y == none ? -1 : (nmap ? nmap[p.y] : p.y);
+    int const q2 = p.z == none ? -1 : (nmap ? nmap[p.z] : p.z);
+    int const q3 = p.w == none ? -1 : (nmap ? nmap[p.w] : p.w);
+    p = v4_t{q0, q1, q2, q3};
+    __builtin_nontemporal_store(p, p4 + i);
+  }
+  size_t const t = nq * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t < n) {
+    int const q = pred[t];
+    pred[t]     = q == none ? -1 : (nmap ? nmap[q] : q);
+  }
+}
+
 // dist / pred = INF and the three bitmaps cleared in one launch (was 2 fills + 3 memsets)
 template <typename V>
 __global__ void k_bfs_setup(V* dist, V* pred, int64_t nv, V inf, uint32_t* vis, uint32_t* fr, uint32_t* nxt,
@@ -692,7 +734,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     qa[c].resize(nv, s);
     qb[c].resize(nv, s);
   }
-  dbuf<bfs_ctr> ctr(1, s), ctr2(1, s);  // ctr2: queue lengths of a bitmap -> queues conversion
+  // ctr2: queue lengths of a bitmap -> queues conversion; ctr3: a speculative level's counters
+  dbuf<bfs_ctr> ctr(1, s), ctr2(1, s), ctr3(1, s);
   bfs_ctr* hctr = h.pinned_as<bfs_ctr>();
 
   bfs_args<V, E> a{};
@@ -717,10 +760,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // memcpy + synchronize form, A/B)
   bool const poll = std::getenv("CGX_BFS_SYNC") == nullptr && !ctr_memcpy;
   bfs_ctr* pctr   = poll ? h.polled_as<bfs_ctr>() : nullptr;
-  auto read_ctr = [&](int const* bad_flag = nullptr) {
+  // ctr_b / src_m: see k_publish_seq (poll mode only)
+  auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr const* src_m = nullptr) {
     if (poll) {
       unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
-      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag);
+      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m);
       CGX_LAUNCH_CHECK();
       for (unsigned long long n = 1; __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) != seq; ++n) {
         __builtin_ia32_pause();
@@ -754,15 +798,51 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: sources have invalid vertex IDs.");
     zero_ctr();
     for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
-    hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, a,
-                       fr.data(), nwords);
-    CGX_LAUNCH_CHECK();
-    read_ctr(bad.data());
-    if (poll) CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
-    unsigned long long ncur[3] = {hctr->qlen[0], hctr->qlen[1], hctr->qlen[2]};
-    unsigned long long n_f = ncur[0] + ncur[1] + ncur[2];
-    unsigned long long m_f = hctr->next_m;
-    unsigned long long m_u = (unsigned long long)g.num_edges - m_f;
+    // Level 0 is certainly top-down when even every source at the maximum degree
+    // stays below the switch rule: then the source counts are not read here -- level
+    // 0 takes its queue lengths on the device (as after a bitmap -> queues
+    // conversion) and the source check and the sources' edge count come back with
+    // level 0's counters (one host round trip fewer)
+    double const alpha_do = std::getenv("CGX_BFS_ALPHA") ? std::atof(std::getenv("CGX_BFS_ALPHA")) : 40.0;
+    bool const spec_ok    = poll && std::getenv("CGX_BFS_NO_SPEC") == nullptr;  // A/B: read every level
+    bool quick_start      = false;
+    if (spec_ok && std::getenv("CGX_BFS_CONV_SYNC") == nullptr && adj.degree_sorted) {
+      if (adj.max_degree < 0) {
+        E o[2];
+        HIP_CHECK(hipMemcpyAsync(o, adj.offsets.data<E>(), sizeof(o), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        adj.max_degree = (int64_t)(o[1] - o[0]);  // vertex 0 has the largest degree
+      }
+      double const m_src = (double)sources->size * (double)adj.max_degree;
+      quick_start        = !dir_opt || m_src <= ((double)g.num_edges - m_src) / alpha_do;
+    }
+    unsigned long long ncur[3];
+    unsigned long long n_f, m_f, m_u;
+    bool pending_src = false;  // level 0's read also returns the source check and the sources' edge count
+    if (quick_start) {
+      HIP_CHECK(hipMemsetAsync(ctr2.data(), 0, sizeof(bfs_ctr), s));
+      bfs_args<V, E> ac = a;
+      ac.ctr            = ctr2.data();
+      hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, ac,
+                         fr.data(), nwords);
+      CGX_LAUNCH_CHECK();
+      for (int c = 0; c < 3; ++c) ncur[c] = sources->size;  // bounds: the grid covers every class
+      a.ncur_dev = reinterpret_cast<unsigned long long const*>(ctr2.data());
+      n_f        = sources->size;
+      m_f        = 0;  // counted into m_u when level 0's counters come back
+      m_u        = (unsigned long long)g.num_edges;
+      pending_src = true;
+    } else {
+      hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, a,
+                         fr.data(), nwords);
+      CGX_LAUNCH_CHECK();
+      read_ctr(bad.data());
+      if (poll) CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
+      for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
+      n_f = ncur[0] + ncur[1] + ncur[2];
+      m_f = hctr->next_m;
+      m_u = (unsigned long long)g.num_edges - m_f;
+    }
     bool bottom_up  = false;
     bool have_queue = true;  // frontier available as queues (qa); else as bitmap fr
     bool have_bitmap = false; // frontier bitmap fr valid (else fr is all zero: k_bitmap_to_queues clears it)
@@ -791,7 +871,6 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // (alpha, beta): (4, 24) 135K; (14, 24) 211K; (14, 64) 218K; (40, 24) 224K;
     // (40, 64) 226K; (80, 64) 223K; (80, 128) 225K; (150, 64) 209K.
     // Env overrides are measurement only.
-    double const alpha_do = std::getenv("CGX_BFS_ALPHA") ? std::atof(std::getenv("CGX_BFS_ALPHA")) : 40.0;
     double const beta_do  = std::getenv("CGX_BFS_BETA") ? std::atof(std::getenv("CGX_BFS_BETA")) : 64.0;
     // A/B: mark the visited bits after every top-down level, as before (CGX_BFS_MARK_ALL=1)
     bool const mark_all = std::getenv("CGX_BFS_MARK_ALL") != nullptr;
@@ -878,7 +957,76 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           CGX_LAUNCH_CHECK();
         }
         a.ncur_dev = nullptr;
-        read_ctr();
+        // Speculative next level: once a bottom-up phase is over the frontier only
+        // shrinks, so the level after this one is launched top-down before this one's
+        // counters are read (its queue lengths read on the device, its grid that of
+        // this level, every class at least one segment), and both levels come back
+        // with one host round trip.  Results do not depend on the direction schedule
+        // (smallest-id parent either way), so a wrong guess costs time only.
+        bool const spec = spec_ok && bu_steps > 0 && !pending_src && depth + 1 < limit;
+        if (spec) {
+          // this level's new frontier is the next level's visited set
+          hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
+                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data());
+          CGX_LAUNCH_CHECK();
+          HIP_CHECK(hipMemsetAsync(ctr3.data(), 0, sizeof(bfs_ctr), s));
+          bfs_args<V, E> b = a;
+          b.depth          = (V)(depth + 1);
+          b.ctr            = ctr3.data();
+          b.ncur_dev       = reinterpret_cast<unsigned long long const*>(ctr.data());
+          for (int c = 0; c < 3; ++c) {
+            b.qcur[c]  = qb[c].data();
+            b.qnext[c] = qa[c].data();
+          }
+          long long const sl = std::max(nb_large, 8ll), sm = std::max(nb_mid, 8ll), ss = std::max(nb_small, 8ll);
+          b.blk_mid_start    = sl;
+          b.blk_small_start  = sl + sm;
+          hipLaunchKernelGGL((k_topdown<V, E>), dim3(sl + sm + ss), dim3(kBlock), 0, s, b);
+          CGX_LAUNCH_CHECK();
+          read_ctr(nullptr, ctr3.data());
+          bfs_ctr const l2 = pctr[1];
+          unsigned long long const n1 = hctr->qlen[0] + hctr->qlen[1] + hctr->qlen[2];
+          unsigned long long const m1 = hctr->next_m;
+          if (dbg)
+            std::fprintf(stderr, "[bfs] level %d top-down n_f=%llu m_f=%llu m_u=%llu (speculated next)\n", (int)depth,
+                         n1, m1, m_u);
+          m_u = m_u > m1 ? m_u - m1 : 0;
+          ++depth;
+          ++levels;
+          // the speculative level (empty when this one found nothing): its output is in qa
+          for (int c = 0; c < 3; ++c) ncur[c] = l2.qlen[c];
+          n_f = ncur[0] + ncur[1] + ncur[2];
+          m_f = l2.next_m;
+          if (n1 == 0) {  // nothing was discovered: the traversal is over
+            n_f = 0;
+            m_f = 0;
+            break;
+          }
+          unsigned long long const m_u_next = m_u > m_f ? m_u - m_f : 0;
+          bool const next_bu = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
+          bool const last    = n_f == 0 || depth + 1 >= limit;
+          if (mark_all ? n_f > 0 : (!last && !next_bu)) {
+            hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s,
+                               qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(),
+                               nullptr);
+            CGX_LAUNCH_CHECK();
+          }
+          have_bitmap = false;
+          if (dbg)
+            std::fprintf(stderr, "[bfs] level %d top-down n_f=%llu m_f=%llu m_u=%llu (speculative)\n", (int)depth,
+                         n_f, m_f, m_u);
+          m_u = m_u > m_f ? m_u - m_f : 0;
+          ++depth;
+          ++levels;
+          continue;
+        }
+        read_ctr(pending_src ? bad.data() : nullptr, nullptr, pending_src ? ctr2.data() : nullptr);
+        if (pending_src) {  // level 0 also brought back the source check and the sources' edge count
+          CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
+          unsigned long long const m_src = pctr->pad[2];
+          m_u         = m_u > m_src ? m_u - m_src : 0;
+          pending_src = false;
+        }
         for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
         n_f = ncur[0] + ncur[1] + ncur[2];
         m_f = hctr->next_m;
@@ -904,12 +1052,27 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       ++depth;
       ++levels;
     }
+    if (pending_src) {  // no level ran (depth limit 0): the source check is still owed
+      read_ctr(bad.data());
+      CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
+    }
     h.last_bfs_levels    = levels;
     h.last_bfs_bottom_up = bu_steps;
   } catch (...) {
     throw;
   }
   if (pred) {
+    bool const vec4 = sizeof(V) == 4 && (reinterpret_cast<uintptr_t>(pred) & 15) == 0 &&
+                      std::getenv("CGX_BFS_PRED_SCALAR") == nullptr;  // A/B
+    if constexpr (sizeof(V) == 4) {
+      if (vec4) {
+        hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 3) / 4, kBlock, 16384)), dim3(kBlock), 0, s,
+                           reinterpret_cast<int*>(pred), (size_t)nv, (int)INF,
+                           g.renumbered ? g.number_map.data<int>() : (int const*)nullptr);
+        CGX_LAUNCH_CHECK();
+        return;
+      }
+    }
     hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for((nv + 3) / 4, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF,
                        g.renumbered ? g.number_map.data<V>() : (V const*)nullptr);
     CGX_LAUNCH_CHECK();

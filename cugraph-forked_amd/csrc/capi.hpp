@@ -34,6 +34,7 @@ struct handle_t {
   size_t last_bfs_levels     = 0;
   size_t last_bfs_bottom_up  = 0;
   size_t last_louvain_levels = 0;
+  double last_louvain_sweep_bytes = 0;  // MG: average bytes sent per sweep by this rank
   // Host-pinned scratch for the per-level / per-chunk device state reads and a pool
   // of profiling events, both kept for the handle's lifetime: hipHostMalloc +
   // hipHostFree per call measured ~250 us of host stall per BFS traversal.
@@ -120,7 +121,8 @@ struct pr_push_t {
   buffer seg_base;     // uint32[nunits * 16]: running source before each 512-entry wave segment
   buffer units;        // push_unit[nunits], in (window, source) order
   int64_t nunits = 0;
-  buffer acc;          // u64[nacc] fixed-point sums by row, zero between iterations
+  buffer acc;          // u64[nacc] fixed-point sums by row; windows stored whole by one item are
+                       // overwritten each iteration, the others (win_multi) are cleared by the apply
   int64_t nacc = 0;
   buffer items;        // int64[nitems + 1]: first unit of every item (a window or a share of one)
   buffer queue;        // int64[nitems]: item ids of queue 0, 1, ..., 7
@@ -142,6 +144,7 @@ struct adjacency_t {
   bool idx_padded = false;
   // degree-binned schedule (built on first use, see schedule.hpp)
   bool degree_sorted = false;  // majors already in descending-degree order (renumbered build)
+  int64_t max_degree = -1;     // cached on first use (BFS), -1 = not known yet
   bool sched_valid   = false;
   buffer order;                         // vertex_t[V] processing order if !degree_sorted
   std::vector<int64_t> bin_begin;       // positions (in processing order) where each bin starts

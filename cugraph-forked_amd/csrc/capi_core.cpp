@@ -506,5 +506,9 @@ extern "C" size_t cugraph_amd_last_louvain_levels(const cugraph_resource_handle_
 {
   return H(handle)->last_louvain_levels;
 }
+extern "C" double cugraph_amd_last_louvain_sweep_bytes(const cugraph_resource_handle_t* handle)
+{
+  return H(handle)->last_louvain_sweep_bytes;
+}
 extern "C" size_t cugraph_amd_trim_device_cache(void) { return cgx::device_cache_trim(); }
 extern "C" const char* cugraph_amd_version(void) { return "cugraph-forked_amd libcugraph_c gfx950 " __DATE__; }

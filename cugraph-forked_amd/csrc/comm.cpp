@@ -76,8 +76,15 @@ template <typename T>
 dbuf<T> exchange(comm_t& comm, T const* send, std::vector<size_t> const& counts, std::vector<size_t>& rcounts,
                  hipStream_t st)
 {
-  int P   = comm.size;
   rcounts = exchange_counts(comm, counts, st);
+  return exchange_known<T>(comm, send, counts, rcounts, st);
+}
+
+template <typename T>
+dbuf<T> exchange_known(comm_t& comm, T const* send, std::vector<size_t> const& counts,
+                       std::vector<size_t> const& rcounts, hipStream_t st)
+{
+  int P = comm.size;
   std::vector<size_t> sd(P), rd(P);
   size_t tot = 0;
   for (int q = 0; q < P; ++q) {
@@ -91,6 +98,18 @@ dbuf<T> exchange(comm_t& comm, T const* send, std::vector<size_t> const& counts,
   out.n = tot;
   return out;
 }
+
+#define CGX_EXCHANGE_KNOWN(T)                                                                                \
+  template dbuf<T> exchange_known<T>(comm_t&, T const*, std::vector<size_t> const&, std::vector<size_t> const&, \
+                                     hipStream_t);
+CGX_EXCHANGE_KNOWN(int32_t)
+CGX_EXCHANGE_KNOWN(int64_t)
+CGX_EXCHANGE_KNOWN(float)
+CGX_EXCHANGE_KNOWN(double)
+CGX_EXCHANGE_KNOWN(uint32_t)
+CGX_EXCHANGE_KNOWN(unsigned long long)
+CGX_EXCHANGE_KNOWN(long long)
+#undef CGX_EXCHANGE_KNOWN
 
 template dbuf<int32_t> exchange<int32_t>(comm_t&, int32_t const*, std::vector<size_t> const&, std::vector<size_t>&,
                                          hipStream_t);

@@ -80,6 +80,12 @@ template <typename T>
 dbuf<T> exchange(comm_t& comm, T const* send, std::vector<size_t> const& counts, std::vector<size_t>& rcounts,
                  hipStream_t st);
 
+// The same with the receive counts already known (a reply to an exchange: its
+// send counts are the request's receive counts), so no count exchange is needed.
+template <typename T>
+dbuf<T> exchange_known(comm_t& comm, T const* send, std::vector<size_t> const& counts,
+                       std::vector<size_t> const& rcounts, hipStream_t st);
+
 // recv counts from send counts (every rank's count vector)
 std::vector<size_t> exchange_counts(comm_t& comm, std::vector<size_t> const& counts, hipStream_t st);
 

@@ -1022,6 +1022,7 @@ struct louvain_state {
   comm_t* comm = nullptr;  // multi-GPU: the world communicator; nullptr on one GPU
   dbuf<double> scratch;    // device_sum partials
   dbuf<double> scal;       // 2 scalars
+  size_t bytes = 0;        // multi-GPU: bytes this rank sent in the exchanges being counted
   explicit louvain_state(hipStream_t st) : s(st), scratch(1024, st), scal(2, st) {}
 };
 
@@ -1573,32 +1574,47 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
 // ================================================================ multi-GPU
 //
 // Reference: louvain_impl.cuh:46-237 with multi_gpu = true, the MG branches of
-// common_methods.cuh:200-382 (cluster weights shuffled to the key owner, the
-// neighbour clusters' weights collected from their owners) and
-// coarsen_graph_impl.cuh:243-516 (coarse edges shuffled to the owner of their
-// source, renumbered per owner).  The MI355X layout:
+// common_methods.cuh:200-382 (cluster weights kept at the key owner,
+// louvain_impl.cuh:91-103; the neighbour clusters' weights collected from their
+// owners, per_v_transform_reduce_dst_key_aggregated_outgoing_e.cuh:506-611,736-753)
+// and coarsen_graph_impl.cuh:243-516 (coarse edges shuffled to the owner of their
+// source, renumbered per owner).  The MI355X layout (owner-sharded, no O(V) state
+// or collective per rank):
 //
 //  * rows: every rank holds the out-edges of the vertices it owns ([voff[p],
 //    voff[p+1]) of the level's global ids, a 1D partition by source owner),
-//    sorted by (row, destination) with fp64 weights;
-//  * the clustering c, the cluster weights a and the present flags are dense
-//    arrays over all of the level's ids on every rank (4 + 8 + 1 bytes per vertex:
-//    1 GB at RMAT-26 against 288 GB of HBM).  A sweep runs the single-GPU local
-//    move on the rank's rows, then one allgather of the moved rows' clusters and
-//    one SUM / MAX allreduce of the per-rank cluster-weight partials re-replicate
-//    them -- no per-edge exchange at all;
-//  * modularity: per-rank partials (own edges, own cluster-id range) + a 2-double
-//    allreduce, so every rank takes the same branch of the level loop;
+//    sorted by (row, destination) with fp64 weights.  Per level the destinations
+//    become local ids: own rows [0, nr), then the ghosts (distinct remote
+//    destinations, sorted), so the single-GPU sweep kernels run unchanged;
+//  * clusters: every rank keeps the clusters of its rows and of its ghosts; the
+//    owners know which of their rows each rank mirrors (one exchange per level);
+//  * cluster weights: at the owner of the cluster id, in 64-bit fixed point (scale
+//    2^(60 - e), total weight < 2^e: integer adds, order-free and exact for
+//    integer weights), with a count of members that have edges (present flag);
+//  * a sweep: the referenced clusters (own rows' and ghosts') are collected from
+//    their owners (keys out, values back), the single-GPU local move runs on local
+//    cluster ids (order-preserving, so the tie rule on cluster ids is unchanged);
+//    then the moved rows send (old, -k) / (new, +k) to the cluster owners and the
+//    owners send the moved rows' new clusters to the ranks that mirror them.
+//    Per-sweep traffic per rank: O(referenced clusters + moved rows + their
+//    mirrors), reported per sweep (CGX_LOUVAIN_TRACE) and as the handle statistic
+//    last_louvain_sweep_bytes;
+//  * modularity: per-rank partials (own internal weight, own cluster ids' a_c^2)
+//    and a 2-double allreduce, so every rank takes the same branch of the level
+//    loop;
 //  * contraction: coarse pairs (label(u), label(v)) are reduced locally, sent to
-//    the owner of label(u) with one all-to-all and merged there; each owner numbers
-//    its used labels by descending coarse degree (ties: ascending label), the
-//    owners' ranges stay contiguous, and a dense label -> new id table is
-//    allgathered.
+//    the owner of label(u) and merged there; each owner numbers its used labels by
+//    descending coarse degree (ties: ascending label), the owners' ranges stay
+//    contiguous, and the new ids of label(v) and of the rows' labels are collected
+//    from their owners (no dense label table);
+//  * flatten: each level's owners answer for the ids the owned level-0 vertices
+//    have reached.
 //
-// With one rank this is exactly the single-GPU algorithm (same ids, same sums).
-// With several, every decision is the single-GPU decision on the same
-// (MG-numbered) level graph whenever the sums are exact (integer weights), which is
-// what the reference's MG test checks level by level (mg_louvain_test.cpp:82-151).
+// With one rank this is the single-GPU algorithm (same ids, same exact sums for
+// integer weights).  With several, every decision is the single-GPU decision on the
+// same (MG-numbered) level graph whenever the sums are exact (integer weights),
+// which is what the reference's MG test checks level by level
+// (mg_louvain_test.cpp:82-151).
 
 template <typename V>
 __global__ void k_owner_of_src(V const* src, int64_t n, int64_t const* voff, int P, int* dest)
@@ -1643,55 +1659,11 @@ __global__ void k_mg_row_keys(V const* src, V const* dst, int64_t n, int64_t bas
     keys[i] = ((u64)((int64_t)src[i] - base) << 32) | (u64)(uint32_t)dst[i];
 }
 
-// coarse pair key (label(row + base), label(dst)) of every local edge
-__global__ void k_mg_pair_keys(uint32_t const* src, uint32_t const* dst, uint32_t const* lab, uint32_t base,
-                               int64_t ne, u64* keys)
-{
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
-    keys[e] = ((u64)lab[src[e] + base] << 32) | (u64)lab[dst[e]];
-}
-
-// used[l - lo] = 1 for every label l in [lo, hi) that some vertex carries
-__global__ void k_mark_used_range(uint32_t const* lab, int64_t nv, int64_t lo, int64_t hi, uint32_t* used)
-{
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-    int64_t l = lab[v];
-    if (l >= lo && l < hi) used[l - lo] = 1u;
-  }
-}
-
 
 __global__ void k_new_ids_off(uint32_t const* nmap, int64_t n, uint32_t first, uint32_t* new_of_label)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     new_of_label[nmap[i]] = first + (uint32_t)i;
-}
-
-// (label(u), label(v)) -> (new(u) - new_lo, new(v))
-__global__ void k_relabel_pairs_local(u64 const* keys, int64_t n, uint32_t const* nl, uint32_t new_lo, u64* out)
-{
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = ((u64)(nl[(uint32_t)(keys[i] >> 32)] - new_lo) << 32) | (u64)nl[(uint32_t)keys[i]];
-}
-
-// out[voff[q] ..] = every rank's `own` slice (allgather padded to the largest slice)
-template <typename T>
-void allgatherv_dense(comm_t& comm, T const* own, std::vector<int64_t> const& voff, T* out, hipStream_t s)
-{
-  int const P = comm.size, p = comm.rank;
-  int64_t nmax = 0;
-  for (int q = 0; q < P; ++q) nmax = std::max(nmax, voff[q + 1] - voff[q]);
-  if (nmax == 0) return;
-  dbuf<T> sb(nmax, s), rb((size_t)nmax * P, s);
-  int64_t const n = voff[p + 1] - voff[p];
-  if (n) HIP_CHECK(hipMemcpyAsync(sb.data(), own, n * sizeof(T), hipMemcpyDeviceToDevice, s));
-  comm.allgather<T>(sb.data(), rb.data(), (size_t)nmax, s);
-  for (int q = 0; q < P; ++q) {
-    int64_t nq = voff[q + 1] - voff[q];
-    if (nq)
-      HIP_CHECK(hipMemcpyAsync(out + voff[q], rb.data() + (size_t)q * nmax, nq * sizeof(T), hipMemcpyDeviceToDevice,
-                               s));
-  }
 }
 
 std::vector<int64_t> bounds_to_counts(dbuf<int64_t> const& b, int P, hipStream_t s)
@@ -1759,32 +1731,508 @@ level_graph mg_level0(handle_t& h, graph_t& g)
   return out;
 }
 
-// contract by the dense level labels `lab` (nv entries, values in [0, nv)); on
-// return `voff` holds the coarse level's vertex ranges and `lab` the coarse ids
-level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, std::vector<int64_t>& voff)
+// ---------------------------------------------------------------- owner-sharded state
+// Every exchange of the sweep loop goes through these helpers, which also count the
+// bytes this rank sends (S.sweep_bytes; per-sweep figure in DESIGN.md, trace
+// CGX_LOUVAIN_TRACE=1, handle statistic last_louvain_sweep_bytes).
+template <typename T>
+dbuf<T> xchg(louvain_state& S, T const* send, std::vector<size_t> const& counts, std::vector<size_t>& rcounts)
+{
+  size_t n = 0;
+  for (size_t q = 0; q < counts.size(); ++q)
+    if ((int)q != S.comm->rank) n += counts[q];
+  S.bytes += n * sizeof(T);
+  return exchange<T>(*S.comm, send, counts, rcounts, S.s);
+}
+
+template <typename T>
+dbuf<T> xchg_known(louvain_state& S, T const* send, std::vector<size_t> const& counts,
+                   std::vector<size_t> const& rcounts)
+{
+  size_t n = 0;
+  for (size_t q = 0; q < counts.size(); ++q)
+    if ((int)q != S.comm->rank) n += counts[q];
+  S.bytes += n * sizeof(T);
+  return exchange_known<T>(*S.comm, send, counts, rcounts, S.s);
+}
+
+// first position of ids >= voff[q] in a sorted u32 array, q = 0..P
+__global__ void k_id_bounds(uint32_t const* ids, int64_t n, int64_t const* voff, int P, int64_t* out)
+{
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > P) return;
+  int64_t const t = voff[q];
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)ids[mid] < t) lo = mid + 1;
+    else hi = mid;
+  }
+  out[q] = lo;
+}
+
+// destinations outside this rank's rows [lo, lo + nr) -> their ids, others -> ~0u
+__global__ void k_remote_ids(uint32_t const* dst, int64_t ne, uint32_t lo, uint32_t nr, uint32_t* out)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const d = dst[e];
+    out[e]           = (d - lo < nr) ? ~0u : d;
+  }
+}
+
+__device__ inline int64_t lower_bound_u32(uint32_t const* a, int64_t n, uint32_t x)
+{
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// global destination -> local index: own rows [0, nr), ghosts nr + their position
+// in the sorted ghost list
+__global__ void k_localize(uint32_t* dst, int64_t ne, uint32_t lo, uint32_t nr, uint32_t const* ghost, int64_t ng)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const d = dst[e];
+    dst[e]           = (d - lo < nr) ? d - lo : nr + (uint32_t)lower_bound_u32(ghost, ng, d);
+  }
+}
+
+// out[i] = position of x[i] in the sorted key list
+__global__ void k_rank_in(uint32_t const* x, int64_t n, uint32_t const* keys, int64_t nk, uint32_t* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)lower_bound_u32(keys, nk, x[i]);
+}
+
+// owner side of a lookup: out[i] = table[key[i] - lo]
+template <typename T>
+__global__ void k_owner_gather(uint32_t const* key, int64_t n, uint32_t lo, T const* table, T* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = table[key[i] - lo];
+}
+
+__global__ void k_sub_u32(uint32_t* x, int64_t n, uint32_t lo)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] -= lo;
+}
+
+// fixed-point vertex weights of the rows: K = rint(k * scale)
+__global__ void k_to_fixed(double const* k, int64_t n, double scale, long long* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = __double2ll_rn(k[i] * scale);
+}
+
+// the sweep's cluster weights and present flags from the owners' answers
+__global__ void k_cluster_vals(long long const* afix, int const* pcnt, int64_t n, double inv, int all_present,
+                               double* a, uint8_t* present)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    a[i]       = (double)afix[i] * inv;
+    present[i] = (all_present || pcnt[i] > 0) ? 1 : 0;
+  }
+}
+
+// sum over the owned cluster ids of a_c^2 (present clusters only)
+struct sumsq_fixed_f {
+  long long const* afix;
+  int const* pcnt;
+  double inv;
+  int all_present;
+  __device__ double operator()(int64_t i) const
+  {
+    double const a = (double)afix[i] * inv;
+    return (all_present || pcnt[i] > 0) ? a * a : 0.0;
+  }
+};
+
+// local clusters after the sweep -> global ids; moved rows flagged, the owners'
+// weight deltas listed: (old cluster, -K, -has) and (new cluster, +K, +has) per move
+__global__ void k_advance(uint32_t const* next_loc, uint32_t const* ref, int64_t nr, uint32_t* c_own,
+                          uint8_t* moved)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nr; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const nc = ref[next_loc[i]];
+    moved[i]          = nc != c_own[i];
+    c_own[i]          = nc;
+  }
+}
+
+__global__ void k_move_deltas(uint32_t const* old_c, uint32_t const* new_c, uint8_t const* moved,
+                              uint32_t const* pos, int64_t nr, long long const* kfix, uint8_t const* has_edges,
+                              uint32_t* key, long long* dk, int* dh)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nr; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!moved[i]) continue;
+    int64_t const j = 2 * (int64_t)pos[i];
+    key[j]          = old_c[i];
+    dk[j]           = -kfix[i];
+    dh[j]           = -(int)has_edges[i];
+    key[j + 1]      = new_c[i];
+    dk[j + 1]       = kfix[i];
+    dh[j + 1]       = (int)has_edges[i];
+  }
+}
+
+// owner side: apply the received weight deltas (integer adds: order-free)
+__global__ void k_apply_deltas(uint32_t const* key, long long const* dk, int const* dh, int64_t n, uint32_t lo,
+                               long long* afix, int* pcnt)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(afix + (key[i] - lo)), (unsigned long long)dk[i]);
+    atomicAdd(pcnt + (key[i] - lo), dh[i]);
+  }
+}
+
+// mirror entries whose row moved -> flag (for the compaction of ghost updates)
+__global__ void k_mirror_flags(uint32_t const* mir, int64_t n, uint8_t const* moved, uint32_t* flag)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    flag[i] = moved[mir[i]];
+}
+
+__global__ void k_mirror_pack(uint32_t const* mir, uint32_t const* mir_pos, uint32_t const* flag,
+                              uint32_t const* pos, int64_t n, uint32_t const* c_own, uint32_t* out_pos,
+                              uint32_t* out_c)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (flag[i]) {
+      out_pos[pos[i]] = mir_pos[i];
+      out_c[pos[i]]   = c_own[mir[i]];
+    }
+}
+
+__global__ void k_scatter_u32(uint32_t const* pos, uint32_t const* val, int64_t n, uint32_t* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[pos[i]] = val[i];
+}
+
+// coarse pair key (label(u), label(v)) of every local edge; labels of the local
+// ids: own rows from lab_own, ghosts from lab_gh
+__global__ void k_mg_pair_keys_loc(uint32_t const* src, uint32_t const* dst, uint32_t const* lab_own,
+                                   uint32_t const* lab_gh, uint32_t nr, int64_t ne, u64* keys)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const d  = dst[e];
+    uint32_t const lv = d < nr ? lab_own[d] : lab_gh[d - nr];
+    keys[e]           = ((u64)lab_own[src[e]] << 32) | (u64)lv;
+  }
+}
+
+__global__ void k_mark_used_list(uint32_t const* lab, int64_t n, uint32_t lo, uint32_t* used)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    used[lab[i] - lo] = 1u;
+}
+
+// (l(u), l(v)) -> (new(l(u)) - new_lo, new(l(v))): l(u) is owned (nl_own), l(v)
+// through the looked-up table (keys sorted, values new ids)
+__global__ void k_relabel_pairs_mg(u64 const* keys, int64_t n, uint32_t const* nl_own, uint32_t lo,
+                                   uint32_t const* tk, uint32_t const* tv, int64_t nt, uint32_t new_lo, u64* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const lu = (uint32_t)(keys[i] >> 32), lv = (uint32_t)keys[i];
+    uint32_t const nv = tv[lower_bound_u32(tk, nt, lv)];
+    out[i]            = ((u64)(nl_own[lu - lo] - new_lo) << 32) | (u64)nv;
+  }
+}
+
+__global__ void k_key_lo(u64 const* keys, int64_t n, uint32_t* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)keys[i];
+}
+
+// x[i] -> the value of x[i] in the table (keys sorted, every x present)
+__global__ void k_lookup_u32(uint32_t* x, int64_t n, uint32_t const* tk, uint32_t const* tv, int64_t nt)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = tv[lower_bound_u32(tk, nt, x[i])];
+}
+
+// sorted unique of n u32 keys (values < 2^bits) into out; returns the count
+int64_t sort_unique_u32(uint32_t const* in, int64_t n, dbuf<uint32_t>& out, int bits, hipStream_t s)
+{
+  out.resize(std::max<int64_t>(n, 1), s);
+  if (n == 0) return 0;
+  dbuf<uint32_t> tmp(n, s);
+  radix_sort_keys<uint32_t>(in, tmp.data(), (size_t)n, 0, bits, s);
+  dbuf<size_t> cnt(1, s);
+  size_t tb = 0;
+  HIP_CHECK(rocprim::unique(nullptr, tb, tmp.data(), out.data(), cnt.data(), (size_t)n,
+                            rocprim::equal_to<uint32_t>(), s));
+  buffer t(std::max<size_t>(tb, 1), s);
+  HIP_CHECK(rocprim::unique(t.data(), tb, tmp.data(), out.data(), cnt.data(), (size_t)n,
+                            rocprim::equal_to<uint32_t>(), s));
+  return (int64_t)to_host_scalar(cnt.data(), s);
+}
+
+// per-owner counts of a sorted id list (owner ranges voff, device copy voff_d)
+std::vector<size_t> owner_counts(uint32_t const* ids, int64_t n, dbuf<int64_t> const& voff_d, int P, hipStream_t s)
+{
+  dbuf<int64_t> bnd(P + 1, s);
+  hipLaunchKernelGGL(k_id_bounds, dim3(1), dim3(256), 0, s, ids, n, voff_d.data(), P, bnd.data());
+  CGX_LAUNCH_CHECK();
+  auto c = bounds_to_counts(bnd, P, s);
+  return std::vector<size_t>(c.begin(), c.end());
+}
+
+// collect_values_for_keys: keys (sorted unique ids of this level, n) -> the values
+// their owners hold in own_vals[id - voff[owner]] (out[i] for keys[i])
+template <typename T>
+dbuf<T> collect_by_key(louvain_state& S, uint32_t const* keys, int64_t n, dbuf<int64_t> const& voff_d, int64_t lo,
+                       T const* own_vals)
 {
   hipStream_t s = S.s;
-  comm_t& comm  = *S.comm;
+  auto counts   = owner_counts(keys, n, voff_d, S.comm->size, s);
+  std::vector<size_t> rc;
+  auto rk = xchg<uint32_t>(S, keys, counts, rc);
+  dbuf<T> ans(std::max<size_t>(rk.n, 1), s);
+  if (rk.n)
+    hipLaunchKernelGGL(k_owner_gather<T>, dim3(blocks((int64_t)rk.n)), dim3(kBlock), 0, s, rk.data(), (int64_t)rk.n,
+                       (uint32_t)lo, own_vals, ans.data());
+  CGX_LAUNCH_CHECK();
+  return xchg_known<T>(S, ans.data(), rc, counts);
+}
+
+// One level of the owner-sharded local move.  The level graph's destinations are
+// turned into local ids ([0, nr): own rows, then the ghosts), so the single-GPU
+// sweep kernels run unchanged on (rows, local ids, local cluster ids).
+struct mg_level {
+  int64_t nv = 0, lo = 0, nr = 0, ng = 0;
+  std::vector<int64_t> voff;
+  dbuf<int64_t> voff_d;
+  dbuf<uint32_t> ghost;     // ng: sorted global ids of remote destinations
+  dbuf<uint32_t> mir;       // rows (id - lo) mirrored to other ranks, in requester order
+  dbuf<uint32_t> mir_pos;   // their positions in the requester's ghost list
+  std::vector<size_t> mir_cnt, mir_rcv;  // per requester; the update exchange's receive counts are unknown
+  dbuf<uint32_t> c_own, c_gh;  // clusters (global ids) of the rows and of the ghosts
+  dbuf<long long> kfix, afix;  // rows' fixed-point weights; owned clusters' fixed-point weights
+  dbuf<int> pcnt;              // owned clusters: members with edges
+  double scale = 0, inv = 0;
+};
+
+void mg_setup_level(louvain_state& S, level_graph& g, mg_level& L, uint8_t const* has_edges, double const* k)
+{
+  hipStream_t s = S.s;
+  int const P   = S.comm->size;
+  int64_t const ne = g.ne, nr = L.nr, r1 = std::max<int64_t>(nr, 1);
+  // ghosts: distinct remote destinations
+  dbuf<uint32_t> rem(std::max<int64_t>(ne, 1), s);
+  if (ne)
+    hipLaunchKernelGGL(k_remote_ids, dim3(blocks(ne)), dim3(kBlock), 0, s, g.dst.data(), ne, (uint32_t)L.lo,
+                       (uint32_t)nr, rem.data());
+  CGX_LAUNCH_CHECK();
+  int64_t nu = sort_unique_u32(rem.data(), ne, L.ghost, 32, s);
+  if (nu && to_host_scalar(L.ghost.data() + nu - 1, s) == ~0u) --nu;  // the own-destination marker
+  L.ng = nu;
+  // mirror lists: every ghost list goes to the owners of its ids
+  auto gcount = owner_counts(L.ghost.data(), L.ng, L.voff_d, P, s);
+  {
+    dbuf<uint32_t> gpos(std::max<int64_t>(L.ng, 1), s);
+    iota<uint32_t>(gpos.data(), L.ng, 0u, s);
+    L.mir     = xchg<uint32_t>(S, L.ghost.data(), gcount, L.mir_cnt);
+    L.mir_pos = xchg_known<uint32_t>(S, gpos.data(), gcount, L.mir_cnt);
+  }
+  if (L.mir.n)
+    hipLaunchKernelGGL(k_sub_u32, dim3(blocks((int64_t)L.mir.n)), dim3(kBlock), 0, s, L.mir.data(), (int64_t)L.mir.n,
+                       (uint32_t)L.lo);
+  CGX_LAUNCH_CHECK();
+  L.mir_rcv = gcount;  // ghost updates come back from the owners in these blocks at most
+  // local destination ids
+  if (ne)
+    hipLaunchKernelGGL(k_localize, dim3(blocks(ne)), dim3(kBlock), 0, s, g.dst.data(), ne, (uint32_t)L.lo,
+                       (uint32_t)nr, L.ghost.data(), L.ng);
+  CGX_LAUNCH_CHECK();
+  g.base = 0;
+  g.nv   = nr + L.ng;
+  // singleton clusters: rows lo + i, ghosts their own ids
+  L.c_own.resize(r1, s);
+  iota<uint32_t>(L.c_own.data(), nr, (uint32_t)L.lo, s);
+  L.c_gh.resize(std::max<int64_t>(L.ng, 1), s);
+  if (L.ng)
+    HIP_CHECK(hipMemcpyAsync(L.c_gh.data(), L.ghost.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  // fixed-point cluster weights at the owners: scale 2^(60 - e), sum of all weights < 2^e
+  int const e = S.m > 0 ? std::ilogb(S.m) + 1 : 0;
+  L.scale     = std::ldexp(1.0, 60 - e);
+  L.inv       = std::ldexp(1.0, e - 60);
+  L.kfix.resize(r1, s);
+  L.afix.resize(r1, s);
+  L.pcnt.resize(r1, s);
+  if (nr) {
+    hipLaunchKernelGGL(k_to_fixed, dim3(blocks(nr)), dim3(kBlock), 0, s, k, nr, L.scale, L.kfix.data());
+    CGX_LAUNCH_CHECK();
+    HIP_CHECK(hipMemcpyAsync(L.afix.data(), L.kfix.data(), nr * sizeof(long long), hipMemcpyDeviceToDevice, s));
+    convert<int, uint8_t>(L.pcnt.data(), has_edges, nr, s);
+  }
+}
+
+// the local clustering of the sweep: referenced clusters (own rows' and ghosts'),
+// their weights and present flags from the owners
+struct mg_sweep_view {
+  int64_t ncl = 0;
+  dbuf<uint32_t> ref;       // sorted global cluster ids referenced here
+  dbuf<uint32_t> c_loc;     // nr + ng local cluster ids
+  dbuf<double> a;           // ncl
+  dbuf<uint8_t> present;    // ncl
+};
+
+void mg_view(louvain_state& S, mg_level& L, bool all_present, mg_sweep_view& W)
+{
+  hipStream_t s   = S.s;
+  int64_t const n = L.nr + L.ng;
+  dbuf<uint32_t> all(std::max<int64_t>(n, 1), s);
+  if (L.nr) HIP_CHECK(hipMemcpyAsync(all.data(), L.c_own.data(), L.nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  if (L.ng)
+    HIP_CHECK(hipMemcpyAsync(all.data() + L.nr, L.c_gh.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  W.ncl = sort_unique_u32(all.data(), n, W.ref, bits_for((unsigned long long)std::max<int64_t>(L.nv - 1, 1)), s);
+  W.c_loc.resize(std::max<int64_t>(n, 1), s);
+  if (n)
+    hipLaunchKernelGGL(k_rank_in, dim3(blocks(n)), dim3(kBlock), 0, s, all.data(), n, W.ref.data(), W.ncl,
+                       W.c_loc.data());
+  CGX_LAUNCH_CHECK();
+  auto af = collect_by_key<long long>(S, W.ref.data(), W.ncl, L.voff_d, L.lo, L.afix.data());
+  auto pc = collect_by_key<int>(S, W.ref.data(), W.ncl, L.voff_d, L.lo, L.pcnt.data());
+  W.a.resize(std::max<int64_t>(W.ncl, 1), s);
+  W.present.resize(std::max<int64_t>(W.ncl, 1), s);
+  if (W.ncl)
+    hipLaunchKernelGGL(k_cluster_vals, dim3(blocks(W.ncl)), dim3(kBlock), 0, s, af.data(), pc.data(), W.ncl, L.inv,
+                       all_present ? 1 : 0, W.a.data(), W.present.data());
+  CGX_LAUNCH_CHECK();
+}
+
+// Q of the clustering the sweep started from: sum of own(row) (the internal weight
+// by-product of the sweep) and sum of a_c^2 over the owned cluster ids
+double mg_modularity(louvain_state& S, mg_level& L, double const* own, bool all_present)
+{
+  device_sum(plain_f{own}, (size_t)L.nr, S.scal.data(), S.scratch.data(), S.s);
+  device_sum(sumsq_fixed_f{L.afix.data(), L.pcnt.data(), L.inv, all_present ? 1 : 0}, (size_t)L.nr,
+             S.scal.data() + 1, S.scratch.data(), S.s);
+  S.comm->allreduce<double>(S.scal.data(), S.scal.data(), 2, CGX_COMM_SUM, S.s);
+  auto hv = to_host(S.scal.data(), 2, S.s);
+  return hv[0] / S.m - (S.gamma * hv[1]) / (S.m * S.m);
+}
+
+// clusters <- the sweep's result: rows' new global clusters, the owners' weights
+// updated by the moves, the moved rows' new clusters sent to the ranks that
+// mirror them.  Traffic: O(moved rows + their mirrors).
+void mg_advance(louvain_state& S, mg_level& L, mg_sweep_view& W, uint32_t const* next_loc, uint8_t const* has_edges)
+{
+  hipStream_t s    = S.s;
+  int const P      = S.comm->size;
+  int64_t const nr = L.nr, r1 = std::max<int64_t>(nr, 1);
+  dbuf<uint32_t> old_c(r1, s);
+  dbuf<uint8_t> moved(r1, s);
+  dbuf<uint32_t> mflag(r1, s), mpos(r1 + 1, s);
+  int64_t nm = 0;
+  if (nr) {
+    HIP_CHECK(hipMemcpyAsync(old_c.data(), L.c_own.data(), nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_advance, dim3(blocks(nr)), dim3(kBlock), 0, s, next_loc, W.ref.data(), nr, L.c_own.data(),
+                       moved.data());
+    CGX_LAUNCH_CHECK();
+    convert<uint32_t, uint8_t>(mflag.data(), moved.data(), nr, s);
+    exclusive_scan<uint32_t, uint32_t>(mflag.data(), mpos.data(), (size_t)nr + 1, s);
+    nm = (int64_t)to_host_scalar(mpos.data() + nr, s);
+  }
+  // 1. weight deltas to the owners of the old and the new clusters
+  int64_t const nd = 2 * nm, d1 = std::max<int64_t>(nd, 1);
+  dbuf<uint32_t> dkey(d1, s), dkey2(d1, s);
+  dbuf<long long> dk(d1, s);
+  dbuf<int> dh(d1, s);
+  dbuf<int64_t> perm(d1, s), perm2(d1, s);
+  if (nm) {
+    hipLaunchKernelGGL(k_move_deltas, dim3(blocks(nr)), dim3(kBlock), 0, s, old_c.data(), L.c_own.data(),
+                       moved.data(), mpos.data(), nr, L.kfix.data(), has_edges, dkey.data(), dk.data(), dh.data());
+    CGX_LAUNCH_CHECK();
+    iota<int64_t>(perm.data(), nd, 0, s);
+    radix_sort_pairs<uint32_t, int64_t>(dkey.data(), dkey2.data(), perm.data(), perm2.data(), (size_t)nd, 0, 32, s);
+  }
+  dbuf<long long> dk2(d1, s);
+  dbuf<int> dh2(d1, s);
+  if (nm) {
+    gather<long long, int64_t>(dk2.data(), dk.data(), perm2.data(), nd, s);
+    gather<int, int64_t>(dh2.data(), dh.data(), perm2.data(), nd, s);
+  }
+  auto counts = owner_counts(dkey2.data(), nd, L.voff_d, P, s);
+  std::vector<size_t> rc;
+  auto rk  = xchg<uint32_t>(S, dkey2.data(), counts, rc);
+  auto rdk = xchg_known<long long>(S, dk2.data(), counts, rc);
+  auto rdh = xchg_known<int>(S, dh2.data(), counts, rc);
+  if (rk.n)
+    hipLaunchKernelGGL(k_apply_deltas, dim3(blocks((int64_t)rk.n)), dim3(kBlock), 0, s, rk.data(), rdk.data(),
+                       rdh.data(), (int64_t)rk.n, (uint32_t)L.lo, L.afix.data(), L.pcnt.data());
+  CGX_LAUNCH_CHECK();
+  // 2. ghost updates: mirror entries of moved rows, per requester
+  int64_t const nmir = (int64_t)L.mir.n, m1 = std::max<int64_t>(nmir, 1);
+  dbuf<uint32_t> fl(m1, s), fpos(m1 + 1, s);
+  std::vector<size_t> ucnt(P, 0);
+  int64_t nup = 0;
+  if (nmir) {
+    hipLaunchKernelGGL(k_mirror_flags, dim3(blocks(nmir)), dim3(kBlock), 0, s, L.mir.data(), nmir, moved.data(),
+                       fl.data());
+    CGX_LAUNCH_CHECK();
+    exclusive_scan<uint32_t, uint32_t>(fl.data(), fpos.data(), (size_t)nmir + 1, s);
+    // per-requester counts from the scan at the block boundaries
+    std::vector<int64_t> bo(P + 1, 0);
+    for (int q = 0; q < P; ++q) bo[q + 1] = bo[q] + (int64_t)L.mir_cnt[q];
+    dbuf<int64_t> bod(P + 1, s);
+    dbuf<uint32_t> atd(P + 1, s);
+    to_device(bod.data(), bo.data(), (size_t)P + 1, s);
+    gather<uint32_t, int64_t>(atd.data(), fpos.data(), bod.data(), (size_t)P + 1, s);
+    auto at = to_host(atd.data(), (size_t)P + 1, s);
+    for (int q = 0; q < P; ++q) ucnt[q] = at[q + 1] - at[q];
+    nup = at[P];
+  }
+  dbuf<uint32_t> upos(std::max<int64_t>(nup, 1), s), uc(std::max<int64_t>(nup, 1), s);
+  if (nup)
+    hipLaunchKernelGGL(k_mirror_pack, dim3(blocks(nmir)), dim3(kBlock), 0, s, L.mir.data(), L.mir_pos.data(),
+                       fl.data(), fpos.data(), nmir, L.c_own.data(), upos.data(), uc.data());
+  CGX_LAUNCH_CHECK();
+  std::vector<size_t> urc;
+  auto rpos = xchg<uint32_t>(S, upos.data(), ucnt, urc);
+  auto rc2  = xchg_known<uint32_t>(S, uc.data(), ucnt, urc);
+  if (rpos.n)
+    hipLaunchKernelGGL(k_scatter_u32, dim3(blocks((int64_t)rpos.n)), dim3(kBlock), 0, s, rpos.data(), rc2.data(),
+                       (int64_t)rpos.n, L.c_gh.data());
+  CGX_LAUNCH_CHECK();
+}
+
+// contract by the level's clustering (lab_own: rows' clusters, lab_gh: ghosts'
+// clusters, global ids): coarse pairs to the owner of label(u), used labels numbered
+// there by descending coarse degree, the new ids of label(v) and of the rows'
+// labels collected from their owners.  On return lab_own holds the rows' coarse ids
+// and voff the coarse level's ranges.
+level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uint32_t* lab_own, uint32_t const* lab_gh,
+                        std::vector<int64_t>& voff)
+{
+  hipStream_t s  = S.s;
+  comm_t& comm   = *S.comm;
   int const P = comm.size, p = comm.rank;
-  int64_t const nv = g.nv, ne = g.ne, nr = g.nrows, lo = g.base;
+  int64_t const ne = g.ne, nr = L.nr, lo = L.lo, nv = L.nv;
   int64_t const n1 = std::max<int64_t>(ne, 1);
-  dbuf<int64_t> voff_d(P + 1, s), bnd(P + 1, s);
-  HIP_CHECK(hipMemcpyAsync(voff_d.data(), voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  int const lb = bits_for((unsigned long long)std::max<int64_t>(nv - 1, 1));
   // 1. local coarse pairs, summed
   dbuf<u64> keys(n1, s), keys2(n1, s);
   dbuf<double> w2(n1, s), cw(n1, s);
   int64_t nce = 0;
   if (ne) {
-    hipLaunchKernelGGL(k_mg_pair_keys, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), lab,
-                       (uint32_t)lo, ne, keys.data());
+    hipLaunchKernelGGL(k_mg_pair_keys_loc, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), lab_own,
+                       lab_gh, (uint32_t)nr, ne, keys.data());
     CGX_LAUNCH_CHECK();
-    radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0,
-                                  32 + bits_for(nv - 1), s);
+    radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0, 32 + lb, s);
     nce = reduce_by_key(keys2.data(), w2.data(), (size_t)ne, keys.data(), cw.data(), rocprim::plus<double>(),
                         rocprim::equal_to<u64>(), s);
   }
-  // 2. to the owner of label(u) (keys are sorted, owner ranges ascending)
-  hipLaunchKernelGGL(k_key_bounds, dim3(1), dim3(256), 0, s, keys.data(), nce, voff_d.data(), P, bnd.data());
+  // 2. to the owner of label(u) (keys sorted, owner ranges ascending)
+  dbuf<int64_t> bnd(P + 1, s);
+  hipLaunchKernelGGL(k_key_bounds, dim3(1), dim3(256), 0, s, keys.data(), nce, L.voff_d.data(), P, bnd.data());
   CGX_LAUNCH_CHECK();
   auto c64 = bounds_to_counts(bnd, P, s);
   std::vector<size_t> counts(c64.begin(), c64.end()), rc;
@@ -1795,16 +2243,22 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, s
   dbuf<double> mw(r1, s), mw2(r1, s);
   int64_t nm = 0;
   if (nrcv) {
-    radix_sort_pairs<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0,
-                                  32 + bits_for(nv - 1), s);
+    radix_sort_pairs<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0, 32 + lb, s);
     nm = reduce_by_key(mk2.data(), mw2.data(), (size_t)nrcv, mk.data(), mw.data(), rocprim::plus<double>(),
                        rocprim::equal_to<u64>(), s);
   }
-  // 3. my used labels, numbered by descending coarse out-degree (stable)
+  // 3. used labels: every rank sends its rows' distinct labels to their owners
+  dbuf<uint32_t> ul;
+  int64_t const nul = sort_unique_u32(lab_own, nr, ul, lb, s);
+  auto ucounts = owner_counts(ul.data(), nul, L.voff_d, P, s);
+  std::vector<size_t> urc;
+  auto rl = exchange<uint32_t>(comm, ul.data(), ucounts, urc, s);
   dbuf<uint32_t> used(nr + 1, s), pos(nr + 1, s), deg(std::max<int64_t>(nr, 1), s);
   fill<uint32_t>(used.data(), nr + 1, 0u, s);
   fill<uint32_t>(deg.data(), std::max<int64_t>(nr, 1), 0u, s);
-  hipLaunchKernelGGL(k_mark_used_range, dim3(blocks(nv)), dim3(kBlock), 0, s, lab, nv, lo, lo + nr, used.data());
+  if (rl.n)
+    hipLaunchKernelGGL(k_mark_used_list, dim3(blocks((int64_t)rl.n)), dim3(kBlock), 0, s, rl.data(), (int64_t)rl.n,
+                       (uint32_t)lo, used.data());
   CGX_LAUNCH_CHECK();
   if (nm && nr)
     hipLaunchKernelGGL(k_count_src, dim3(blocks(nr)), dim3(kBlock), 0, s, mk.data(), nm, lo, nr, deg.data());
@@ -1827,9 +2281,17 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, s
   if (nu)
     hipLaunchKernelGGL(k_new_ids_off, dim3(blocks(nu)), dim3(kBlock), 0, s, nmap.data(), nu, new_lo, nl_own.data());
   CGX_LAUNCH_CHECK();
-  // 4. dense label -> new id table (entries of unused labels are never read)
-  dbuf<uint32_t> nl(std::max<int64_t>(nv, 1), s);
-  allgatherv_dense<uint32_t>(comm, nl_own.data(), voff, nl.data(), s);
+  // (nl_own: the new id of every used label, indexed by label - lo)
+  // 4. new ids of the labels this rank still needs: label(v) of its merged pairs and
+  //    its rows' labels
+  int64_t const nq = nm + nr;
+  dbuf<uint32_t> want(std::max<int64_t>(nq, 1), s), wk;
+  if (nm)
+    hipLaunchKernelGGL(k_key_lo, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, want.data());
+  CGX_LAUNCH_CHECK();
+  if (nr) HIP_CHECK(hipMemcpyAsync(want.data() + nm, lab_own, nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  int64_t const nw = sort_unique_u32(want.data(), nq, wk, lb, s);
+  auto wv = collect_by_key<uint32_t>(S, wk.data(), nw, L.voff_d, lo, nl_own.data());
   level_graph out;
   out.nv    = nvoff[P];
   out.base  = nvoff[p];
@@ -1839,8 +2301,8 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, s
   out.dst.resize(std::max<int64_t>(nm, 1), s);
   out.w.resize(std::max<int64_t>(nm, 1), s);
   if (nm) {
-    hipLaunchKernelGGL(k_relabel_pairs_local, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, nl.data(), new_lo,
-                       mk2.data());
+    hipLaunchKernelGGL(k_relabel_pairs_mg, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, nl_own.data(),
+                       (uint32_t)lo, wk.data(), wv.data(), nw, new_lo, mk2.data());
     CGX_LAUNCH_CHECK();
     radix_sort_pairs<u64, double>(mk2.data(), mk.data(), mw.data(), out.w.data(), (size_t)nm, 0,
                                   32 + bits_for(std::max<int64_t>(nu - 1, 0)), s);
@@ -1848,7 +2310,7 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, uint32_t* lab, s
                        out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_gather_u32, dim3(blocks(nv)), dim3(kBlock), 0, s, nl.data(), lab, nv);
+  if (nr) hipLaunchKernelGGL(k_lookup_u32, dim3(blocks(nr)), dim3(kBlock), 0, s, lab_own, nr, wk.data(), wv.data(), nw);
   CGX_LAUNCH_CHECK();
   voff = nvoff;
   return out;
@@ -1861,96 +2323,139 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
   CGX_EXPECTS(g.weighted, CUGRAPH_UNKNOWN_ERROR, "Graph must be weighted");  // louvain_impl.cuh:290
   mg_graph_t& mg = *g.mg;
   comm_t& comm   = *h.mg->world;
-  int const p    = mg.p;
+  int const p    = mg.p, P = mg.P;
   int64_t const nv0 = g.num_vertices, n_own = mg.n_own();
-  CGX_EXPECTS((uint64_t)nv0 < (1ull << 32), CUGRAPH_NOT_IMPLEMENTED, "Louvain: more than 2^32 vertices");
+  CGX_EXPECTS((uint64_t)nv0 < (1ull << 32) - 1, CUGRAPH_NOT_IMPLEMENTED, "Louvain: 2^32 - 1 or more vertices");
   res.vertices = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
   if (n_own)
     HIP_CHECK(hipMemcpyAsync(res.vertices->buf.data(), g.number_map.data(), n_own * sizeof(V), hipMemcpyDeviceToDevice,
                              s));
   res.clusters = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
-  h.last_louvain_levels = 0;
-  res.modularity        = 0;
+  h.last_louvain_levels      = 0;
+  h.last_louvain_sweep_bytes = 0;
+  res.modularity             = 0;
   if (nv0 == 0) return;
 
   louvain_state S(s);
-  S.gamma        = resolution;
-  S.comm         = &comm;
+  S.gamma         = resolution;
+  S.comm          = &comm;
   level_graph cur = mg_level0<V, R>(h, g);
   device_sum(plain_f{cur.w.data()}, (size_t)cur.ne, S.scal.data(), S.scratch.data(), s);
   comm.allreduce<double>(S.scal.data(), S.scal.data(), 1, CGX_COMM_SUM, s);
   S.m = to_host_scalar(S.scal.data(), s);
 
+  bool const trace = std::getenv("CGX_LOUVAIN_TRACE") != nullptr;  // measurement only
   std::vector<int64_t> voff = mg.voff;
-  std::vector<dbuf<uint32_t>> dendrogram;  // dense: every level-i id on every rank
+  std::vector<dbuf<uint32_t>> dendrogram;  // per level: the owned ids' clusters (coarse ids after contraction)
   std::vector<std::vector<int64_t>> level_voff;
   double best_q = -1.0;
+  size_t sweeps = 0, sweep_bytes = 0;
   while (dendrogram.size() < max_level) {
-    int64_t const nv = cur.nv, nr = cur.nrows, r1 = std::max<int64_t>(nr, 1);
-    dendrogram.emplace_back(std::max<int64_t>(nv, 1), s);
+    mg_level L;
+    L.nv   = cur.nv;
+    L.lo   = cur.base;
+    L.nr   = cur.nrows;
+    L.voff = voff;
+    L.voff_d.resize(P + 1, s);
+    to_device(L.voff_d.data(), voff.data(), (size_t)P + 1, s);
+    int64_t const nr = L.nr, r1 = std::max<int64_t>(nr, 1);
     level_voff.push_back(voff);
-    uint32_t* level = dendrogram.back().data();
-    iota<uint32_t>(level, nv, 0u, s);
     dbuf<int64_t> off(nr + 1, s);
     hipLaunchKernelGGL(k_row_offsets, dim3(blocks(nr + 1)), dim3(kBlock), 0, s, cur.src.data(), cur.ne, nr,
                        off.data());
     CGX_LAUNCH_CHECK();
-    dbuf<double> k(r1, s), self(r1, s), a(nv, s);
-    dbuf<uint8_t> has_edges(r1, s), present(nv, s);
-    if (nr)
-      vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
-    allgatherv_dense<double>(comm, k.data(), voff, a.data(), s);
-    fill<uint8_t>(present.data(), nv, 1, s);
-    dbuf<uint32_t> clusters(nv, s), next(r1, s);
-    iota<uint32_t>(clusters.data(), nv, 0u, s);
+    dbuf<double> k(r1, s), self(r1, s);
+    dbuf<uint8_t> has_edges(r1, s);
+    // vertex weights on the global destinations (self loops: dst == row + base), then
+    // the destinations become local ids
+    if (nr) vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
+    S.bytes = 0;
+    mg_setup_level(S, cur, L, has_edges.data(), k.data());
+    size_t const setup_bytes = S.bytes;
+    dendrogram.emplace_back(r1, s);
+    uint32_t* level = dendrogram.back().data();
+    dbuf<uint32_t> level_gh(std::max<int64_t>(L.ng, 1), s);
+    HIP_CHECK(hipMemcpyAsync(level, L.c_own.data(), nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    if (L.ng)
+      HIP_CHECK(hipMemcpyAsync(level_gh.data(), L.c_gh.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     sweep_plan plan;
     plan_sweeps(S, cur, off.data(), k.data(), plan);
     dbuf<double> own(r1, s);
-    bool up_down = true;  // as the single-GPU loop: sweep k + 1 before the decision on clustering k
-    sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down,
+    dbuf<uint32_t> next(r1, s);
+    mg_sweep_view W;
+    bool all_present = true;  // the first sweep: every cluster present (fill 1, as the single-GPU loop)
+    bool up_down     = true;  // as the single-GPU loop: sweep k + 1 before the decision on clustering k
+    S.bytes          = 0;
+    mg_view(S, L, all_present, W);
+    sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), up_down,
           own.data());
-    double new_q = modularity_own(S, cur, own.data(), a.data(), present.data());
+    double new_q = mg_modularity(S, L, own.data(), all_present);
+    ++sweeps;
+    sweep_bytes += S.bytes;
+    if (trace && p == 0)
+      std::fprintf(stderr, "[louvain-mg] level %zu nv=%lld setup %zu B/rank, sweep %zu B/rank q=%.6f\n",
+                   dendrogram.size() - 1, (long long)L.nv, setup_bytes, S.bytes, new_q);
     double cur_q = new_q - 1.0;
     while (new_q > cur_q + 0.0001) {
       cur_q = new_q;
-      allgatherv_dense<uint32_t>(comm, next.data(), voff, clusters.data(), s);
-      cluster_weights(S, cur, clusters.data(), k.data(), has_edges.data(), a.data(), present.data());
-      up_down = !up_down;
-      sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down,
+      S.bytes = 0;
+      mg_advance(S, L, W, next.data(), has_edges.data());
+      all_present = false;
+      up_down     = !up_down;
+      mg_view(S, L, all_present, W);
+      sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), up_down,
             own.data());
-      new_q = modularity_own(S, cur, own.data(), a.data(), present.data());
-      if (new_q > cur_q)
-        HIP_CHECK(hipMemcpyAsync(level, clusters.data(), nv * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      new_q = mg_modularity(S, L, own.data(), all_present);
+      ++sweeps;
+      sweep_bytes += S.bytes;
+      if (trace && p == 0)
+        std::fprintf(stderr, "[louvain-mg]   sweep %zu B/rank (%lld referenced clusters) q=%.6f\n", S.bytes,
+                     (long long)W.ncl, new_q);
+      if (new_q > cur_q) {
+        HIP_CHECK(hipMemcpyAsync(level, L.c_own.data(), nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        if (L.ng)
+          HIP_CHECK(
+            hipMemcpyAsync(level_gh.data(), L.c_gh.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      }
     }
     if (cur_q <= best_q) break;
     best_q = cur_q;
-    cur    = mg_contract(S, cur, level, voff);
+    cur    = mg_contract(S, cur, L, level, level_gh.data(), voff);
   }
-  // flatten_dendrogram for the owned level-0 vertices
-  int64_t const lo0 = mg.voff[p];
+  // flatten_dendrogram for the owned level-0 vertices: level i's owners answer
+  // for the ids the chain has reached
   dbuf<uint32_t> flat(std::max<int64_t>(n_own, 1), s);
-  if (n_own) {
-    HIP_CHECK(hipMemcpyAsync(flat.data(), dendrogram[0].data() + lo0, n_own * sizeof(uint32_t),
-                             hipMemcpyDeviceToDevice, s));
-    for (size_t i = 1; i < dendrogram.size(); ++i)
-      hipLaunchKernelGGL(k_gather_u32, dim3(blocks(n_own)), dim3(kBlock), 0, s, dendrogram[i].data(), flat.data(),
-                         n_own);
+  if (n_own)
+    HIP_CHECK(hipMemcpyAsync(flat.data(), dendrogram[0].data(), n_own * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  for (size_t i = 1; i < dendrogram.size(); ++i) {
+    dbuf<int64_t> vd(P + 1, s);
+    to_device(vd.data(), level_voff[i].data(), (size_t)P + 1, s);
+    dbuf<uint32_t> fk;
+    int const lb = bits_for((unsigned long long)std::max<int64_t>(level_voff[i][P] - 1, 1));
+    int64_t const nk = sort_unique_u32(flat.data(), n_own, fk, lb, s);
+    auto fv          = collect_by_key<uint32_t>(S, fk.data(), nk, vd, level_voff[i][p], dendrogram[i].data());
+    if (n_own)
+      hipLaunchKernelGGL(k_lookup_u32, dim3(blocks(n_own)), dim3(kBlock), 0, s, flat.data(), n_own, fk.data(),
+                         fv.data(), nk);
     CGX_LAUNCH_CHECK();
+  }
+  if (n_own) {
     hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, flat.data(), n_own,
                        res.clusters->buf.data<V>());
     CGX_LAUNCH_CHECK();
   }
   for (size_t i = 0; i < dendrogram.size(); ++i) {
-    int64_t const b = level_voff[i][p], n = level_voff[i][p + 1] - b;
+    int64_t const n = level_voff[i][p + 1] - level_voff[i][p];
     res.levels.push_back(std::make_unique<device_array_t>((size_t)n, g.vertex_type, s));
     if (n)
-      hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(n)), dim3(kBlock), 0, s, dendrogram[i].data() + b, n,
+      hipLaunchKernelGGL(k_to_vertex<V>, dim3(blocks(n)), dim3(kBlock), 0, s, dendrogram[i].data(), n,
                          res.levels.back()->buf.data<V>());
     CGX_LAUNCH_CHECK();
   }
   HIP_CHECK(hipStreamSynchronize(s));
-  res.modularity        = best_q;
-  h.last_louvain_levels = dendrogram.size();
+  res.modularity             = best_q;
+  h.last_louvain_levels      = dendrogram.size();
+  h.last_louvain_sweep_bytes = sweeps ? (double)sweep_bytes / (double)sweeps : 0.0;
 }
 
 }  // namespace

@@ -1119,10 +1119,14 @@ inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std
   std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.nwin, 1), 0);
   for (int64_t i = 0; i < nitems; ++i) {
     int64_t const u = item_u[i], last = item_u[i + 1] - 1;
-    bool const whole = !no_whole && (u == 0 || hu[u - 1].win != hu[u].win) &&
-                       (last + 1 >= nunits || hu[last + 1].win != hu[u].win);
+    // the flag may already sit on an earlier item's first unit: compare and index
+    // by the window bits only
+    int64_t const wu = hu[u].win & kWinMask;
+    bool const whole = !no_whole && (u == 0 || (hu[u - 1].win & kWinMask) != wu) &&
+                       (last + 1 >= nunits || (hu[last + 1].win & kWinMask) != wu);
+    CGX_EXPECTS(!(hu[u].win & kWholeItem), CUGRAPH_UNKNOWN_ERROR, "mark_whole_items: unit already flagged");
     if (whole) hu[u].win |= kWholeItem;
-    else multi[hu[u].win] = 1;
+    else multi[wu] = 1;
   }
   to_device(units, hu.data(), (size_t)nunits, s);
   pp.win_multi.set_stream(s);

@@ -78,7 +78,7 @@ def bfs(input_graph, start, depth_limit=None, return_distances=True, check_start
     starts = np.atleast_1d(np.asarray(start)).astype(np.int64)
     if check_start:
         e = G.edgelist
-        present = torch.zeros(starts.size, dtype=torch.int64)
+        present = torch.zeros(starts.size, dtype=torch.int64, device=_comms.collective_device())
         for i, x in enumerate(starts.tolist()):
             present[i] = int(((e["src"] == x).any() | (e["dst"] == x).any()).item())
         dist.all_reduce(present, op=dist.ReduceOp.MAX)

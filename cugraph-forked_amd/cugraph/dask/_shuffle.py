@@ -41,13 +41,13 @@ def shuffle_dedup(src, dst, w, directed):
     import torch.distributed as dist
     P = dist.get_world_size()
     dev = src.device
-    on_host = dist.get_backend() == "gloo"  # gloo collectives take host tensors
+    from .comms.comms import collective_device
     s, d = src.to(torch.int64), dst.to(torch.int64)
     if not directed:  # canonical pair: the smaller id first
         s, d = torch.minimum(s, d), torch.maximum(s, d)
-    if on_host:
-        s, d = s.cpu(), d.cpu()
-        w = None if w is None else w.cpu()
+    cdev = collective_device()
+    s, d = s.to(cdev), d.to(cdev)
+    w = None if w is None else w.to(cdev)
     dest = _owner(s, d, P)
     s, d = _exchange(s, dest, P), _exchange(d, dest, P)
     ww = None if w is None else _exchange(w, dest, P)

@@ -9,7 +9,8 @@ libcugraph_c communicators over the default ``torch.distributed`` group -- RCCL
 torch.distributed callbacks (``backend="torch"``: gloo, several ranks on one GPU,
 for tests).  The 2D grid follows the reference: ``prows x pcols`` given, or pcols
 = the largest divisor of the world size not above its square root
-(``__get_2D_div``, comms.py:40-45), so 8 GPUs make 2 x 4.
+(``__get_2D_div``, comms.py:40-45), so 8 GPUs make R x C = 4 x 2 (row communicators
+of 2).
 """
 from __future__ import annotations
 
@@ -56,6 +57,19 @@ def initialize(comms=None, p2p=False, prows=None, pcols=None, partition_type=1, 
     p = _plc()
     ctx = p.comms.init_rccl(C) if backend == "rccl" else p.comms.init_torch(C)
     _state.update(ctx=ctx, handle=p.ResourceHandle(ctx.ptr), R=world // C, C=C, backend=backend)
+
+
+def collective_device():
+    """Device for the small host-side collectives of the Python driver (max id,
+    edge counts, start-vertex checks): CPU when the default group runs them on
+    gloo ("gloo" or "cpu:gloo,cuda:nccl"), else the GPU (an RCCL-only group
+    refuses CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+    b = str(dist.get_backend())
+    if b == "gloo" or "cpu:gloo" in b:
+        return torch.device("cpu")
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def is_initialized():

@@ -127,11 +127,12 @@ class Graph:
                 w = w.to(torch.float32)
             self.graph_properties.weights = True
         src, dst, w = _shuffle.shuffle_dedup(src, dst, w, self.graph_properties.directed)
-        hi = torch.tensor([int(max(src.max(), dst.max())) if src.numel() else 0], dtype=torch.int64)
+        cdev = dcomms.collective_device()
+        hi = torch.tensor([int(max(src.max(), dst.max())) if src.numel() else 0], dtype=torch.int64, device=cdev)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         vt = torch.int32 if int(hi) < 2**31 - 1 else torch.int64
         src, dst = src.to(vt), dst.to(vt)
-        ne = torch.tensor([src.numel()], dtype=torch.int64)
+        ne = torch.tensor([src.numel()], dtype=torch.int64, device=cdev)
         dist.all_reduce(ne)
         self.edgelist = {"src": src, "dst": dst, "weights": w}
         self.store_transposed = bool(store_transposed)

@@ -75,6 +75,10 @@ class ResourceHandle:
     def last_louvain_levels(self):
         return _lib.lib.cugraph_amd_last_louvain_levels(self.c_resource_handle_ptr)
 
+    def last_louvain_sweep_bytes(self):
+        """Multi-GPU Louvain: average bytes this rank sent per local-move sweep."""
+        return _lib.lib.cugraph_amd_last_louvain_sweep_bytes(self.c_resource_handle_ptr)
+
     def measure_copy_bandwidth(self, nbytes=4 << 30, reps=10):
         """HBM ceiling: 16-B-per-lane copy kernel on this handle's stream, GB/s (read + write)."""
         r = _lib.lib.cugraph_amd_measure_copy_bandwidth(self.c_resource_handle_ptr, int(nbytes), int(reps))

@@ -129,18 +129,21 @@ _TYPESTR = {_lib.INT32: "<i4", _lib.INT64: "<i8", _lib.FLOAT32: "<f4", _lib.FLOA
 class ResultOwner:
     """Keeps a libcugraph_c result -- and the device arrays it owns -- alive while
     tensors view its arrays; frees it when the last of them is gone.  The free
-    returns the memory to the library's stream-ordered cache, so the caller's
-    stream is synchronised first: no reader on it can still be running when the
+    returns the memory to the library's stream-ordered cache, which reuses blocks
+    without waiting on other streams, so the whole device that owns the arrays is
+    synchronised first: no reader on any stream (torch's current one, a side
+    stream, another device's current stream) can still be running when the
     library reuses the block."""
 
     def __init__(self, ptr, free_fn):
         self.ptr = ptr
         self._free = free_fn
+        self._device = _torch().cuda.current_device()
 
     def __del__(self, _sd=_lib.SHUTDOWN):
         if getattr(self, "ptr", None) and not _sd[0]:
             try:
-                _torch().cuda.current_stream().synchronize()
+                _torch().cuda.synchronize(self._device)
             finally:
                 self._free(self.ptr)
                 self.ptr = None

@@ -103,6 +103,9 @@ size_t cugraph_amd_last_bfs_levels(const cugraph_resource_handle_t* handle);
 size_t cugraph_amd_last_bfs_bottom_up_steps(const cugraph_resource_handle_t* handle);
 /* Louvain: levels of the last call */
 size_t cugraph_amd_last_louvain_levels(const cugraph_resource_handle_t* handle);
+/* Multi-GPU Louvain: average bytes this rank sent per local-move sweep (cluster
+ * lookups, weight deltas, ghost updates) in the last call; 0 on one GPU */
+double cugraph_amd_last_louvain_sweep_bytes(const cugraph_resource_handle_t* handle);
 /* Louvain dendrogram (the reference C++ API returns Dendrogram<vertex_t>,
  * louvain_impl.cuh:280-301; the C ABI only exposes the flattened clustering).
  * Level i holds the cluster of every level-i vertex this rank owns, in global-id

@@ -1,10 +1,20 @@
 """Parity at the benchmark sizes (the exact graphs bench.py builds and times).
 
+* Graph structure of RMAT-22 and RMAT-24 (both orientations), checked
+  independently of the library: the symmetrised, de-duplicated edge set is rebuilt
+  from the same generator output with plain torch ops (sort + unique of
+  ``min << 32 | max`` keys) and compared with the CSR/CSC edge set mapped through
+  the number map; degrees are non-increasing in internal id with ties by ascending
+  external id (create_graph_from_edgelist_impl.cuh:557-776,
+  renumber_edgelist_impl.cuh:384-390, symmetrize.py:78-93); rows are strictly
+  increasing (sorted, no multi-edges).
 * PageRank on RMAT-22 (configs[1]) and RMAT-24 (the headline): the HIP path
   against the fp64 oracle (oracle/cpu_baseline.c cpu_pagerank_f64 -- the numpy
   oracle's arithmetic compiled with OpenMP, checked against it in
   tests/test_cpu_baseline.py) at 1e-6 relative per vertex, same iteration count
-  within one (the L1 sum order differs).
+  within one (the L1 sum order differs).  Unweighted (the C-ABI bench leg) and
+  all-ones fp32 weights (what the reference's cugraph.Graph attaches,
+  simpleGraph.py:840-843) on RMAT-22.
 * BFS on RMAT-24 (configs[2]) from all 8 bench roots, direction-optimising:
   distances bit-exact against the compiled restatement of the reference's
   bfs_reference (bfs_test.cpp:41-79), plus Graph500-style full-size properties
@@ -14,9 +24,7 @@
     pred[v] = min{u in N(v) : d[u] = d[v] - 1} (the build's tie rule: smallest
     internal id), computed with scatter_reduce(amin).
 
-The oracle input is the library's own adjacency of the GPU-built graph (graph
-construction is pinned against the oracle's at smaller scales by
-tests/test_gpu_rmat.py and the dataset tests).
+Each bench graph is built once per module (fixtures) and shared by its tests.
 """
 import numpy as np
 import pytest
@@ -39,42 +47,148 @@ def _cpu():
     return cpu_native
 
 
-@pytest.mark.parametrize("scale", [22, 24])
-def test_pagerank_bench_graph_vs_fp64_oracle(scale):
+class _Bench:
+    """One bench graph (bench.build_rmat_graph) with its handle, number map and
+    host copies of the adjacency, built once and shared by the module's tests."""
+
+    def __init__(self, scale, want_roots=0):
+        import torch
+        bench, p = _bench()
+        self.scale, self.p = scale, p
+        self.h = p.ResourceHandle()
+        self.g, self.roots, _ = bench.build_rmat_graph(p, self.h, scale, transposed=True, want_roots=want_roots)
+        # result vertices are the number map in internal order (pagerank.cpp:231-237)
+        v, _ = p.pagerank(self.h, self.g, None, None, None, None, 0.85, 1e-2, 500, False)
+        self.number_map = v.to(torch.int64)
+        self._host = {}
+
+    def adjacency(self, transposed):
+        return self.g.adjacency(self.h, transposed=transposed)
+
+    def host_adjacency(self, transposed):
+        if transposed not in self._host:
+            off, idx, _ = self.adjacency(transposed)
+            self._host[transposed] = (off.cpu().numpy().astype(np.int64), idx.cpu().numpy())
+        return self._host[transposed]
+
+    def close(self):
+        import torch
+        self.g = None
+        self._host.clear()
+        torch.cuda.synchronize()
+        self.p.trim_device_cache()
+        torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def rmat22():
+    b = _Bench(22)
+    yield b
+    b.close()
+
+
+@pytest.fixture(scope="module")
+def rmat24():
+    b = _Bench(24, want_roots=8)
+    yield b
+    b.close()
+
+
+def _check_structure(b, transposed):
+    """The library's adjacency against an independent torch rebuild of the
+    symmetrised, de-duplicated edge set of the same generator output."""
     import torch
-    bench, p = _bench()
-    cpu = _cpu()
-    h = p.ResourceHandle()
-    g, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
+    p, h = b.p, b.h
+    n = 16 << b.scale
+    s, d = p.generators.generate_rmat_edgelist(h, b.scale, n, 0.57, 0.19, 0.19, 42, False, True)
+    s, d = s.to(torch.int64), d.to(torch.int64)
+    lo, hi = torch.minimum(s, d), torch.maximum(s, d)
+    del s, d
+    want = torch.unique(lo << 32 | hi)  # sorted undirected edges, self loops once
+    verts = torch.unique(torch.cat([lo, hi]))
+    del lo, hi
+    nm = b.number_map
+    V = nm.numel()
+    assert V == verts.numel(), "vertex count differs from the edge list's endpoint set"
+    assert torch.equal(torch.sort(nm).values, verts), "number map is not the endpoint set"
+    off, idx, w = b.adjacency(transposed)
+    assert w is None
+    off = off.to(torch.int64)
+    assert off.numel() == V + 1 and int(off[0]) == 0
+    deg = off[1:] - off[:-1]
+    assert bool((deg[:-1] >= deg[1:]).all()), "degrees increase somewhere in internal id order"
+    tie = deg[:-1] == deg[1:]
+    assert bool((nm[:-1][tie] < nm[1:][tie]).all()), "equal-degree vertices not in ascending external id"
+    rows = torch.repeat_interleave(torch.arange(V, device=off.device), deg)
+    idx = idx.to(torch.int64)
+    same_row = rows[1:] == rows[:-1]
+    assert bool((idx[1:][same_row] > idx[:-1][same_row]).all()), "a row is unsorted or holds a multi-edge"
+    u, v = nm[rows], nm[idx]
+    del rows, idx, same_row
+    if transposed:  # CSC: major = destination
+        u, v = v, u
+    fwd = u <= v
+    got = torch.sort(u[fwd] << 32 | v[fwd]).values
+    assert torch.equal(got, want), "edge set (u <= v) differs from the independent rebuild"
+    back = torch.sort(v[~fwd] << 32 | u[~fwd]).values
+    nonself = (want >> 32) != (want & 0xFFFFFFFF)
+    assert torch.equal(back, want[nonself]), "the graph is not symmetric"
+    E = u.numel()
+    print(f"RMAT-{b.scale} {'CSC' if transposed else 'CSR'}: V={V} E={E} ({int(want.numel())} undirected) ok")
+    assert E == b.g.number_of_edges()
+
+
+@pytest.mark.parametrize("scale", [22, 24])
+@pytest.mark.parametrize("transposed", [True, False])
+def test_bench_graph_structure_independent(scale, transposed, request):
+    _check_structure(request.getfixturevalue(f"rmat{scale}"), transposed)
+
+
+def _pagerank_vs_oracle(b, g, weighted):
+    import torch
+    p, h = b.p, b.h
     v, pr = p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False)
     it_gpu = h.last_iterations()
-    off, idx, _ = g.adjacency(h, transposed=True)
-    off_h, idx_h = off.cpu().numpy().astype(np.int64), idx.cpu().numpy()
-    del off, idx
-    ref, it_ref = cpu.pagerank_f64(off_h, idx_h, 0.85, 1e-6, 500, threads=16)
+    assert torch.equal(v.to(torch.int64), b.number_map)
+    off_h, idx_h = b.host_adjacency(True)
+    ref, it_ref = _cpu().pagerank_f64(off_h, idx_h, 0.85, 1e-6, 500, threads=16)
     got = pr.cpu().numpy().astype(np.float64)
     rel = np.abs(got - ref) / ref
-    print(f"RMAT-{scale}: V={ref.size} E={idx_h.size} iterations gpu {it_gpu} oracle {it_ref} "
-          f"max rel {rel.max():.3e}")
+    print(f"RMAT-{b.scale}{' weighted' if weighted else ''}: V={ref.size} E={idx_h.size} iterations gpu {it_gpu} "
+          f"oracle {it_ref} max rel {rel.max():.3e}")
     assert abs(it_gpu - it_ref) <= 1
     assert rel.max() < REL
     assert abs(got.sum() - 1.0) < 1e-4
+
+
+@pytest.mark.parametrize("scale", [22, 24])
+def test_pagerank_bench_graph_vs_fp64_oracle(scale, request):
+    b = request.getfixturevalue(f"rmat{scale}")
+    _pagerank_vs_oracle(b, b.g, False)
+
+
+def test_pagerank_rmat22_all_ones_weights_vs_fp64_oracle(rmat22):
+    """The graph the reference's cugraph.Graph builds for an unweighted edge list:
+    the same edges with all-ones fp32 weights (simpleGraph.py:840-843)."""
+    import torch
+    bench, p = _bench()
+    b = rmat22
+    g, _, _ = bench.build_rmat_graph(p, b.h, 22, transposed=True, weighted="ones")
+    _pagerank_vs_oracle(b, g, True)
     del g
     torch.cuda.synchronize()
-    p.trim_device_cache()
 
 
-def _bfs_properties(off, idx, dist, pred_ext, number_map, src, chunk=1 << 26):
-    """Full-size device checks; off/idx the CSR (internal ids), dist by internal id,
-    pred_ext external ids, number_map internal -> external."""
+def _bfs_properties(off, idx, rows_all, dist, pred_ext, number_map, src, chunk=1 << 26):
+    """Full-size device checks; off/idx the CSR (internal ids), rows_all the row of
+    every CSR entry, dist by internal id, pred_ext external ids, number_map
+    internal -> external."""
     import torch
     V = off.numel() - 1
     dev = dist.device
     d64 = dist.to(torch.int64)
     assert int(d64[src]) == 0
     minp = torch.full((V,), INF, dtype=torch.int64, device=dev)
-    deg = (off[1:] - off[:-1]).to(torch.int64)
-    rows_all = torch.repeat_interleave(torch.arange(V, device=dev, dtype=torch.int64), deg)
     E = idx.numel()
     for lo in range(0, E, chunk):
         hi = min(E, lo + chunk)
@@ -88,7 +202,6 @@ def _bfs_properties(off, idx, dist, pred_ext, number_map, src, chunk=1 << 26):
         cand = both & (du == dv - 1)
         minp.scatter_reduce_(0, v[cand], u[cand], reduce="amin")
         del u, v, du, dv, ru, rv, both, cand
-    del rows_all
     reached = d64 != INF
     nonsrc = reached.clone()
     nonsrc[src] = False
@@ -100,31 +213,30 @@ def _bfs_properties(off, idx, dist, pred_ext, number_map, src, chunk=1 << 26):
     assert bool((pred_ext.to(torch.int64) == want).all()), "predecessor is not the smallest-id parent"
 
 
-def test_bfs_rmat24_all_bench_roots():
+def test_bfs_rmat24_all_bench_roots(rmat24):
     import torch
-    bench, p = _bench()
-    cpu = _cpu()
-    h = p.ResourceHandle()
-    g, roots, _ = bench.build_rmat_graph(p, h, 24, transposed=False, want_roots=8)
-    assert len(roots) == 8
-    off, idx, _ = g.adjacency(h, transposed=False)
-    off_h, idx_h = off.cpu().numpy().astype(np.int64), idx.cpu().numpy()
+    b = rmat24
+    p, h, g = b.p, b.h, b.g
+    assert len(b.roots) == 8
+    off, idx, _ = b.adjacency(False)
+    off_h, idx_h = b.host_adjacency(False)
+    deg = (off[1:] - off[:-1]).to(torch.int64)
+    rows_all = torch.repeat_interleave(torch.arange(off.numel() - 1, device=off.device, dtype=torch.int64), deg)
     bottom_up = 0
-    for r in roots:
+    for r in b.roots:
         dist, pred, verts = p.bfs(h, g, torch.tensor([int(r)], dtype=torch.int32, device="cuda"), True, 0, True,
                                   False)
         bottom_up += h.last_bfs_bottom_up_steps()
-        vh = verts.cpu().numpy()
-        src = int(np.nonzero(vh == r)[0][0])
-        _bfs_properties(off, idx, dist, pred, verts, src)
-        _, dref, _ = cpu.bfs(off_h, idx_h, src, threads=16)
+        assert torch.equal(verts.to(torch.int64), b.number_map)
+        src = int(torch.nonzero(b.number_map == int(r))[0, 0])
+        _bfs_properties(off, idx, rows_all, dist, pred, verts, src)
+        _, dref, _ = _cpu().bfs(off_h, idx_h, src, threads=16)
         assert np.array_equal(dist.cpu().numpy(), dref), f"root {r}: distances differ from the reference restatement"
         print(f"root {r}: reached {int((dref != INF).sum())}, levels {h.last_bfs_levels()}, "
               f"bottom-up steps {h.last_bfs_bottom_up_steps()}")
     assert bottom_up > 0  # the direction-optimising path was exercised
-    del g, off, idx
+    del off, idx, rows_all, deg
     torch.cuda.synchronize()
-    p.trim_device_cache()
 
 
 def test_louvain_bench_graph_modularity():
@@ -145,7 +257,11 @@ def test_louvain_bench_graph_modularity():
     w64 = w.to(torch.float64)
     m = w64.sum()
     internal = torch.where(c[rows] == c[idx.to(torch.int64)], w64, torch.zeros_like(w64)).sum()
-    k = torch.zeros(V, dtype=torch.float64, device=off.device).index_add_(0, rows, w64)
+    # row sums from a prefix sum (an index_add_ of 259M fp64 atomics onto the hub rows
+    # took ~2 minutes)
+    cs = torch.cat([torch.zeros(1, dtype=torch.float64, device=off.device), torch.cumsum(w64, 0)])
+    off64 = off.to(torch.int64)
+    k = cs[off64[1:]] - cs[off64[:-1]]
     a = torch.zeros(int(c.max()) + 1, dtype=torch.float64, device=off.device).index_add_(0, c, k)
     Q = float(internal / m - (a * a).sum() / (m * m))
     print(f"RMAT-23 Louvain: Q reported {q:.12f} recomputed {Q:.12f}, levels {h.last_louvain_levels()}, "

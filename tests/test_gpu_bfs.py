@@ -187,3 +187,55 @@ def test_result_tensors_own_library_memory():
     gc.collect()
     assert np.array_equal(host(view), snap[0][1:])
     assert np.array_equal(host(pred), snap[1]) and np.array_equal(host(verts), snap[2])
+
+
+@pytest.mark.parametrize("scale", [14, 18])
+def test_bitmap_to_queue_conversion_device_vs_host(scale, monkeypatch, capfd):
+    """A bottom-up -> top-down switch converts the frontier bitmap to queues with the
+    queue lengths read on the device (default) or on the host (CGX_BFS_CONV_SYNC=1,
+    and the memcpy + synchronize form CGX_BFS_SYNC=1): same distances and
+    predecessors, and the runs do contain such a switch (CGX_BFS_DEBUG level log)."""
+    s, d = rmat_sym(scale)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    deg = np.bincount(s)
+    srcs = [int(np.argmax(deg)), int(s[len(s) // 3])]
+    monkeypatch.setenv("CGX_BFS_DEBUG", "1")
+    capfd.readouterr()
+    base = [run(h, G, [x], True) for x in srcs]
+    log = capfd.readouterr().err
+    dirs = [ln.split()[3] for ln in log.splitlines() if ln.startswith("[bfs] level")]
+    assert any(a == "bottom-up" and b == "top-down" for a, b in zip(dirs, dirs[1:])), log[-2000:]
+    for env in ("CGX_BFS_CONV_SYNC", "CGX_BFS_SYNC"):
+        monkeypatch.setenv(env, "1")
+        for x, (v0, d0, p0) in zip(srcs, base):
+            v, dist, pred = run(h, G, [x], True)
+            assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0), env
+        monkeypatch.delenv(env)
+    if scale == 14:
+        for x, (v0, d0, p0) in zip(srcs, base):
+            check_vs_oracle(s, d, v0, d0, p0, [x])
+
+
+def test_result_freed_after_side_stream_reader():
+    """A result tensor read on a non-default stream, then dropped: its memory goes
+    back to the library's cache only after the device is synchronised
+    (ResultOwner.__del__), so the next algorithm's arrays cannot overwrite it while
+    the side-stream reader still runs."""
+    import gc
+    import torch
+    s, d = rmat_sym(16)
+    h, G = make_graph(s, d, None, renumber=True, symmetric=True)
+    src = np.asarray([int(s[0])], np.int32)
+    dist, pred, verts = plc().bfs(h, G, src, True, 0, True, False)
+    want = dist.clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        acc = torch.zeros_like(dist, dtype=torch.int64)
+        for _ in range(50):  # a long reader queued on the side stream
+            acc += dist.to(torch.int64)
+    del dist, pred, verts
+    gc.collect()
+    plc().bfs(h, G, np.asarray([int(d[-1])], np.int32), True, 0, True, False)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, want.to(torch.int64) * 50)
