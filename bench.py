@@ -167,12 +167,12 @@ def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want
 
 
 # ----------------------------------------------------------------------------- PageRank
-def pagerank_leg(p, args, scale, steps, warmup, ctx=None):
+def pagerank_leg(p, args, scale, steps, warmup, ctx=None, weighted=False):
     import torch
     h = p.ResourceHandle(ctx.ptr if ctx else None)
     barrier(args)
     t0 = time.perf_counter()
-    g, _, _ = build_rmat_graph(p, h, scale, mg=args.mg)
+    g, _, _ = build_rmat_graph(p, h, scale, weighted=weighted, mg=args.mg)
     build_s = max_over_ranks(args, time.perf_counter() - t0)
     V, E = g.number_of_vertices(), g.number_of_edges()
     log(f"[bench] pagerank RMAT-{scale}: V={V} E={E} (build {build_s:.2f}s)")
@@ -194,8 +194,8 @@ def pagerank_leg(p, args, scale, steps, warmup, ctx=None):
     t = max_over_ranks(args, time.perf_counter() - t0)
     h.set_profiling(False)
     value = E * sum(iters) / t
-    # algorithmic bytes of one rank's share: (4E + 16V) / N
-    bytes_per_iter = (4 * E + 16 * V) / args.world
+    # algorithmic bytes of one rank's share: (4E + 16V) / N, +4E weighted
+    bytes_per_iter = ((8 if weighted else 4) * E + 16 * V) / args.world
     avg_ms = kms / max(klaunch, 1)
     achieved = bytes_per_iter / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     log(f"[bench] pagerank RMAT-{scale}: {value:.4g} edges/s, iters {iters}, {avg_ms:.4f} ms/iter, "
@@ -655,6 +655,23 @@ def main():
                 r2 = pagerank_leg(p, args, 22, args.steps, args.warmup)
                 out["pagerank_rmat22"] = pagerank_summary(r2, args, "sg")
                 del r2
+                release_caches(p)
+                # the reference Python path's graph: all-ones fp32 weights (simpleGraph.py:840-843),
+                # detected at the first call and run on the unweighted push; then the same graph
+                # on the entry-weight push (CGX_PR_UNIT_W=0: 32-bit entries + 4 B weights)
+                for key, env in (("pagerank_rmat24_weighted", None), ("pagerank_rmat24_weighted_entry_push", "0")):
+                    if env is not None:
+                        os.environ["CGX_PR_UNIT_W"] = env
+                    try:
+                        r2 = pagerank_leg(p, args, args.scale, max(1, args.steps // 2), 1, weighted="ones")
+                    finally:
+                        os.environ.pop("CGX_PR_UNIT_W", None)
+                    out[key] = pagerank_summary(r2, args, "sg")
+                    out[key]["weights"] = "all-ones fp32 (cugraph.Graph unweighted edge list)"
+                    out[key]["push"] = ("unweighted 16-bit entries (unit weights detected)" if env is None else
+                                        "32-bit entries + fp32 entry weights (CGX_PR_UNIT_W=0)")
+                    del r2
+                    release_caches(p)
             else:
                 alt = p.comms.flat_row_comm_size(world) if C != p.comms.flat_row_comm_size(world) \
                     else p.comms.default_row_comm_size(world)

@@ -38,21 +38,55 @@ constexpr int kSmallDeg = 16;    // 4-lane groups
 constexpr int kMidDeg   = 1024;  // one wave; above: edge chunks over blocks
 constexpr int kChunk    = 2048;  // edges per large-class chunk
 
-struct bfs_ctr {
+// What the host reads of a level (64 B)
+struct bfs_ctr_hdr {
   unsigned long long qlen[3];  // next queues: small / mid / large (first: bfs_args::ncur_dev points here)
   unsigned long long next_n;   // vertices discovered this level
   unsigned long long next_m;   // sum of their degrees
   unsigned long long pad[3];
 };
 
-// level counters -> the handle's pinned host block (zero-copy), so the per-level
-// host read is one tiny kernel instead of a D2H copy command
-__global__ void k_publish_ctr(bfs_ctr const* ctr, bfs_ctr* host)
+// The device block.  Every kernel block adds its discovered-vertex and edge counts
+// at the end (flush_counts); same-address atomics serialise at the memory side
+// (~8 ns each), so the block counts go to kCtrParts partial counters 256 B apart
+// (different L2 channels) and the publish kernel folds them into next_n / next_m.
+// That lets the bottom-up probe run on larger grids.
+constexpr int kCtrParts = 16;
+struct bfs_ctr : bfs_ctr_hdr {
+  unsigned long long part[kCtrParts][32];  // [p][0]: vertices, [p][1]: edges
+};
+
+// (next_n, next_m) of a block with the partial counters folded in; lanes 0..15 of
+// one wave read the parts, every lane gets the totals; zero: clear the parts
+__device__ __forceinline__ void fold_parts(bfs_ctr* c, bool zero, unsigned long long& n, unsigned long long& m)
 {
+  int const lane = threadIdx.x & 63;
+  unsigned long long pn = 0, pm = 0;
+  if (lane < kCtrParts) {
+    pn = c->part[lane][0];
+    pm = c->part[lane][1];
+    if (zero) {
+      c->part[lane][0] = 0ull;
+      c->part[lane][1] = 0ull;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    pn += __shfl_xor(pn, o, 64);
+    pm += __shfl_xor(pm, o, 64);
+  }
+  n = pn + c->next_n;
+  m = pm + c->next_m;
+}
+
+// level counters -> the handle's pinned host block (A/B form of the poll)
+__global__ void k_publish_ctr(bfs_ctr* ctr, bfs_ctr_hdr* host)
+{
+  unsigned long long n, m;
+  fold_parts(ctr, false, n, m);
   int const i = threadIdx.x;
-  if (i < (int)(sizeof(bfs_ctr) / 8))
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(host) + i, reinterpret_cast<unsigned long long const*>(ctr)[i],
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned long long v = i < 3 ? ctr->qlen[i] : (i == 3 ? n : m);
+  if (i < 5)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(host) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the level counters (then zeroed for the next level: no memset launch per level)
@@ -60,25 +94,29 @@ __global__ void k_publish_ctr(bfs_ctr const* ctr, bfs_ctr* host)
 // a system fence.  ctr_b: a second level's counters (a speculative top-down level)
 // -> host[1], also zeroed; src_m: the sources' edge count of a conversion the host
 // did not read (bfs_ctr::next_m of that block) -> pad[2]
-__global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr* host, unsigned long long seq, int const* bad, bfs_ctr* ctr_b,
-                              bfs_ctr const* src_m)
+__global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr_hdr* host, unsigned long long seq, int const* bad, bfs_ctr* ctr_b,
+                              bfs_ctr* src_m)
 {
+  unsigned long long n, m, nb = 0, mb = 0, ns = 0, ms = 0;
+  fold_parts(ctr, true, n, m);
+  if (ctr_b) fold_parts(ctr_b, true, nb, mb);
+  if (src_m) fold_parts(src_m, false, ns, ms);
   if (threadIdx.x != 0) return;
   unsigned long long* c  = reinterpret_cast<unsigned long long*>(ctr);
   unsigned long long* hp = reinterpret_cast<unsigned long long*>(host);
   for (int i = 0; i < 5; ++i) {
-    __hip_atomic_store(hp + i, c[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hp + i, i < 3 ? c[i] : (i == 3 ? n : m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     c[i] = 0ull;
   }
   if (ctr_b) {
     unsigned long long* cb = reinterpret_cast<unsigned long long*>(ctr_b);
     unsigned long long* hb = reinterpret_cast<unsigned long long*>(host + 1);
     for (int i = 0; i < 5; ++i) {
-      __hip_atomic_store(hb + i, cb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(hb + i, i < 3 ? cb[i] : (i == 3 ? nb : mb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       cb[i] = 0ull;
     }
   }
-  __hip_atomic_store(&host->pad[2], src_m ? src_m->next_m : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&host->pad[2], ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&host->pad[1], bad ? (unsigned long long)*bad : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();
   __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -233,8 +271,9 @@ __device__ __forceinline__ void flush_counts(bfs_ctr* ctr, unsigned long long n,
   if (threadIdx.x == 0) {
     unsigned long long tn = sn[0] + sn[1] + sn[2] + sn[3];
     unsigned long long tm = sm_[0] + sm_[1] + sm_[2] + sm_[3];
-    if (tn) atomicAdd(&ctr->next_n, tn);
-    if (tm) atomicAdd(&ctr->next_m, tm);
+    int const pi = blockIdx.x % kCtrParts;
+    if (tn) atomicAdd(&ctr->part[pi][0], tn);
+    if (tm) atomicAdd(&ctr->part[pi][1], tm);
   }
 }
 
@@ -736,7 +775,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   }
   // ctr2: queue lengths of a bitmap -> queues conversion; ctr3: a speculative level's counters
   dbuf<bfs_ctr> ctr(1, s), ctr2(1, s), ctr3(1, s);
-  bfs_ctr* hctr = h.pinned_as<bfs_ctr>();
+  bfs_ctr_hdr* hctr = h.pinned_as<bfs_ctr_hdr>();
 
   bfs_args<V, E> a{};
   a.off   = adj.offsets.data<E>();
@@ -759,9 +798,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // sequence word -- no hipStreamSynchronize per level (CGX_BFS_SYNC=1: the
   // memcpy + synchronize form, A/B)
   bool const poll = std::getenv("CGX_BFS_SYNC") == nullptr && !ctr_memcpy;
-  bfs_ctr* pctr   = poll ? h.polled_as<bfs_ctr>() : nullptr;
+  bfs_ctr_hdr* pctr = poll ? h.polled_as<bfs_ctr_hdr>() : nullptr;  // [0]: a level, [1]: a speculative level
   // ctr_b / src_m: see k_publish_seq (poll mode only)
-  auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr const* src_m = nullptr) {
+  auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr* src_m = nullptr) {
     if (poll) {
       unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
       hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m);
@@ -775,11 +814,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
             throw std::runtime_error("BFS: level counters not published");
         }
       }
-      std::memcpy(hctr, pctr, sizeof(bfs_ctr));
+      std::memcpy(hctr, pctr, sizeof(bfs_ctr_hdr));
       return;
     }
-    if (ctr_memcpy) hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(64), 0, s, ctr.data(), hctr);
-    else HIP_CHECK(hipMemcpyAsync(hctr, ctr.data(), sizeof(bfs_ctr), hipMemcpyDeviceToHost, s));
+    // (the partial counters need the fold: the copy form also goes through the kernel)
+    hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(64), 0, s, ctr.data(), hctr);
     HIP_CHECK(hipStreamSynchronize(s));
   };
   auto zero_ctr = [&]() { HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(bfs_ctr), s)); };
@@ -863,8 +902,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
                                                                    : 1024u;
     // (top-down segments capped at 1024 blocks each: 176.5K vs 148K MTEPS uncapped; 256-2048 within noise)
     long long const td_cap = std::getenv("CGX_BFS_TD_CAP") ? std::atoll(std::getenv("CGX_BFS_TD_CAP")) : 1024;
+    // probe grid: with the level counters spread over kCtrParts slots the block-end
+    // atomics no longer serialise, and more waves hide the probe's dependent loads
+    // (RMAT-24, 3 reps x 8 roots: 1024 / 2048 / 4096 blocks = 318K / 335K / 339K MTEPS)
     unsigned const probe_grid = std::getenv("CGX_BFS_PROBE_GRID") ? (unsigned)std::atoi(std::getenv("CGX_BFS_PROBE_GRID"))
-                                                                  : 1024u;
+                                                                  : 4096u;
     // Direction switch thresholds (Beamer's form).  Our bottom-up is cheap per edge
     // (hub-first adjacency, early exit), so it pays to stay top-down longer and
     // bottom-up longer than Beamer's alpha 14 / beta 24.  RMAT-24 harmonic-mean MTEPS
@@ -984,7 +1026,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           hipLaunchKernelGGL((k_topdown<V, E>), dim3(sl + sm + ss), dim3(kBlock), 0, s, b);
           CGX_LAUNCH_CHECK();
           read_ctr(nullptr, ctr3.data());
-          bfs_ctr const l2 = pctr[1];
+          bfs_ctr_hdr const l2 = pctr[1];
           unsigned long long const n1 = hctr->qlen[0] + hctr->qlen[1] + hctr->qlen[2];
           unsigned long long const m1 = hctr->next_m;
           if (dbg)

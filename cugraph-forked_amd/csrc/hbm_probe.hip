@@ -1,8 +1,7 @@
 // Measured HBM ceiling for the roofline lines of bench.py ("also
-// report a measured stream-copy ceiling").  A 16-byte-per-lane grid-stride copy,
-// the access shape MI355X_MICROARCH.md quotes its 6.29 TB/s float4 copy for; four
-// loads in flight per lane before the stores, nontemporal on both sides so the
-// copy does not fill the caches it is measuring past.  Timed with HIP events on
+// report a measured stream-copy ceiling").  A 16-byte-per-lane copy, the access
+// shape MI355X_MICROARCH.md quotes its 6.29 TB/s float4 copy for, nontemporal on
+// both sides so the copy does not fill the caches it is measuring past.  Timed with HIP events on
 // the handle's stream; bytes = read + write.
 #include "capi.hpp"
 
@@ -45,7 +44,10 @@ extern "C" double cugraph_amd_measure_copy_bandwidth(const cugraph_resource_hand
     if (n <= 0 || reps <= 0) return 0.0;
     buffer a(n * sizeof(u32x4), s), b(n * sizeof(u32x4), s);
     HIP_CHECK(hipMemsetAsync(a.data(), 0, n * sizeof(u32x4), s));
-    int const grid = 256 * 8;  // 8 blocks per CU, grid-stride
+    // one-shot grid (about one 16-B vector per lane, the tail of the unrolled loop
+    // takes it): scripts/ubench/mem_calib.hip measured 6.27 TB/s this way against
+    // 5.3-5.4 TB/s for persistent 2048-8192-block grids
+    int const grid = (int)std::min<int64_t>((n + kCopyBlock - 1) / kCopyBlock, 1 << 20);
     hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(kCopyBlock), 0, s, a.data<u32x4>(), b.data<u32x4>(), n);
     CGX_LAUNCH_CHECK();
     hipEvent_t e0 = h->event(0), e1 = h->event(1);

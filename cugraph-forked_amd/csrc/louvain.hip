@@ -1,4 +1,4 @@
-// Louvain modularity clustering (single GPU).
+// Louvain modularity clustering (single GPU; the multi-GPU driver is at the end).
 //
 // Reference: cpp/src/community/louvain_impl.cuh:46-301 (level loop, dendrogram,
 // flatten), community/detail/common_methods.cuh:49-382 (delta-modularity local
@@ -14,13 +14,20 @@
 // order differs from numpy's are exact for integer weights, so the clustering is
 // bit-identical there and modularity agrees to rounding otherwise.
 //
-// Each level is a COO sorted by (source, destination) with 32-bit ids.  A sweep:
-//   1. key = source << cb | cluster(destination) per edge (cb = cluster-id bits), radix sort;
-//   2. reduce_by_key -> (u, c, sum of w) for every (vertex, neighbour cluster);
-//   3. gain per pair, reduce_by_key over u with (max gain, smaller cluster) -> move.
-// Cluster weights are a reduce_by_key over vertices sorted by cluster.  All
-// reductions are rocPRIM's fixed-partition scans or block-ordered sums: the run is
-// deterministic.
+// Each level is a COO sorted by (source, destination) with 32-bit ids.  A sweep
+// (the local move) aggregates every row's (neighbour cluster, weight) pairs in LDS
+// hash tables with 64-bit fixed-point sums, no per-sweep sort (plan_sweeps /
+// sweep below):
+//   * rows of <= 1024 edges: k_sweep_hash, one block per chunk of whole rows;
+//   * heavier rows: k_big_partials (2048-edge segments -> per-bucket partials),
+//     k_big_buckets (merge a bucket's partials, gains), k_big_move (best bucket);
+//   * a row the tables cannot hold (or a level with negative weights): the sort
+//     path sweep_sorted -- key = row << cb | cluster(destination), radix sort,
+//     reduce_by_key to (row, cluster, sum), gains, reduce_by_key over the row
+//     (also the A/B switch CGX_LOUVAIN_HASH=0).
+// Ties go to the smaller cluster id in every path.  Cluster weights are a
+// reduce_by_key over vertices sorted by cluster; the modularity's internal weight
+// comes from the sweep's own-cluster sums.  The run is deterministic.
 #include "capi.hpp"
 #include "comm.hpp"
 #include "mg_graph.hpp"

@@ -387,6 +387,8 @@ constexpr int kTileUnits   = 8;    // units per tile below 2^22 rows (RMAT-22: 8
 constexpr int kGroupItems  = 128;  // items per group dealt to a queue
 constexpr int kCtrStride   = 32;   // queue heads 128 B apart
 constexpr int kPushBlocks  = 512;  // persistent grid: two 1024-thread blocks per CU, 256 CUs
+constexpr int kSrcBinBits  = 14;   // source-range cut granularity: 16K sources
+constexpr int kMaxSliceRanges = 12;
 #ifndef CGX_APPLY_BATCH
 #define CGX_APPLY_BATCH 4
 #endif
@@ -453,6 +455,12 @@ struct push_args {
   uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
                             // its sums), 0 = stored whole; nullptr: clear every sum
   int win_bits;
+  int ngroups;     // source groups: the apply sums acc[g * nacc + v] over g (pr_push_t::ngroups)
+  int64_t nacc;    // per group
+  int64_t nwin;    // windows (win_multi is [ngroups][nwin])
+  uint32_t xmask;  // measurement only (CGX_PR_ABLATE_XMASK): x~ gathered at source & xmask; ~0u normally
+  int ablate;      // measurement only (CGX_PR_ABLATE): 1 = every unit re-reads its item's first unit's
+                   // entries (no entry stream), 2 = no LDS atomics (one register sum per thread)
 };
 
 template <typename T>
@@ -709,6 +717,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     // to whole segments), <= 0 for the waves past the end of a window's last unit
     int n      = (int)(units[ua].k1 - k0) - wave * kSegEntries;
     uint32_t base = __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]);
+    unsigned long long ablate_sum = 0;
     uint16_t ent[kRows];
 #pragma unroll
     for (int j = 0; j < kRows; ++j) ent[j] = nt_load(sa.ent16 + k0 + wave * kSegEntries + j * 64 + lane);  // padded
@@ -733,11 +742,11 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         for (int j = 0; j < kRows; ++j) {
           uint32_t const src = run + sc[j];
           run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-          xv[j] = x[src];  // every lane loads (jumps and padding read a valid source id)
+          xv[j] = x[src & sa.xmask];  // every lane loads (jumps and padding read a valid source id)
           xv[j] = live[j] ? xv[j] : xw_t(0);
         }
       }
-      int64_t const nx  = un + 1 < ub ? un + 1 : un;
+      int64_t const nx  = (sa.ablate & 1) ? ua : (un + 1 < ub ? un + 1 : un);
       int64_t const k0n = units[nx].k0;
       int const nn      = (int)(units[nx].k1 - k0n) - wave * kSegEntries;
       uint32_t const bn = sa.seg_base[nx * kSegsPerUnit + wave];
@@ -746,10 +755,18 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       for (int j = 0; j < kRows; ++j) ent_n[j] = nt_load(sa.ent16 + k0n + wave * kSegEntries + j * 64 + lane);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
       if (active) {
+        if (sa.ablate & 2) {
 #pragma unroll
-        for (int j = 0; j < kRows; ++j) {
-          if constexpr (ENC) atomicAdd(&acc[slot[j]], dec_fixed(xv[j]));
-          else atomicAdd(&acc[slot[j]], fixed_of(xv[j]));
+          for (int j = 0; j < kRows; ++j) {
+            if constexpr (ENC) ablate_sum += dec_fixed(xv[j]) ^ slot[j];
+            else ablate_sum += fixed_of(xv[j]) ^ slot[j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < kRows; ++j) {
+            if constexpr (ENC) atomicAdd(&acc[slot[j]], dec_fixed(xv[j]));
+            else atomicAdd(&acc[slot[j]], fixed_of(xv[j]));
+          }
         }
       }
 #pragma unroll
@@ -757,6 +774,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       n    = nn;
       base = __builtin_amdgcn_readfirstlane(bn);
     }
+    if (sa.ablate & 2) atomicAdd(&acc[tid], ablate_sum);  // keeps the ablated sums live
     flush_window<WB, V, E, R>(sa, acc, win);
   }
 }
@@ -790,16 +808,34 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
       old[j] = a.pr[v + j * stride];
       ow[j]  = a.outw[v + j * stride];
     }
+    if (sa.ngroups > 1) {  // sliced sources: one partial sum per group, integer adds (order-free)
+      unsigned long long fg[kApplyBatch];
+      for (int g = 1; g < sa.ngroups; ++g) {
+#pragma unroll
+        for (int j = 0; j < kApplyBatch; ++j) fg[j] = sa.acc[g * sa.nacc + v + j * stride];
+#pragma unroll
+        for (int j = 0; j < kApplyBatch; ++j) {
+          int64_t const vj = v + j * stride;
+          if (fg[j] && sa.win_multi[g * sa.nwin + (vj >> sa.win_bits)]) sa.acc[g * sa.nacc + vj] = 0ull;
+          f[j] += fg[j];
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kApplyBatch; ++j) {
-      if (f[j] && (!sa.win_multi || sa.win_multi[(v + j * stride) >> sa.win_bits])) sa.acc[v + j * stride] = 0ull;
-      vertex_update_from<V, E, R>(a, (V)(v + j * stride), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base,
-                                  pf, my_diff, my_dang);
+      int64_t const vj = v + j * stride;
+      if (sa.acc[vj] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
+      vertex_update_from<V, E, R>(a, (V)vj, (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf, my_diff,
+                                  my_dang);
     }
   }
   for (; v < a.nv; v += stride) {
-    unsigned long long f = sa.acc[v];
-    if (f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
+    unsigned long long f = 0;
+    for (int g = 0; g < sa.ngroups; ++g) {
+      unsigned long long const x = sa.acc[g * sa.nacc + v];
+      if (x && (!sa.win_multi || sa.win_multi[g * sa.nwin + (v >> sa.win_bits)])) sa.acc[g * sa.nacc + v] = 0ull;
+      f += x;
+    }
     vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
@@ -828,6 +864,43 @@ __global__ void k_push_keys(C const* cols, uint32_t const* rows, int64_t ne, int
     keys[e] = ((uint64_t)(rows[e] >> wb) << 32) | (uint32_t)cols[e];
     vals[e] = (uint32_t)e;
   }
+}
+
+// Source slices (see plan_slices): the key's high word is the virtual window
+// w * nslice + slice(source); slices are source ranges, so (virtual window, source)
+// order is (window, source) order with every window's entries grouped by slice
+struct slice_table {
+  int n;                 // ranges
+  uint32_t lo[kMaxSliceRanges + 1];  // range r = [lo[r], lo[r + 1]) of source ids
+  int sidx[kMaxSliceRanges];
+};
+
+template <typename C>
+__global__ void k_push_keys_sliced(C const* cols, uint32_t const* rows, int64_t ne, int wb, slice_table t, int nslice,
+                                   uint64_t* keys, uint32_t* vals)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const c = (uint32_t)cols[e];
+    int r            = 0;
+    while (r + 1 < t.n && c >= t.lo[r + 1]) ++r;
+    uint64_t const vw = (uint64_t)(rows[e] >> wb) * (uint64_t)nslice + (uint64_t)t.sidx[r];
+    keys[e]           = (vw << 32) | c;
+    vals[e]           = (uint32_t)e;
+  }
+}
+
+// entries per 2^kSrcBinBits-source bin (the out-degree histogram of the push)
+template <typename C>
+__global__ void k_src_hist(C const* cols, int64_t ne, int nbins, unsigned long long* cnt)
+{
+  extern __shared__ unsigned int h_bins[];
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) h_bins[b] = 0u;
+  __syncthreads();
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h_bins[(uint32_t)cols[e] >> kSrcBinBits], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x)
+    if (h_bins[b]) atomicAdd(cnt + b, (unsigned long long)h_bins[b]);
 }
 
 // first position of every window w in [0, nwin] among the sorted keys
@@ -897,12 +970,12 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
 // jumps in front of real entry k: its source gap D to the previous entry of the
 // window (0 before the window's first) is coded in the entry when D <= dmax,
 // else by ceil(D / pmax) jumps and an entry of delta 0
-__global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t dmax, uint32_t pmax,
-                              uint32_t* mj)
+__global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t const* vlo, int nsl,
+                              uint32_t dmax, uint32_t pmax, uint32_t* mj)
 {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t const w     = (int64_t)(keys[k] >> 32);
-    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
+    uint32_t const prev = k == ws[w] ? vlo[w % nsl] : (uint32_t)keys[k - 1];
     uint32_t const D    = (uint32_t)keys[k] - prev;
     mj[k]               = D > dmax ? (D + pmax - 1) / pmax : 0u;
   }
@@ -911,13 +984,14 @@ __global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* w
 // real entry k at k + cm[k] (cm = inclusive prefix of the jump counts), its jumps
 // right before it
 __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, int64_t ne,
-                         int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
-                         unsigned long long const* pb, int wb, uint32_t pmax, uint16_t* ent16)
+                         int64_t const* ws, uint32_t const* vlo, int nsl, uint32_t const* mj,
+                         unsigned long long const* cm, unsigned long long const* pb, int wb, uint32_t pmax,
+                         uint16_t* ent16)
 {
   uint32_t const jump = (1u << (16 - wb)) - 1, low = (1u << wb) - 1;
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t const w     = (int64_t)(keys[k] >> 32);
-    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
+    uint32_t const prev = k == ws[w] ? vlo[w % nsl] : (uint32_t)keys[k - 1];
     uint32_t const D    = (uint32_t)keys[k] - prev;
     uint32_t const m    = mj[k];
     int64_t const pos   = k + (int64_t)cm[k] + (int64_t)pb[w];
@@ -983,8 +1057,9 @@ __global__ void k_packed_unit_heads(uint32_t const* flag, uint32_t const* uid, i
 
 // running source before the first entry of every (unit, wave segment)
 __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t const* keys, int64_t ne,
-                            int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
-                            unsigned long long const* pb, uint32_t dmax, uint32_t pmax, uint32_t* seg_base)
+                            int64_t const* ws, uint32_t const* vlo, int nsl, uint32_t const* mj,
+                            unsigned long long const* cm, unsigned long long const* pb, uint32_t dmax, uint32_t pmax,
+                            uint32_t* seg_base)
 {
   int64_t const n = nunits * kSegsPerUnit;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1002,7 +1077,7 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
       uint32_t const m    = mj[k];
       int64_t const w     = (int64_t)(keys[k] >> 32);
       int64_t const j     = p - (k + (int64_t)cm[k] + (int64_t)pb[w] - m);
-      uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
+      uint32_t const prev = k == ws[w] ? vlo[w % nsl] : (uint32_t)keys[k - 1];
       uint32_t const src  = (uint32_t)keys[k];
       uint32_t const D    = src - prev;
       base = j < (int64_t)m ? prev + pmax * (uint32_t)j : src - (m ? 0u : (D <= dmax ? D : 0u));
@@ -1017,7 +1092,6 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
 // every window go to XCD k's queue -- each XCD's L2 then holds the head plus 1/8 of
 // the tail's x~ (offline LRU model, RMAT-24 / 8K windows: 12.9M -> 0.4M L2 misses
 // per iteration).
-constexpr int kSrcBinBits = 14;  // cut granularity: 16K sources
 constexpr int kSrcParts   = kQueues;
 
 // entries per 2^kSrcBinBits-source bin: thread per (window, bin), two binary searches
@@ -1116,7 +1190,7 @@ inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std
 {
   int64_t const nunits = (int64_t)hu.size();
   bool const no_whole  = env_is("CGX_PR_WHOLE", "0");  // A/B: every flush adds, the apply clears every sum
-  std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.nwin, 1), 0);
+  std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.ngroups * pp.nwin, 1), 0);
   for (int64_t i = 0; i < nitems; ++i) {
     int64_t const u = item_u[i], last = item_u[i + 1] - 1;
     // the flag may already sit on an earlier item's first unit: compare and index
@@ -1214,6 +1288,160 @@ inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit* units, 
   upload_items(s, pp, item_u, queue, nitems);
 }
 
+// ---- source slices (default from 2^21 sources; CGX_PR_SLICE=0/1 overrides)
+// The push moves every x~ line a window needs from beyond the XCD's L2, and those
+// line fills are its bound (profiles/r03_counters.md: 128-B fills at up to 7.3 TB/s;
+// RMAT-24 33.9M (window, line) pairs per iteration, 4.1 GB).  Slicing the sources
+// keeps each XCD's x~ working set in its 4 MB L2:
+//   head  = sources [0, H)        (the hubs, ~1 MB of x~; ~2/3 of the entries)
+//   mid_k = 8 source ranges after the head, k = 0..7, each <= F sources of x~ and
+//           about 1/8 of the mid entries
+//   tail  = the rest              (low degree: few entries, little reuse anyway)
+// Every window's entries are grouped (head, tail, mid_0, ..., mid_7) -- virtual
+// windows w * 10 + slice, each its own run of packed segments -- and summed in
+// 9 groups: group k < 8 = mid_k, group 8 = head + tail.  All group-k items (every
+// window's mid_k entries) are queued on XCD k, so that XCD reads mid_k's x~ lines
+// from its own L2; head + tail items are dealt to level the queues.  Each item
+// stores its LDS window into its group's partial sums (acc block g; shares of a
+// large (window, group) add), and k_pr_apply adds the 9 partials: integer sums, so
+// the ranks are bitwise those of the unsliced push.  Cost: 8 more V-sized u64
+// arrays written by the push and read by the apply.
+struct slice_plan {
+  int nslice  = 1;
+  int ngroups = 1;
+  slice_table t{};
+  std::vector<int> group_of_sidx{0};
+};
+
+inline int64_t env_i64(char const* name, int64_t dflt)
+{
+  char const* e = std::getenv(name);
+  return e ? std::atoll(e) : dflt;
+}
+
+inline bool slices_wanted(int64_t n_cols)
+{
+  char const* e = std::getenv("CGX_PR_SLICE");
+  if (e) return e[0] == '1';
+  return n_cols >= (int64_t(1) << 21);
+}
+
+inline slice_plan plan_slices(std::vector<unsigned long long> const& bins, int64_t n_cols)
+{
+  slice_plan P;
+  P.t.n      = 1;
+  P.t.lo[0]  = 0;
+  P.t.lo[1]  = (uint32_t)n_cols;
+  P.t.sidx[0] = 0;
+  int64_t const nb = (int64_t)bins.size();
+  int64_t const H  = env_i64("CGX_PR_SLICE_HEAD", int64_t(1) << 18);     // head sources (1 MB of x~)
+  int64_t const F  = env_i64("CGX_PR_SLICE_SRC", int64_t(640) << 10);    // sources per mid slice (2.5 MB)
+  int64_t const h0 = H >> kSrcBinBits, fb = std::max<int64_t>(F >> kSrcBinBits, 1);
+  if (h0 + kQueues > nb) return P;  // too few sources to slice
+  unsigned long long mid = 0;
+  for (int64_t b = h0; b < nb; ++b) mid += bins[b];
+  unsigned long long const T = (mid + kQueues - 1) / kQueues;
+  std::vector<int64_t> cut{h0};
+  int64_t b = h0;
+  for (int k = 0; k < kQueues; ++k) {
+    int64_t const b0 = b;
+    unsigned long long acc = 0;
+    while (b < nb && (b == b0 || (acc < T && b - b0 < fb))) acc += bins[b++];
+    cut.push_back(b);
+  }
+  // ranges: head -> slice 0, mid_k -> slice 2 + k, tail -> slice 1
+  P.nslice  = 2 + kQueues;
+  P.ngroups = kQueues + 1;
+  P.group_of_sidx.assign(P.nslice, 0);
+  P.group_of_sidx[0] = kQueues;
+  P.group_of_sidx[1] = kQueues;
+  for (int k = 0; k < kQueues; ++k) P.group_of_sidx[2 + k] = k;
+  int n = 0;
+  P.t.lo[n]     = 0;
+  P.t.sidx[n++] = 0;
+  for (int k = 0; k < kQueues; ++k) {
+    if (cut[k + 1] == cut[k]) continue;
+    P.t.lo[n]     = (uint32_t)(cut[k] << kSrcBinBits);
+    P.t.sidx[n++] = 2 + k;
+  }
+  if (cut[kQueues] < nb) {
+    P.t.lo[n]     = (uint32_t)(cut[kQueues] << kSrcBinBits);
+    P.t.sidx[n++] = 1;
+  }
+  P.t.n     = n;
+  P.t.lo[n] = (uint32_t)n_cols;
+  return P;
+}
+
+// Items and queues of a sliced schedule: units carry virtual windows; their flush
+// key becomes group * nwin + window (so flush_window lands in the group's block of
+// acc); an item is a run of units with one flush key (split in shares of ~tg
+// entries); group k < 8 -> queue k, group 8 items dealt in runs to level the queues.
+inline void build_items_sliced(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, slice_plan const& SP)
+{
+  auto hu          = to_host(units, nunits, s);
+  int64_t const nw = pp.nwin;
+  int const S      = SP.nslice;
+  for (auto& u : hu) u.win = (int64_t)SP.group_of_sidx[u.win % S] * nw + u.win / S;
+  int64_t const ne = nunits ? hu[nunits - 1].k1 : 0;
+  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * item_share_div()));
+  std::vector<int64_t> item_u, item_e, item_g;
+  for (int64_t u0 = 0; u0 < nunits;) {
+    int64_t u1 = u0;
+    while (u1 < nunits && hu[u1].win == hu[u0].win) ++u1;
+    int64_t const size = hu[u1 - 1].k1 - hu[u0].k0;
+    int64_t const n    = std::max<int64_t>(1, (size + tg / 2) / tg);
+    int64_t k          = 0;
+    for (int64_t u = u0; u < u1; ++u) {
+      int64_t const done = hu[u].k0 - hu[u0].k0;
+      if (u == u0 || (k < n && done * n >= k * size)) {
+        item_u.push_back(u);
+        item_e.push_back(0);
+        item_g.push_back(hu[u0].win / nw);
+        ++k;
+      }
+      item_e.back() += hu[u].k1 - hu[u].k0;
+    }
+    u0 = u1;
+  }
+  int64_t const nitems = (int64_t)item_u.size();
+  item_u.push_back(nunits);
+  std::vector<int> iq(nitems, 0);
+  int64_t load[kQueues] = {};
+  for (int64_t i = 0; i < nitems; ++i)
+    if (item_g[i] < kQueues) {
+      iq[i] = (int)item_g[i];
+      load[iq[i]] += item_e[i];
+    }
+  // head + tail items in runs of kGroupItems consecutive ones, largest run first
+  std::vector<int64_t> hi;
+  for (int64_t i = 0; i < nitems; ++i)
+    if (item_g[i] == kQueues) hi.push_back(i);
+  int64_t const nruns = ((int64_t)hi.size() + kGroupItems - 1) / kGroupItems;
+  std::vector<int64_t> rsize(nruns, 0), rorder(nruns);
+  for (size_t j = 0; j < hi.size(); ++j) rsize[j / kGroupItems] += item_e[hi[j]];
+  for (int64_t r = 0; r < nruns; ++r) rorder[r] = r;
+  std::stable_sort(rorder.begin(), rorder.end(), [&](int64_t a, int64_t b) { return rsize[a] > rsize[b]; });
+  for (int64_t r : rorder) {
+    int best = 0;
+    for (int q = 1; q < kQueues; ++q)
+      if (load[q] < load[best]) best = q;
+    for (int64_t j = r * kGroupItems; j < std::min<int64_t>((int64_t)hi.size(), (r + 1) * kGroupItems); ++j)
+      iq[hi[j]] = best;
+    load[best] += rsize[r];
+  }
+  std::vector<int64_t> queue;
+  queue.reserve(nitems);
+  for (int q = 0; q < kQueues; ++q) {
+    pp.qoff[q] = (int64_t)queue.size();
+    for (int64_t i = 0; i < nitems; ++i)
+      if (iq[i] == q) queue.push_back(i);
+  }
+  pp.qoff[kQueues] = (int64_t)queue.size();
+  mark_whole_items(s, pp, units, hu, item_u, nitems);
+  upload_items(s, pp, item_u, queue, nitems);
+}
+
 // Items and queues over the units (host logic, once per graph)
 inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, bool xcd_queues_wanted,
                         std::vector<int64_t> const& cutpos = {}, int ncut = 0)
@@ -1290,7 +1518,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
 // or one MG 2D block.
 template <typename C, typename R>
 void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
-                         int64_t n_cols, pr_push_t& pp)
+                         int64_t n_cols, pr_push_t& pp, bool allow_slices = false)
 {
   pp.built = true;
   pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
@@ -1301,9 +1529,30 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.win_bits        = wb;
   pp.nwin            = nwin;
   pp.nacc            = nwin << wb;
+  // source slices (single GPU, see plan_slices): virtual windows w * nslice + slice
+  slice_plan SP;
+  if (allow_slices && ne > 0 && (uint64_t)n_cols < (1ull << 32) && slices_wanted(n_cols)) {
+    int const nbins = (int)((n_cols + (int64_t(1) << kSrcBinBits) - 1) >> kSrcBinBits);
+    if (nbins * sizeof(unsigned int) <= 64 * 1024) {  // the histogram lives in LDS
+      dbuf<unsigned long long> bc(nbins, s);
+      fill<unsigned long long>(bc.data(), nbins, 0ull, s);
+      hipLaunchKernelGGL(k_src_hist<C>, dim3(grid_for(ne, kBlock, 2048)), dim3(kBlock), nbins * sizeof(unsigned int),
+                         s, cols, ne, nbins, bc.data());
+      CGX_LAUNCH_CHECK();
+      SP = plan_slices(to_host(bc.data(), nbins, s), n_cols);
+    }
+  }
+  int64_t const nvw = nwin * SP.nslice;  // virtual windows (== nwin unsliced)
+  // a virtual window's first entry is coded relative to its slice's first source
+  std::vector<uint32_t> vlo_h(SP.nslice, 0u);
+  for (int r = 0; r < SP.t.n; ++r) vlo_h[SP.t.sidx[r]] = SP.t.lo[r];
+  dbuf<uint32_t> vlo(SP.nslice, s);
+  to_device(vlo.data(), vlo_h.data(), (size_t)SP.nslice, s);
+  int const nsl = SP.nslice;
+  pp.ngroups        = SP.ngroups;
   pp.acc.set_stream(s);
-  pp.acc.resize(pp.nacc * sizeof(unsigned long long));
-  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
+  pp.acc.resize(pp.ngroups * pp.nacc * sizeof(unsigned long long));
+  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.ngroups * pp.nacc * sizeof(unsigned long long), s));
   pp.tile_ctr.set_stream(s);
   pp.tile_ctr.resize(kQueues * kCtrStride * sizeof(unsigned int));
   HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, kQueues * kCtrStride * sizeof(unsigned int), s));
@@ -1316,15 +1565,20 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   {
     dbuf<uint64_t> keys(ne, s);
     dbuf<uint32_t> vals(ne, s);
-    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
-                       keys.data(), vals.data());
+    if (SP.nslice > 1)
+      hipLaunchKernelGGL(k_push_keys_sliced<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne,
+                         wb, SP.t, SP.nslice, keys.data(), vals.data());
+    else
+      hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
+                         keys.data(), vals.data());
     CGX_LAUNCH_CHECK();
     radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
-                                         32 + bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)), s);
+                                         32 + bits_for((unsigned long long)std::max<int64_t>(nvw - 1, 1)), s);
   }
-  dbuf<int64_t> ws(nwin + 1, s);
-  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                     nwin, ws.data());
+  // from here on the windows are the virtual windows (a unit never mixes slices)
+  dbuf<int64_t> ws(nvw + 1, s);
+  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nvw + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
+                     nvw, ws.data());
   CGX_LAUNCH_CHECK();
   // source partition cuts (empty: window items only)
   std::vector<int64_t> cuts;
@@ -1332,28 +1586,29 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   {
     int64_t const nbins = (n_cols + (int64_t(1) << kSrcBinBits) - 1) >> kSrcBinBits;
     // (32-bit entries only: its cuts would break the packed format's whole segments)
-    if (n_cols >= (int64_t)kSrcParts << (kSrcBinBits + 2) && srcpart_enabled() && (w || !packed_enabled())) {
+    if (SP.nslice == 1 && n_cols >= (int64_t)kSrcParts << (kSrcBinBits + 2) && srcpart_enabled() &&
+        (w || !packed_enabled())) {
       dbuf<unsigned long long> bc(nbins, s);
       fill<unsigned long long>(bc.data(), nbins, 0ull, s);
-      hipLaunchKernelGGL(k_src_bin_counts, dim3(grid_for(nwin * nbins, kBlock, 16384)), dim3(kBlock), 0, s,
-                         keys_out.data(), ws.data(), nwin, nbins, bc.data());
+      hipLaunchKernelGGL(k_src_bin_counts, dim3(grid_for(nvw * nbins, kBlock, 16384)), dim3(kBlock), 0, s,
+                         keys_out.data(), ws.data(), nvw, nbins, bc.data());
       CGX_LAUNCH_CHECK();
       cuts = plan_source_cuts(to_host(bc.data(), nbins, s), n_cols, ne);
       if (!cuts.empty()) pp.src_head = cuts[0];
     }
   }
   int const ncut = (int)cuts.size();
-  dbuf<int64_t> cutd(std::max(ncut, 1), s), cutpos(std::max<int64_t>(nwin * ncut, 1), s);
+  dbuf<int64_t> cutd(std::max(ncut, 1), s), cutpos(std::max<int64_t>(nvw * ncut, 1), s);
   if (ncut) to_device(cutd.data(), cuts.data(), ncut, s);
   auto cut_positions = [&](unsigned long long const* cm, uint32_t* flag) {
     if (!ncut) return std::vector<int64_t>{};
-    hipLaunchKernelGGL(k_src_cut_positions, dim3(grid_for(nwin * ncut, kBlock, 4096)), dim3(kBlock), 0, s,
-                       keys_out.data(), ws.data(), nwin, cutd.data(), ncut, cm, cutpos.data());
+    hipLaunchKernelGGL(k_src_cut_positions, dim3(grid_for(nvw * ncut, kBlock, 4096)), dim3(kBlock), 0, s,
+                       keys_out.data(), ws.data(), nvw, cutd.data(), ncut, cm, cutpos.data());
     CGX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_mark_positions, dim3(grid_for(nwin * ncut, kBlock, 4096)), dim3(kBlock), 0, s, cutpos.data(),
-                       nwin * ncut, flag);
+    hipLaunchKernelGGL(k_mark_positions, dim3(grid_for(nvw * ncut, kBlock, 4096)), dim3(kBlock), 0, s, cutpos.data(),
+                       nvw * ncut, flag);
     CGX_LAUNCH_CHECK();
-    return to_host(cutpos.data(), (size_t)(nwin * ncut), s);
+    return to_host(cutpos.data(), (size_t)(nvw * ncut), s);
   };
   pp.packed = false;
   if (!w && packed_enabled()) {  // 16-bit entries unless the jumps would grow the entries by more than half
@@ -1362,19 +1617,19 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     dbuf<uint32_t> mj(ne + 1, s);
     dbuf<unsigned long long> ex(ne + 1, s);
     hipLaunchKernelGGL(k_jump_counts, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                       ws.data(), dmax, pmax, mj.data());
+                       ws.data(), vlo.data(), nsl, dmax, pmax, mj.data());
     CGX_LAUNCH_CHECK();
     fill<uint32_t>(mj.data() + ne, 1, 0u, s);
     exclusive_scan<uint32_t, unsigned long long>(mj.data(), ex.data(), ne + 1, s);
     int64_t const total0 = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
     unsigned long long const* cm = ex.data() + 1;  // inclusive prefix
     // windows padded to whole wave segments (k_packed_pads)
-    dbuf<unsigned long long> pad(nwin + 1, s), pb(nwin + 1, s);
-    hipLaunchKernelGGL(k_packed_pads, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nwin,
+    dbuf<unsigned long long> pad(nvw + 1, s), pb(nvw + 1, s);
+    hipLaunchKernelGGL(k_packed_pads, dim3(grid_for(nvw + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nvw,
                        total0, pad.data());
     CGX_LAUNCH_CHECK();
-    exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nwin + 1, s);
-    int64_t const total = total0 + (int64_t)to_host(pb.data() + nwin, 1, s)[0];
+    exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nvw + 1, s);
+    int64_t const total = total0 + (int64_t)to_host(pb.data() + nvw, 1, s)[0];
     if (total <= ne + ne / 2 && (uint64_t)total < (1ull << 32)) {
       uint16_t const pad_code = (uint16_t)(((1u << (16 - wb)) - 1) << wb);  // a jump of 0: no edge
       pp.packed = true;
@@ -1382,15 +1637,15 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // + a unit: the kernel prefetches whole units
       fill<uint16_t>(pp.ent16.data<uint16_t>(), (size_t)(total + kPushUnit), pad_code, s);
       hipLaunchKernelGGL(k_pack16, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                         vals_out.data(), rows, ne, ws.data(), mj.data(), cm, pb.data(), wb, pmax,
+                         vals_out.data(), rows, ne, ws.data(), vlo.data(), nsl, mj.data(), cm, pb.data(), wb, pmax,
                          pp.ent16.data<uint16_t>());
       CGX_LAUNCH_CHECK();
-      dbuf<int64_t> nws(nwin + 1, s);
-      hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
-                         cm, pb.data(), nwin, total0, nws.data());
+      dbuf<int64_t> nws(nvw + 1, s);
+      hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nvw + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
+                         cm, pb.data(), nvw, total0, nws.data());
       dbuf<uint32_t> pflag(total + 1, s), puid(total + 1, s);
       fill<uint32_t>(pflag.data(), (size_t)(total + 1), 0u, s);
-      hipLaunchKernelGGL(k_packed_unit_marks, dim3(grid_for(nwin, 64, 4096)), dim3(64), 0, s, nws.data(), nwin,
+      hipLaunchKernelGGL(k_packed_unit_marks, dim3(grid_for(nvw, 64, 4096)), dim3(64), 0, s, nws.data(), nvw,
                          pflag.data());
       CGX_LAUNCH_CHECK();
       std::vector<int64_t> const cp;  // no source partition with packed entries
@@ -1400,19 +1655,20 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
       push_unit* units = pp.units.data<push_unit>();
       hipLaunchKernelGGL(k_packed_unit_heads, dim3(grid_for(total, kBlock, 16384)), dim3(kBlock), 0, s, pflag.data(),
-                         puid.data(), total, nws.data(), nwin, units);
+                         puid.data(), total, nws.data(), nvw, units);
       CGX_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, total);
       CGX_LAUNCH_CHECK();
       pp.seg_base.set_stream(s);
       pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
       hipLaunchKernelGGL(k_seg_bases, dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0, s, units,
-                         nunits, keys_out.data(), ne, ws.data(), mj.data(), cm, pb.data(), dmax, pmax,
-                         pp.seg_base.data<uint32_t>());
+                         nunits, keys_out.data(), ne, ws.data(), vlo.data(), nsl, mj.data(), cm, pb.data(), dmax,
+                         pmax, pp.seg_base.data<uint32_t>());
       CGX_LAUNCH_CHECK();
       pp.ent.release();
       pp.ew.release();
-      build_items(s, pp, units, nunits, wb == 13, cp, ncut);
+      if (SP.nslice > 1) build_items_sliced(s, pp, units, nunits, SP);
+      else build_items(s, pp, units, nunits, wb == 13, cp, ncut);
       pp.nunits = nunits;
       HIP_CHECK(hipStreamSynchronize(s));
       return;
@@ -1448,13 +1704,43 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
                      w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
-  build_items(s, pp, units, nunits, wb == 13, cp, ncut);
+  if (SP.nslice > 1) build_items_sliced(s, pp, units, nunits, SP);
+  else build_items(s, pp, units, nunits, wb == 13, cp, ncut);
   pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
+// weights all exactly 1 (what cugraph.Graph attaches to an unweighted edge list,
+// simpleGraph.py:840-843): then outw = degree and x~ * w = x~ bit for bit, so the
+// push takes the unweighted 16-bit entries and skips the 4 B/edge weight stream
+template <typename R>
+__global__ void k_count_non_unit(R const* w, size_t n, int* bad)
+{
+  int mine = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    mine |= w[i] != R(1);
+  if (__any(mine) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
+template <typename R>
+bool unit_weights(handle_t& h, graph_t& g, adjacency_t& adj)
+{
+  if (!g.weighted) return false;
+  if (adj.unit_weights < 0) {
+    hipStream_t s = h.stream;
+    dbuf<int> bad(1, s);
+    fill<int>(bad.data(), 1, 0, s);
+    if (g.num_edges)
+      hipLaunchKernelGGL(k_count_non_unit<R>, dim3(grid_for((size_t)g.num_edges, kBlock, 4096)), dim3(kBlock), 0, s,
+                         adj.weights.data<R>(), (size_t)g.num_edges, bad.data());
+    CGX_LAUNCH_CHECK();
+    adj.unit_weights = (to_host_scalar(bad.data(), s) == 0 && !env_is("CGX_PR_UNIT_W", "0")) ? 1 : 0;  // A/B
+  }
+  return adj.unit_weights == 1;
+}
+
 template <typename V, typename E, typename R>
-void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
+void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_weights)
 {
   hipStream_t s = h.stream;
   int64_t nv    = g.num_vertices;
@@ -1469,8 +1755,8 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj)
     hipLaunchKernelGGL(k_edge_rows<E>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, adj.offsets.data<E>(),
                        nv, ne, rows.data());
   CGX_LAUNCH_CHECK();
-  build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), g.weighted ? adj.weights.data<R>() : nullptr, ne,
-                            nv, nv, adj.pr);
+  build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), use_weights ? adj.weights.data<R>() : nullptr, ne,
+                            nv, nv, adj.pr, /*allow_slices=*/true);
 }
 
 template <typename V, typename R>
@@ -1523,7 +1809,14 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.nitems   = pp.nitems;
   for (int q = 0; q <= kQueues; ++q) sa.qoff[q] = q < (int)pp.qoff.size() ? pp.qoff[q] : 0;
   sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
+  sa.ngroups  = pp.ngroups;
+  sa.nacc     = pp.nacc;
+  sa.nwin     = pp.nwin;
   HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, kQueues * kCtrStride * sizeof(unsigned int), s));
+  // measurement only: gathers confined to the first (mask + 1) sources (wrong ranks)
+  char const* xm = std::getenv("CGX_PR_ABLATE_XMASK");
+  sa.xmask       = xm ? (uint32_t)std::strtoul(xm, nullptr, 0) : ~0u;
+  sa.ablate      = (int)env_i64("CGX_PR_ABLATE", 0);
 }
 
 // the push kernel for the schedule's window bits and entry format
@@ -1657,7 +1950,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   // windowed push (our own out-weight sums keep every fixed-point sum <= 1; user
   // precomputed out-weights may not: generic pull kernel then)
   bool push = pow_v == nullptr && max_iter > 0;
-  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj);
+  bool const push_w = g.weighted && !(push && unit_weights<R>(h, g, adj));  // entry weights in the push
+  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj, push_w);
   push = push && adj.pr.ok;
   // fp32 packed push: x~ as enc_fixed words (CGX_PR_ENC=0: plain floats, A/B)
   a.enc = push && adj.pr.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
@@ -1668,7 +1962,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
 
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  auto pkernel = push_kernel<V, E, R>(adj.pr, g.weighted, a.enc != 0);
+  auto pkernel = push_kernel<V, E, R>(adj.pr, push_w, a.enc != 0);
   if (push) {
     set_queue_args(sa, adj.pr, s);
     sa.win_multi = adj.pr.win_multi.data<uint8_t>();  // single GPU: stored windows are not cleared

@@ -267,3 +267,66 @@ def test_encoded_x_bitwise_equal_float(graph, monkeypatch):
         ref = opr.pagerank(nv, s, d, None, 0.85, 1e-6, 500)
         assert (np.abs(got[:nv] - ref) / ref).max() < REL
 
+
+
+@pytest.mark.parametrize("scale", [12, 20])
+def test_unit_weights_take_unweighted_push(scale, monkeypatch):
+    """All-ones fp32 weights (cugraph.Graph's unweighted graphs, simpleGraph.py:840-843)
+    are detected and run the unweighted 16-bit push: the ranks are bitwise those of
+    the same graph without weights; the entry-weight push (CGX_PR_UNIT_W=0) agrees
+    within 1e-6 relative of the oracle."""
+    s, d, _ = rmat_graph(scale, False, True)
+    ones = np.ones(s.size, np.float32)
+    h, G = make_graph(s, d, None, transposed=True, symmetric=True)
+    v0, r0 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+    hw, Gw = make_graph(s, d, ones, transposed=True, symmetric=True)
+    v1, r1 = plc().pagerank(hw, Gw, None, None, None, None, 0.85, 1e-6, 500, False)
+    assert np.array_equal(host(v0), host(v1)) and np.array_equal(host(r0), host(r1))
+    assert hw.last_iterations() == h.last_iterations()
+    monkeypatch.setenv("CGX_PR_UNIT_W", "0")
+    hq, Gq = make_graph(s, d, ones, transposed=True, symmetric=True)
+    v2, r2 = plc().pagerank(hq, Gq, None, None, None, None, 0.85, 1e-6, 500, False)
+    assert np.array_equal(host(v0), host(v2))
+    rel = np.abs(host(r2).astype(np.float64) - host(r0)) / host(r0)
+    assert rel.max() < 2e-6
+    # a weight that is not 1 keeps the entry-weight push
+    monkeypatch.delenv("CGX_PR_UNIT_W")
+    if scale != 12:
+        return
+    w = ones.copy()
+    w[0] = 2.0  # one direction only: the graph is no longer symmetric
+    h3, G3 = make_graph(s, d, w, transposed=True, symmetric=False)
+    v3, r3 = plc().pagerank(h3, G3, None, None, None, None, 0.85, 1e-6, 500, False)
+    og_g = og.create_graph(s, d, w, store_transposed=True, renumber=True)
+    ref = opr.pagerank_from_graph(og_g, alpha=0.85, epsilon=1e-6, max_iterations=500)
+    ref_ext = np.zeros(int(og_g.number_map.max()) + 1)
+    ref_ext[og_g.number_map] = ref
+    got = by_ext(v3, r3)
+    vv = host(v3)
+    assert (np.abs(got[vv] - ref_ext[vv]) / ref_ext[vv]).max() < REL
+
+
+@pytest.mark.parametrize("scale,head,src", [(18, 16384, 16384), (20, 65536, 32768), (20, 65536, 1 << 20)])
+def test_source_slices_bitwise_equal(scale, head, src, monkeypatch):
+    """Source slices (pagerank.hip plan_slices: head / 8 mid slices queued per XCD /
+    tail, 9 groups of partial sums added by the apply) give the same fixed-point
+    sums -- so the same bits -- as the unsliced push (CGX_PR_SLICE=0).  Small head
+    and slice sizes force every slice kind (and, at the last size, no tail) at
+    test scale."""
+    s, d, _ = rmat_graph(scale, False, True)
+    monkeypatch.setenv("CGX_PR_SLICE", "0")
+    h0, G0 = make_graph(s, d, None, transposed=True, symmetric=True)
+    v0, r0 = plc().pagerank(h0, G0, None, None, None, None, 0.85, 1e-6, 500, False)
+    it0 = h0.last_iterations()
+    monkeypatch.setenv("CGX_PR_SLICE", "1")
+    monkeypatch.setenv("CGX_PR_SLICE_HEAD", str(head))
+    monkeypatch.setenv("CGX_PR_SLICE_SRC", str(src))
+    for packed in ("1", "0"):  # 16-bit and 32-bit entries
+        monkeypatch.setenv("CGX_PR_PACKED", packed)
+        h1, G1 = make_graph(s, d, None, transposed=True, symmetric=True)
+        v1, r1 = plc().pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert h1.last_iterations() == it0
+        assert np.array_equal(host(v0), host(v1)) and np.array_equal(host(r0), host(r1)), packed
+        # a second call reuses the schedule (stored and added partials are reset correctly)
+        _, r2 = plc().pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert np.array_equal(host(r0), host(r2))
