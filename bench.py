@@ -459,8 +459,10 @@ def louvain_leg(p, args):
     torch.cuda.synchronize()
     barrier(args)
     t = max_over_ranks(args, time.perf_counter() - t0)
+    sweep_bytes = max_over_ranks(args, h.last_louvain_sweep_bytes()) if args.world > 1 else 0.0
     return {"scale": scale, "vertices": V, "edges": E, "weights": "uniform [0,1) fp32, seed 43",
             "time_s": t, "modularity": q, "levels": h.last_louvain_levels(), "graph_build_s": round(build_s, 3),
+            "sweep_bytes_per_rank_max": sweep_bytes,
             "n_gpus": args.world,
             "path": "sg" if args.world == 1 else f"mg{args.world} ({'RCCL' if args.comm == 'rccl' else 'torch'})"}
 

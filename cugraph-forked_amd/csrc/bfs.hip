@@ -677,21 +677,36 @@ __global__ void k_finish_pred(V* pred, size_t n, V none, V const* nmap)
   }
 }
 
-// 4-byte ids: four predecessors per lane through one 16-byte load and store
-// (RMAT-24: 8.9M predecessors, 35 MB each way plus the number-map gathers)
+// 4-byte ids: four predecessors per lane through 16-byte loads and stores, kQ quads
+// per lane with every load (and then every number-map gather) issued before the
+// first use, so a lane makes one dependent round trip instead of kQ
 __global__ __launch_bounds__(256) void k_finish_pred4(int* pred, size_t n, int none, int const* nmap)
 {
   typedef int v4_t __attribute__((ext_vector_type(4)));
+  constexpr int kQ    = 4;
   size_t const nq     = n / 4;
   size_t const stride = (size_t)gridDim.x * blockDim.x;
   v4_t* p4            = reinterpret_cast<v4_t*>(pred);
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nq; i += stride) {
+  size_t i            = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i + (kQ - 1) * stride < nq; i += kQ * stride) {
+    v4_t p[kQ];
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) p[k] = __builtin_nontemporal_load(p4 + i + k * stride);
+    int q[kQ][4];
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+      q[k][0] = p[k].x == none ? -1 : (nmap ? nmap[p[k].x] : p[k].x);
+      q[k][1] = p[k].y == none ? -1 : (nmap ? nmap[p[k].y] : p[k].y);
+      q[k][2] = p[k].z == none ? -1 : (nmap ? nmap[p[k].z] : p[k].z);
+      q[k][3] = p[k].w == none ? -1 : (nmap ? nmap[p[k].w] : p[k].w);
+    }
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) __builtin_nontemporal_store(v4_t{q[k][0], q[k][1], q[k][2], q[k][3]}, p4 + i + k * stride);
+  }
+  for (; i < nq; i += stride) {
     v4_t p = __builtin_nontemporal_load(p4 + i);
-    int const q0 = p.x == none ? -1 : (nmap ? nmap[p.x] : p.x);
-    int const q1 = p.y == none ? -1 : (nmap ? nmap[p.y] : p.y);
-    int const q2 = p.z == none ? -1 : (nmap ? nmap[p.z] : p.z);
-    int const q3 = p.w == none ? -1 : (nmap ? nmap[p.w] : p.w);
-    p = v4_t{q0, q1, q2, q3};
+    p      = v4_t{p.x == none ? -1 : (nmap ? nmap[p.x] : p.x), p.y == none ? -1 : (nmap ? nmap[p.y] : p.y),
+                  p.z == none ? -1 : (nmap ? nmap[p.z] : p.z), p.w == none ? -1 : (nmap ? nmap[p.w] : p.w)};
     __builtin_nontemporal_store(p, p4 + i);
   }
   size_t const t = nq * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -1108,7 +1123,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
                       std::getenv("CGX_BFS_PRED_SCALAR") == nullptr;  // A/B
     if constexpr (sizeof(V) == 4) {
       if (vec4) {
-        hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 3) / 4, kBlock, 16384)), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 15) / 16, kBlock, 8192)), dim3(kBlock), 0, s,
                            reinterpret_cast<int*>(pred), (size_t)nv, (int)INF,
                            g.renumbered ? g.number_map.data<int>() : (int const*)nullptr);
         CGX_LAUNCH_CHECK();

@@ -458,9 +458,6 @@ struct push_args {
   int ngroups;     // source groups: the apply sums acc[g * nacc + v] over g (pr_push_t::ngroups)
   int64_t nacc;    // per group
   int64_t nwin;    // windows (win_multi is [ngroups][nwin])
-  uint32_t xmask;  // measurement only (CGX_PR_ABLATE_XMASK): x~ gathered at source & xmask; ~0u normally
-  int ablate;      // measurement only (CGX_PR_ABLATE): 1 = every unit re-reads its item's first unit's
-                   // entries (no entry stream), 2 = no LDS atomics (one register sum per thread)
 };
 
 template <typename T>
@@ -637,6 +634,15 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push_q_wide(push_args<V, E,
 // carry, the same dependent-load depth as the 32-bit format (no escape loads).
 // Entry bytes per edge ~2.1 instead of 4: the 4E entry stream is the push's floor.
 constexpr int kSegEntries = 512;  // entries per wave segment (8 rows of 64 lanes)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// storage index of packed position p: within its 512-entry segment, entry j * 64 + l
+// (row j, lane l) sits at l * 8 + j, so lane l reads its 8 rows as one 16-byte word
+__host__ __device__ __forceinline__ int64_t seg_store_index(int64_t p)
+{
+  int64_t const e = p & (kSegEntries - 1);
+  return (p & ~(int64_t)(kSegEntries - 1)) | ((e & 63) << 3) | (e >> 6);
+}
 constexpr int kSegsPerUnit = kPushUnit / kSegEntries;
 
 // inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts)
@@ -712,69 +718,77 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     }
     int64_t const ua = sa.items[it], ub = sa.items[it + 1];
     int64_t const win = units[ua].win;
-    int64_t k0 = units[ua].k0;
+    // A wave's 512-entry segment is stored lane-interleaved (seg_store_index): lane l
+    // holds its 8 rows' entries (row j = entry j * 64 + l) in one 16-byte word, so
+    // a segment is one dwordx4 load per lane and two more units' segments can be in
+    // flight while this one is summed (3 x 4 VGPRs; the row-major layout needed 8
+    // VGPRs per unit).  Measured: the entry stream was the push's largest stall
+    // (RMAT-24: 0.794 -> 0.464 ms/iteration with the entries served from L2).
+    auto seg_ptr = [&](int64_t u) {
+      return reinterpret_cast<u32x4_t const*>(sa.ent16 + units[u].k0 + wave * kSegEntries) + lane;
+    };
     // entries of this wave's segment: a multiple of kSegEntries (windows are padded
     // to whole segments), <= 0 for the waves past the end of a window's last unit
-    int n      = (int)(units[ua].k1 - k0) - wave * kSegEntries;
-    uint32_t base = __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]);
-    unsigned long long ablate_sum = 0;
-    uint16_t ent[kRows];
+    auto seg_n = [&](int64_t u) { return (int)(units[u].k1 - units[u].k0) - wave * kSegEntries; };
+    auto entry = [&](u32x4_t const& w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
+    // decode a segment's sources (DPP scan of the deltas + the running base) and
+    // issue its 8 gathers; jumps and padding read a valid source and are masked when summed
+    auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows]) {
+      uint32_t sc[kRows];
 #pragma unroll
-    for (int j = 0; j < kRows; ++j) ent[j] = nt_load(sa.ent16 + k0 + wave * kSegEntries + j * 64 + lane);  // padded
+      for (int j = 0; j < kRows; ++j) {
+        uint32_t const e = entry(w, j);
+        sc[j]            = (e >> WB) == kJump ? (e & kLow) : (e >> WB);
+      }
+      wave_incl_scan_rows<kRows>(sc);
+      uint32_t run = base;
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) {
+        uint32_t const src = run + sc[j];
+        run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
+        xv[j] = x[src];
+      }
+    };
+    auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows]) {
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) {
+        uint32_t const e = entry(w, j);
+        unsigned long long fix;
+        if constexpr (ENC) fix = dec_fixed(xv[j]);
+        else fix = fixed_of(xv[j]);
+        atomicAdd(&acc[e & kLow], (e >> WB) == kJump ? 0ull : fix);
+      }
+    };
+    // Software pipeline: the next unit's gathers are issued before this unit is
+    // summed into LDS, so two units' gathers are in flight per wave (the push waits
+    // on its gathers: SQ_WAIT_ANY 52 % of the wave cycles, issue 9 %), and the entries
+    // of the unit after that are prefetched.
+    int64_t const u1 = ua + 1 < ub ? ua + 1 : ua;
+    int nA           = seg_n(ua);
+    int nB           = seg_n(u1);
+    uint32_t bB      = __builtin_amdgcn_readfirstlane(sa.seg_base[u1 * kSegsPerUnit + wave]);
+    u32x4_t wA       = nt_load(seg_ptr(ua));  // padded: the stream has a unit past its end
+    u32x4_t wB       = nt_load(seg_ptr(u1));
+    xw_t xA[kRows];
+    if (nA > 0) gather(wA, __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]), xA);
     for (int64_t un = ua; un < ub; ++un) {
-      bool const active = n > 0;  // wave-uniform
-      uint32_t slot[kRows];
-      xw_t xv[kRows];
-      if (active) {
-        uint32_t sc[kRows];
-        bool live[kRows];
+      bool const actB = un + 1 < ub && nB > 0;  // wave-uniform
+      xw_t xB[kRows];
+      if (actB) gather(wB, bB, xB);
+      int64_t const u2  = un + 2 < ub ? un + 2 : un;
+      int const n2      = seg_n(u2);
+      uint32_t const b2 = sa.seg_base[u2 * kSegsPerUnit + wave];
+      u32x4_t const e2  = nt_load(seg_ptr(u2));
+      __builtin_amdgcn_sched_barrier(0);  // keep the next gathers and the prefetch ahead of the sums
+      if (nA > 0) sum(wA, xA);
+      wA = wB;
 #pragma unroll
-        for (int j = 0; j < kRows; ++j) {
-          uint32_t const e = ent[j];
-          bool const jump  = (e >> WB) == kJump;
-          live[j]          = !jump;
-          slot[j]          = e & kLow;
-          sc[j]            = jump ? (e & kLow) : (e >> WB);
-        }
-        wave_incl_scan_rows<kRows>(sc);
-        uint32_t run = base;
-#pragma unroll
-        for (int j = 0; j < kRows; ++j) {
-          uint32_t const src = run + sc[j];
-          run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-          xv[j] = x[src & sa.xmask];  // every lane loads (jumps and padding read a valid source id)
-          xv[j] = live[j] ? xv[j] : xw_t(0);
-        }
-      }
-      int64_t const nx  = (sa.ablate & 1) ? ua : (un + 1 < ub ? un + 1 : un);
-      int64_t const k0n = units[nx].k0;
-      int const nn      = (int)(units[nx].k1 - k0n) - wave * kSegEntries;
-      uint32_t const bn = sa.seg_base[nx * kSegsPerUnit + wave];
-      uint16_t ent_n[kRows];
-#pragma unroll
-      for (int j = 0; j < kRows; ++j) ent_n[j] = nt_load(sa.ent16 + k0n + wave * kSegEntries + j * 64 + lane);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the first use of a gather
-      if (active) {
-        if (sa.ablate & 2) {
-#pragma unroll
-          for (int j = 0; j < kRows; ++j) {
-            if constexpr (ENC) ablate_sum += dec_fixed(xv[j]) ^ slot[j];
-            else ablate_sum += fixed_of(xv[j]) ^ slot[j];
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < kRows; ++j) {
-            if constexpr (ENC) atomicAdd(&acc[slot[j]], dec_fixed(xv[j]));
-            else atomicAdd(&acc[slot[j]], fixed_of(xv[j]));
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kRows; ++j) ent[j] = ent_n[j];
-      n    = nn;
-      base = __builtin_amdgcn_readfirstlane(bn);
+      for (int j = 0; j < kRows; ++j) xA[j] = xB[j];
+      nA = actB ? nB : 0;
+      wB = e2;
+      nB = n2;
+      bB = __builtin_amdgcn_readfirstlane(b2);
     }
-    if (sa.ablate & 2) atomicAdd(&acc[tid], ablate_sum);  // keeps the ablated sums live
     flush_window<WB, V, E, R>(sa, acc, win);
   }
 }
@@ -997,13 +1011,13 @@ __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t co
     int64_t const pos   = k + (int64_t)cm[k] + (int64_t)pb[w];
     uint32_t const slot = rows[vals[k]] & low;
     if (m == 0) {
-      ent16[pos] = (uint16_t)((D << wb) | slot);
+      ent16[seg_store_index(pos)] = (uint16_t)((D << wb) | slot);
     } else {
       for (uint32_t j = 0; j < m; ++j) {
-        uint32_t const pay   = j + 1 < m ? pmax : D - pmax * (m - 1);
-        ent16[pos - m + j] = (uint16_t)((jump << wb) | pay);
+        uint32_t const pay                  = j + 1 < m ? pmax : D - pmax * (m - 1);
+        ent16[seg_store_index(pos - m + j)] = (uint16_t)((jump << wb) | pay);
       }
-      ent16[pos] = (uint16_t)slot;  // delta 0
+      ent16[seg_store_index(pos)] = (uint16_t)slot;  // delta 0
     }
   }
 }
@@ -1309,6 +1323,7 @@ inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit* units, 
 struct slice_plan {
   int nslice  = 1;
   int ngroups = 1;
+  int nmid    = 0;  // mid slices (groups 0 .. nmid - 1); group nmid = head + tail
   slice_table t{};
   std::vector<int> group_of_sidx{0};
 };
@@ -1319,11 +1334,14 @@ inline int64_t env_i64(char const* name, int64_t dflt)
   return e ? std::atoll(e) : dflt;
 }
 
-inline bool slices_wanted(int64_t n_cols)
+// Off by default: measured RMAT-24 0.974 vs 0.794 ms/iteration, RMAT-22 0.260 vs
+// 0.176 (the x~ misses it removes cost ~0.18 ms of RMAT-24's iteration, less than
+// the 8 extra partial-sum arrays, the per-item flushes and the 9-way apply).
+// CGX_PR_SLICE=1 turns it on (A/B, tests).
+inline bool slices_wanted(int64_t)
 {
   char const* e = std::getenv("CGX_PR_SLICE");
-  if (e) return e[0] == '1';
-  return n_cols >= (int64_t(1) << 21);
+  return e && e[0] == '1';
 }
 
 inline slice_plan plan_slices(std::vector<unsigned long long> const& bins, int64_t n_cols)
@@ -1336,36 +1354,41 @@ inline slice_plan plan_slices(std::vector<unsigned long long> const& bins, int64
   int64_t const nb = (int64_t)bins.size();
   int64_t const H  = env_i64("CGX_PR_SLICE_HEAD", int64_t(1) << 18);     // head sources (1 MB of x~)
   int64_t const F  = env_i64("CGX_PR_SLICE_SRC", int64_t(640) << 10);    // sources per mid slice (2.5 MB)
+  // mid slices: 8 (one per XCD), or 4 / 2 (each read by 2 / 4 XCDs: fewer partial
+  // sums for the apply to add, less of the source range sliced); CGX_PR_SLICE_MID
+  int64_t const nm = env_i64("CGX_PR_SLICE_MID", kQueues);
+  int const nmid   = (nm == 2 || nm == 4) ? (int)nm : kQueues;
   int64_t const h0 = H >> kSrcBinBits, fb = std::max<int64_t>(F >> kSrcBinBits, 1);
-  if (h0 + kQueues > nb) return P;  // too few sources to slice
+  if (h0 + nmid > nb) return P;  // too few sources to slice
   unsigned long long mid = 0;
   for (int64_t b = h0; b < nb; ++b) mid += bins[b];
-  unsigned long long const T = (mid + kQueues - 1) / kQueues;
+  unsigned long long const T = (mid + nmid - 1) / nmid;
   std::vector<int64_t> cut{h0};
   int64_t b = h0;
-  for (int k = 0; k < kQueues; ++k) {
+  for (int k = 0; k < nmid; ++k) {
     int64_t const b0 = b;
     unsigned long long acc = 0;
     while (b < nb && (b == b0 || (acc < T && b - b0 < fb))) acc += bins[b++];
     cut.push_back(b);
   }
   // ranges: head -> slice 0, mid_k -> slice 2 + k, tail -> slice 1
-  P.nslice  = 2 + kQueues;
-  P.ngroups = kQueues + 1;
+  P.nmid    = nmid;
+  P.nslice  = 2 + nmid;
+  P.ngroups = nmid + 1;
   P.group_of_sidx.assign(P.nslice, 0);
-  P.group_of_sidx[0] = kQueues;
-  P.group_of_sidx[1] = kQueues;
-  for (int k = 0; k < kQueues; ++k) P.group_of_sidx[2 + k] = k;
+  P.group_of_sidx[0] = nmid;
+  P.group_of_sidx[1] = nmid;
+  for (int k = 0; k < nmid; ++k) P.group_of_sidx[2 + k] = k;
   int n = 0;
   P.t.lo[n]     = 0;
   P.t.sidx[n++] = 0;
-  for (int k = 0; k < kQueues; ++k) {
+  for (int k = 0; k < nmid; ++k) {
     if (cut[k + 1] == cut[k]) continue;
     P.t.lo[n]     = (uint32_t)(cut[k] << kSrcBinBits);
     P.t.sidx[n++] = 2 + k;
   }
-  if (cut[kQueues] < nb) {
-    P.t.lo[n]     = (uint32_t)(cut[kQueues] << kSrcBinBits);
+  if (cut[nmid] < nb) {
+    P.t.lo[n]     = (uint32_t)(cut[nmid] << kSrcBinBits);
     P.t.sidx[n++] = 1;
   }
   P.t.n     = n;
@@ -1408,15 +1431,17 @@ inline void build_items_sliced(hipStream_t s, pr_push_t& pp, push_unit* units, i
   item_u.push_back(nunits);
   std::vector<int> iq(nitems, 0);
   int64_t load[kQueues] = {};
+  int const per = kQueues / std::max(SP.nmid, 1);  // XCDs per mid slice
   for (int64_t i = 0; i < nitems; ++i)
-    if (item_g[i] < kQueues) {
-      iq[i] = (int)item_g[i];
+    if (item_g[i] < SP.nmid) {  // mid slice k: XCDs k * per .. k * per + per - 1, windows dealt round robin
+      int64_t const win = hu[item_u[i]].win % nw;
+      iq[i]             = (int)(item_g[i] * per + win % per);
       load[iq[i]] += item_e[i];
     }
   // head + tail items in runs of kGroupItems consecutive ones, largest run first
   std::vector<int64_t> hi;
   for (int64_t i = 0; i < nitems; ++i)
-    if (item_g[i] == kQueues) hi.push_back(i);
+    if (item_g[i] == SP.nmid) hi.push_back(i);
   int64_t const nruns = ((int64_t)hi.size() + kGroupItems - 1) / kGroupItems;
   std::vector<int64_t> rsize(nruns, 0), rorder(nruns);
   for (size_t j = 0; j < hi.size(); ++j) rsize[j / kGroupItems] += item_e[hi[j]];
@@ -1813,10 +1838,7 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.nacc     = pp.nacc;
   sa.nwin     = pp.nwin;
   HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, kQueues * kCtrStride * sizeof(unsigned int), s));
-  // measurement only: gathers confined to the first (mask + 1) sources (wrong ranks)
-  char const* xm = std::getenv("CGX_PR_ABLATE_XMASK");
-  sa.xmask       = xm ? (uint32_t)std::strtoul(xm, nullptr, 0) : ~0u;
-  sa.ablate      = (int)env_i64("CGX_PR_ABLATE", 0);
+
 }
 
 // the push kernel for the schedule's window bits and entry format

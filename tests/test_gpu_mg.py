@@ -47,6 +47,8 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -154,6 +156,8 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -179,10 +183,15 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     G = plc.MGGraph(h, plc.GraphProperties(is_symmetric=True, is_multigraph=False), st, dt, wt,
                     store_transposed=False, num_edges=E)
     v, c, q, levels = plc.louvain_dendrogram(h, G, 100, 1.0)
-    mine = (v.cpu().numpy(), c.cpu().numpy(), q, [x.cpu().numpy() for x in levels])
+    # owner-sharded state: per-sweep exchange volume (sends to other ranks only)
+    sb = h.last_louvain_sweep_bytes()
+    mine = (v.cpu().numpy(), c.cpu().numpy(), q, [x.cpu().numpy() for x in levels], sb)
     allr = [None] * world
     dist.all_gather_object(allr, mine)
-    if rank == 0:
+    if rank == 0:  # (every check after the gather: a rank that failed alone would hang the others)
+        for a in allr:
+            assert (a[4] > 0) if world > 1 else (a[4] == 0), a[4]
+            assert a[4] < 64 * E / world + 4096, a[4]  # O(moved + referenced) per sweep, not O(V)
         assert all(a[2] == q for a in allr)  # every rank returns the same modularity
         nmap = np.concatenate([a[0] for a in allr]).astype(np.int64)  # global id -> external id
         assert np.array_equal(np.sort(nmap), np.unique(np.concatenate([s, d])))
@@ -253,6 +262,8 @@ def _pr_options_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -325,6 +336,8 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -419,6 +432,8 @@ def _dask_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)
     import pandas as pd
     import torch
     import torch.distributed as dist
