@@ -789,7 +789,15 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     qb[c].resize(nv, s);
   }
   // ctr2: queue lengths of a bitmap -> queues conversion; ctr3: a speculative level's counters
-  dbuf<bfs_ctr> ctr(1, s), ctr2(1, s), ctr3(1, s);
+  // one allocation and one memset for the three counter blocks; k_publish_seq
+  // zeroes ctr and ctr3 after every read, so they stay clean without more memsets
+  dbuf<bfs_ctr> ctrs(3, s);
+  HIP_CHECK(hipMemsetAsync(ctrs.data(), 0, 3 * sizeof(bfs_ctr), s));
+  struct ctr_ref {
+    bfs_ctr* p;
+    bfs_ctr* data() const { return p; }
+  };
+  ctr_ref const ctr{ctrs.data()}, ctr2{ctrs.data() + 1}, ctr3{ctrs.data() + 2};
   bfs_ctr_hdr* hctr = h.pinned_as<bfs_ctr_hdr>();
 
   bfs_args<V, E> a{};
@@ -850,7 +858,6 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // round trip fewer); invalid ids were skipped by k_bfs_sources
     if (!poll)
       CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: sources have invalid vertex IDs.");
-    zero_ctr();
     for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
     // Level 0 is certainly top-down when even every source at the maximum degree
     // stays below the switch rule: then the source counts are not read here -- level
@@ -873,8 +880,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     unsigned long long ncur[3];
     unsigned long long n_f, m_f, m_u;
     bool pending_src = false;  // level 0's read also returns the source check and the sources' edge count
-    if (quick_start) {
-      HIP_CHECK(hipMemsetAsync(ctr2.data(), 0, sizeof(bfs_ctr), s));
+    if (quick_start) {  // (ctr2 is still zero from the allocation memset)
       bfs_args<V, E> ac = a;
       ac.ctr            = ctr2.data();
       hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, ac,
@@ -1026,7 +1032,6 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
                              0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data());
           CGX_LAUNCH_CHECK();
-          HIP_CHECK(hipMemsetAsync(ctr3.data(), 0, sizeof(bfs_ctr), s));
           bfs_args<V, E> b = a;
           b.depth          = (V)(depth + 1);
           b.ctr            = ctr3.data();

@@ -682,7 +682,30 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
 // 16-byte load, sources as a running sum plus one wave scan, 6 DPP adds per 8
 // entries instead of 48 -- were 20 % slower: each gather then spans the whole
 // 512-entry segment, and the gathers' cost follows the distinct lines each touches.)
-template <int WB, typename V, typename E, typename R, bool ENC>
+// inclusive max-scan over the 64 lanes of a wave, N rows interleaved (as wave_incl_scan_rows)
+template <int N>
+__device__ __forceinline__ void wave_max_scan_rows(uint32_t (&v)[N])
+{
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x111, 0xf, 0xf, false));
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x112, 0xf, 0xf, false));
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x114, 0xf, 0xf, false));
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x118, 0xf, 0xf, false));
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x142, 0xa, 0xf, false));
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x143, 0xc, 0xf, false));
+}
+
+// DD (source dedup): only the lanes that start a run of equal sources in their row
+// gather x~ (exec-masked: ~1/4 of the lanes on RMAT); the others take their run
+// head's value with one ds_bpermute when the row is summed.  The texture path is
+// the push's busiest unit (RMAT-24: TA 71 %, TD 80 % busy, mostly stalled on L2),
+// and its work follows the active lanes.
+template <int WB, typename V, typename E, typename R, bool ENC, bool DD>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -733,12 +756,23 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     auto entry = [&](u32x4_t const& w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
     // decode a segment's sources (DPP scan of the deltas + the running base) and
     // issue its 8 gathers; jumps and padding read a valid source and are masked when summed
-    auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows]) {
+    // (DD) the run head of every lane, 6 bits per row, rows 0-3 / 4-7 in hp[0] / hp[1]
+    auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows], uint32_t (&hp)[2]) {
       uint32_t sc[kRows];
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const e = entry(w, j);
         sc[j]            = (e >> WB) == kJump ? (e & kLow) : (e >> WB);
+      }
+      if constexpr (DD) {  // four rows at a time (registers)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          uint32_t hl[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hl[j] = (sc[4 * g + j] != 0u || lane == 0) ? (uint32_t)lane : 0u;
+          wave_max_scan_rows<4>(hl);
+          hp[g] = hl[0] | (hl[1] << 6) | (hl[2] << 12) | (hl[3] << 18);
+        }
       }
       wave_incl_scan_rows<kRows>(sc);
       uint32_t run = base;
@@ -746,16 +780,25 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       for (int j = 0; j < kRows; ++j) {
         uint32_t const src = run + sc[j];
         run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-        xv[j] = x[src];
+        if constexpr (DD) {
+          if (((hp[j >> 2] >> ((j & 3) * 6)) & 63u) == (uint32_t)lane) xv[j] = x[src];  // run heads only
+        } else {
+          xv[j] = x[src];
+        }
       }
     };
-    auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows]) {
+    auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows], uint32_t const (&hp)[2]) {
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const e = entry(w, j);
+        xw_t v           = xv[j];
+        if constexpr (DD) {
+          uint32_t const h = (hp[j >> 2] >> ((j & 3) * 6)) & 63u;
+          v = __builtin_bit_cast(xw_t, __builtin_amdgcn_ds_bpermute((int)(h << 2), __builtin_bit_cast(int, v)));
+        }
         unsigned long long fix;
-        if constexpr (ENC) fix = dec_fixed(xv[j]);
-        else fix = fixed_of(xv[j]);
+        if constexpr (ENC) fix = dec_fixed(v);
+        else fix = fixed_of(v);
         atomicAdd(&acc[e & kLow], (e >> WB) == kJump ? 0ull : fix);
       }
     };
@@ -764,39 +807,61 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     // on its gathers: SQ_WAIT_ANY 52 % of the wave cycles, issue 9 %), and the entries
     // of the unit after that are prefetched.
     int64_t const u1 = ua + 1 < ub ? ua + 1 : ua;
-    int nA           = seg_n(ua);
-    int nB           = seg_n(u1);
-    uint32_t bB      = __builtin_amdgcn_readfirstlane(sa.seg_base[u1 * kSegsPerUnit + wave]);
-    u32x4_t wA       = nt_load(seg_ptr(ua));  // padded: the stream has a unit past its end
-    u32x4_t wB       = nt_load(seg_ptr(u1));
-    xw_t xA[kRows];
-    if (nA > 0) gather(wA, __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]), xA);
-    for (int64_t un = ua; un < ub; ++un) {
-      bool const actB = un + 1 < ub && nB > 0;  // wave-uniform
-      xw_t xB[kRows];
-      if (actB) gather(wB, bB, xB);
-      int64_t const u2  = un + 2 < ub ? un + 2 : un;
-      int const n2      = seg_n(u2);
-      uint32_t const b2 = sa.seg_base[u2 * kSegsPerUnit + wave];
-      u32x4_t const e2  = nt_load(seg_ptr(u2));
-      __builtin_amdgcn_sched_barrier(0);  // keep the next gathers and the prefetch ahead of the sums
-      if (nA > 0) sum(wA, xA);
-      wA = wB;
+    if constexpr (!DD) {
+      int nA      = seg_n(ua);
+      int nB      = seg_n(u1);
+      uint32_t bB = __builtin_amdgcn_readfirstlane(sa.seg_base[u1 * kSegsPerUnit + wave]);
+      u32x4_t wA  = nt_load(seg_ptr(ua));  // padded: the stream has a unit past its end
+      u32x4_t wB  = nt_load(seg_ptr(u1));
+      xw_t xA[kRows];
+      uint32_t hA[2] = {0u, 0u};
+      if (nA > 0) gather(wA, __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]), xA, hA);
+      for (int64_t un = ua; un < ub; ++un) {
+        bool const actB = un + 1 < ub && nB > 0;  // wave-uniform
+        xw_t xB[kRows];
+        uint32_t hB[2] = {0u, 0u};
+        if (actB) gather(wB, bB, xB, hB);
+        int64_t const u2  = un + 2 < ub ? un + 2 : un;
+        int const n2      = seg_n(u2);
+        uint32_t const b2 = sa.seg_base[u2 * kSegsPerUnit + wave];
+        u32x4_t const e2  = nt_load(seg_ptr(u2));
+        __builtin_amdgcn_sched_barrier(0);  // keep the next gathers and the prefetch ahead of the sums
+        if (nA > 0) sum(wA, xA, hA);
+        wA = wB;
 #pragma unroll
-      for (int j = 0; j < kRows; ++j) xA[j] = xB[j];
-      nA = actB ? nB : 0;
-      wB = e2;
-      nB = n2;
-      bB = __builtin_amdgcn_readfirstlane(b2);
+        for (int j = 0; j < kRows; ++j) xA[j] = xB[j];
+        nA = actB ? nB : 0;
+        wB = e2;
+        nB = n2;
+        bB = __builtin_amdgcn_readfirstlane(b2);
+      }
+    } else {  // (DD needs those registers: one unit at a time, entries one unit ahead)
+      int n         = seg_n(ua);
+      uint32_t base = __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]);
+      u32x4_t w0    = nt_load(seg_ptr(ua));
+      for (int64_t un = ua; un < ub; ++un) {
+        xw_t xv[kRows];
+        uint32_t hp[2] = {0u, 0u};
+        if (n > 0) gather(w0, base, xv, hp);
+        int64_t const u1n = un + 1 < ub ? un + 1 : un;
+        int const n1      = seg_n(u1n);
+        uint32_t const b1 = sa.seg_base[u1n * kSegsPerUnit + wave];
+        u32x4_t const e1  = nt_load(seg_ptr(u1n));
+        __builtin_amdgcn_sched_barrier(0);
+        if (n > 0) sum(w0, xv, hp);
+        w0   = e1;
+        n    = n1;
+        base = __builtin_amdgcn_readfirstlane(b1);
+      }
     }
     flush_window<WB, V, E, R>(sa, acc, win);
   }
 }
 
-template <int WB, typename V, typename E, typename R, bool ENC>
+template <int WB, typename V, typename E, typename R, bool ENC, bool DD = false>
 __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
 {
-  push_body16<WB, V, E, R, ENC>(sa);
+  push_body16<WB, V, E, R, ENC, DD && sizeof(typename std::conditional<ENC, uint32_t, R>::type) == 4>(sa);
 }
 
 template <typename V, typename E, typename R>
@@ -1841,11 +1906,22 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 
 }
 
+// source dedup in the packed push (push_body16 DD); CGX_PR_DEDUP=0/1 (A/B)
+inline bool dedup_enabled()
+{
+  char const* e = std::getenv("CGX_PR_DEDUP");
+  return e && e[0] == '1';
+}
+
 // the push kernel for the schedule's window bits and entry format
 template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
   if (pp.packed) {
+    if (dedup_enabled()) {
+      if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true, true> : k_pr_push16<12, V, E, R, true, true>;
+      return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false, true> : k_pr_push16<12, V, E, R, false, true>;
+    }
     if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true> : k_pr_push16<12, V, E, R, true>;
     return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false> : k_pr_push16<12, V, E, R, false>;
   }

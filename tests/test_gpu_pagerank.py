@@ -330,3 +330,22 @@ def test_source_slices_bitwise_equal(scale, head, src, monkeypatch):
         # a second call reuses the schedule (stored and added partials are reset correctly)
         _, r2 = plc().pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
         assert np.array_equal(host(r0), host(r2))
+
+
+@pytest.mark.parametrize("graph", ["rmat20", "star"])
+def test_source_dedup_bitwise_equal(graph, monkeypatch):
+    """The dedup push (pagerank.hip push_body16 DD: only run heads gather x~, the
+    rest of a run takes the head's value by ds_bpermute) gives the same bits as the
+    plain packed push.  The star graph makes long runs that cross rows and units."""
+    if graph == "star":
+        s, d = _star_plus_ring(300_000)
+    else:
+        s, d, _ = rmat_graph(20, False, True)
+    out = []
+    for dd in ("0", "1"):
+        monkeypatch.setenv("CGX_PR_DEDUP", dd)
+        h, G = make_graph(s, d, None, transposed=True, symmetric=graph != "star")
+        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        out.append((host(v), host(r), h.last_iterations()))
+    assert out[0][2] == out[1][2]
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
