@@ -146,11 +146,25 @@ class _TorchComm:
         if self.memory != "host":
             self.torch.cuda.synchronize()
 
+    # Staging goes through pinned host tensors and explicit stream syncs, never a
+    # pageable hipMemcpy: with several ranks on one GPU the pageable path's shared
+    # staging buffer is where a rehearsal rank once stalled (tests/test_gpu_mg.py).
     def _in(self, t):
-        return t.cpu() if (self.stage and t.device.type != "cpu") else t.clone()
+        if not (self.stage and t.device.type != "cpu"):
+            return t.clone()
+        h = self.torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        if t.numel():
+            h.copy_(t, non_blocking=True)
+            self.torch.cuda.current_stream().synchronize()
+        return h
 
     def _out(self, dst, t):
-        dst.copy_(t)
+        if dst.device.type != "cpu" and t.device.type == "cpu":
+            if t.numel():
+                h = t if t.is_pinned() else self.torch.empty(t.shape, dtype=t.dtype, pin_memory=True).copy_(t)
+                dst.copy_(h, non_blocking=True)
+        else:
+            dst.copy_(t)
         self._sync()
 
     # -- collectives (return 0 on success; exceptions never cross into C)

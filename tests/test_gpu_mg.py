@@ -32,6 +32,42 @@ def _slice(rank, world, E):
     return rank * E // world, (rank + 1) * E // world
 
 
+def _rank_watchdog():
+    """In a worker: SIGUSR1 prints every thread's stack (from the signal handler, so
+    a rank blocked inside a C call still answers); _spawn sends it on a deadline."""
+    import faulthandler
+    import signal
+    import sys
+    faulthandler.register(signal.SIGUSR1, file=sys.stderr, all_threads=True)
+
+
+def _spawn(fn, args, nprocs, deadline=150.0):
+    """torch.multiprocessing.spawn with a deadline: on expiry every live rank prints
+    its stacks (SIGUSR1, see _rank_watchdog), all ranks are killed and the test
+    fails naming them -- one hung rehearsal does not take the suite down with it."""
+    import signal
+    import time
+    import torch.multiprocessing as tmp
+    ctx = tmp.start_processes(fn, args=args, nprocs=nprocs, join=False, start_method="spawn")
+    end = time.monotonic() + deadline
+    while time.monotonic() < end:
+        if ctx.join(timeout=1.0):
+            return
+    alive = [r for r, p in enumerate(ctx.processes) if p.is_alive()]
+    for r in alive:
+        try:
+            os.kill(ctx.processes[r].pid, signal.SIGUSR1)
+        except OSError:
+            pass
+    time.sleep(3.0)
+    for p in ctx.processes:
+        if p.is_alive():
+            p.kill()
+    for p in ctx.processes:
+        p.join(10)
+    pytest.fail(f"ranks {alive} of {nprocs} still running after {deadline:.0f} s (stacks above)")
+
+
 def _graph(scale, weighted, seed=5):
     from oracle import graph as og
     from oracle import rmat
@@ -47,8 +83,7 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    import faulthandler
-    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
+    _rank_watchdog()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -118,23 +153,20 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
 
 @pytest.mark.parametrize("world,C,weighted", [(2, 2, False), (4, 2, True), (2, 1, False)])
 def test_mg_pagerank_vs_oracle(world, C, weighted):
-    import torch.multiprocessing as tmp
-    tmp.spawn(_worker, args=(world, _free_port(), C, 11, weighted, "pagerank"), nprocs=world, join=True)
+    _spawn(_worker, (world, _free_port(), C, 11, weighted, "pagerank"), world)
 
 
 @pytest.mark.parametrize("world,C,algo", [(2, 2, "bfs"), (4, 2, "bfs_do"), (3, 3, "bfs_do"), (2, 1, "bfs"),
                                           (4, 1, "bfs_do")])
 def test_mg_bfs_vs_oracle(world, C, algo):
-    import torch.multiprocessing as tmp
-    tmp.spawn(_worker, args=(world, _free_port(), C, 12, False, algo), nprocs=world, join=True)
+    _spawn(_worker, (world, _free_port(), C, 12, False, algo), world)
 
 
 @pytest.mark.parametrize("algo", ["pagerank", "bfs_do"])
 def test_mg_rccl_single_rank(algo):
     """The RCCL communicators themselves (world / split row / split column), with the
     one rank a single GPU allows: every collective of the MG path runs through RCCL."""
-    import torch.multiprocessing as tmp
-    tmp.spawn(_worker, args=(1, _free_port(), 1, 11, False, algo, "rccl"), nprocs=1, join=True)
+    _spawn(_worker, (1, _free_port(), 1, 11, False, algo, "rccl"), 1)
 
 
 def _same_partition(a, b):
@@ -156,8 +188,7 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    import faulthandler
-    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
+    _rank_watchdog()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -244,13 +275,11 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
 
 @pytest.mark.parametrize("world,C,integer", [(2, 2, True), (3, 3, True), (4, 2, True), (2, 1, False)])
 def test_mg_louvain_levels_vs_oracle(world, C, integer):
-    import torch.multiprocessing as tmp
-    tmp.spawn(_louvain_worker, args=(world, _free_port(), C, 10, integer), nprocs=world, join=True)
+    _spawn(_louvain_worker, (world, _free_port(), C, 10, integer), world)
 
 
 def test_mg_louvain_rccl_single_rank():
-    import torch.multiprocessing as tmp
-    tmp.spawn(_louvain_worker, args=(1, _free_port(), 1, 11, True, "rccl"), nprocs=1, join=True)
+    _spawn(_louvain_worker, (1, _free_port(), 1, 11, True, "rccl"), 1)
 
 
 def _pr_options_worker(rank, world, port, C):
@@ -262,8 +291,7 @@ def _pr_options_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    import faulthandler
-    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
+    _rank_watchdog()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -323,8 +351,7 @@ def _pr_options_worker(rank, world, port, C):
 
 @pytest.mark.parametrize("world,C", [(2, 2), (3, 1)])
 def test_mg_personalized_pagerank_options(world, C):
-    import torch.multiprocessing as tmp
-    tmp.spawn(_pr_options_worker, args=(world, _free_port(), C), nprocs=world, join=True)
+    _spawn(_pr_options_worker, (world, _free_port(), C), world)
 
 
 def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
@@ -336,8 +363,7 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    import faulthandler
-    faulthandler.dump_traceback_later(150, exit=True)  # a hung rank names where it is and ends
+    _rank_watchdog()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -384,22 +410,20 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
 @pytest.mark.parametrize("world,C,symmetric,cutoff", [(2, 2, True, np.inf), (3, 3, False, np.inf),
                                                        (4, 2, True, 0.05)])
 def test_mg_sssp_vs_oracle(world, C, symmetric, cutoff):
-    import torch.multiprocessing as tmp
-    tmp.spawn(_sssp_worker, args=(world, _free_port(), C, 11, symmetric, float(cutoff)), nprocs=world, join=True)
+    _spawn(_sssp_worker, (world, _free_port(), C, 11, symmetric, float(cutoff)), world)
 
 
 @pytest.mark.parametrize("algo", ["pagerank", "bfs_do", "louvain", "sssp"])
 def test_mg_rank_without_edges(algo, monkeypatch):
     """Rank 0 contributes no edges to cugraph_mg_graph_create (it still owns vertices)."""
-    import torch.multiprocessing as tmp
     monkeypatch.setenv("CGX_TEST_SKEW", "1")
     port = _free_port()
     if algo == "louvain":
-        tmp.spawn(_louvain_worker, args=(3, port, 3, 10, True), nprocs=3, join=True)
+        _spawn(_louvain_worker, (3, port, 3, 10, True), 3)
     elif algo == "sssp":
-        tmp.spawn(_sssp_worker, args=(3, port, 3, 10, True, float("inf")), nprocs=3, join=True)
+        _spawn(_sssp_worker, (3, port, 3, 10, True, float("inf")), 3)
     else:
-        tmp.spawn(_worker, args=(3, port, 3, 10, False, algo), nprocs=3, join=True)
+        _spawn(_worker, (3, port, 3, 10, False, algo), 3)
 
 
 # The reference's 8-GPU grid (mg_utilities.cpp:59-62: row communicator size = the
@@ -413,12 +437,11 @@ def test_mg_rank_without_edges(algo, monkeypatch):
 def test_mg_world8_reference_grid(algo, C):
     """(Louvain is partitioned 1D by source owner whatever the grid: only the
     reference's 4 x 2 build is rehearsed for it.)"""
-    import torch.multiprocessing as tmp
     port = _free_port()
     if algo == "louvain":
-        tmp.spawn(_louvain_worker, args=(8, port, C, 10, True), nprocs=8, join=True)
+        _spawn(_louvain_worker, (8, port, C, 10, True), 8)
     else:
-        tmp.spawn(_worker, args=(8, port, C, 11, False, algo), nprocs=8, join=True)
+        _spawn(_worker, (8, port, C, 11, False, algo), 8)
 
 
 def _dask_worker(rank, world, port, C):
@@ -432,8 +455,7 @@ def _dask_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    import faulthandler
-    faulthandler.dump_traceback_later(150, exit=True)
+    _rank_watchdog()
     import pandas as pd
     import torch
     import torch.distributed as dist
@@ -475,5 +497,4 @@ def _dask_worker(rank, world, port, C):
 
 @pytest.mark.parametrize("world,C", [(2, 1), (4, 2)])
 def test_dask_api_vs_single_gpu(world, C):
-    import torch.multiprocessing as tmp
-    tmp.spawn(_dask_worker, args=(world, _free_port(), C), nprocs=world, join=True)
+    _spawn(_dask_worker, (world, _free_port(), C), world)
