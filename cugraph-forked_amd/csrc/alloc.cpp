@@ -54,9 +54,21 @@ size_t trim_locked(cache_t& c)
   return freed;
 }
 
-}  // namespace
+// CGX_POISON=1 (debugging only): every allocation is filled with 0xff bytes on its
+// stream, so a read of memory nobody wrote gives the same garbage on every run
+bool poison_enabled()
+{
+  static bool const on = std::getenv("CGX_POISON") != nullptr;
+  return on;
+}
 
-void* device_alloc(size_t bytes, hipStream_t s)
+void* poisoned(void* p, size_t bytes, hipStream_t s)
+{
+  if (p && poison_enabled()) (void)hipMemsetAsync(p, 0xff, bytes, s);
+  return p;
+}
+
+void* device_alloc_raw(size_t bytes, hipStream_t s)
 {
   cache_t& c       = cache();
   size_t const cls = size_class(bytes);
@@ -85,6 +97,10 @@ void* device_alloc(size_t bytes, hipStream_t s)
   c.live[p] = cls;
   return p;
 }
+
+}  // namespace
+
+void* device_alloc(size_t bytes, hipStream_t s) { return poisoned(device_alloc_raw(bytes, s), size_class(bytes), s); }
 
 void device_free(void* p, hipStream_t s)
 {

@@ -2352,6 +2352,14 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
   S.m = to_host_scalar(S.scal.data(), s);
 
   bool const trace = std::getenv("CGX_LOUVAIN_TRACE") != nullptr;  // measurement only
+  // CGX_LOUVAIN_TRACE=2 (debugging only): every rank syncs and names each phase as it
+  // ends, so a rank that stops shows where
+  bool const phases = trace && std::atoi(std::getenv("CGX_LOUVAIN_TRACE")) >= 2;
+  auto phase        = [&](char const* what, size_t i) {
+    if (!phases) return;
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::fprintf(stderr, "[louvain-mg r%d] %s %zu\n", p, what, i);
+  };
   std::vector<int64_t> voff = mg.voff;
   std::vector<dbuf<uint32_t>> dendrogram;  // per level: the owned ids' clusters (coarse ids after contraction)
   std::vector<std::vector<int64_t>> level_voff;
@@ -2378,6 +2386,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     if (nr) vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
     S.bytes = 0;
     mg_setup_level(S, cur, L, has_edges.data(), k.data());
+    phase("setup", dendrogram.size());
     size_t const setup_bytes = S.bytes;
     dendrogram.emplace_back(r1, s);
     uint32_t* level = dendrogram.back().data();
@@ -2387,6 +2396,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
       HIP_CHECK(hipMemcpyAsync(level_gh.data(), L.c_gh.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     sweep_plan plan;
     plan_sweeps(S, cur, off.data(), k.data(), plan);
+    phase("plan", dendrogram.size());
     dbuf<double> own(r1, s);
     dbuf<uint32_t> next(r1, s);
     mg_sweep_view W;
@@ -2394,8 +2404,10 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     bool up_down     = true;  // as the single-GPU loop: sweep k + 1 before the decision on clustering k
     S.bytes          = 0;
     mg_view(S, L, all_present, W);
+    phase("view", sweeps);
     sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), up_down,
           own.data());
+    phase("sweep", sweeps);
     double new_q = mg_modularity(S, L, own.data(), all_present);
     ++sweeps;
     sweep_bytes += S.bytes;
@@ -2407,11 +2419,14 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
       cur_q = new_q;
       S.bytes = 0;
       mg_advance(S, L, W, next.data(), has_edges.data());
+      phase("advance", sweeps);
       all_present = false;
       up_down     = !up_down;
       mg_view(S, L, all_present, W);
+      phase("view", sweeps);
       sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), up_down,
             own.data());
+      phase("sweep", sweeps);
       new_q = mg_modularity(S, L, own.data(), all_present);
       ++sweeps;
       sweep_bytes += S.bytes;
@@ -2428,6 +2443,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     if (cur_q <= best_q) break;
     best_q = cur_q;
     cur    = mg_contract(S, cur, L, level, level_gh.data(), voff);
+    phase("contract", dendrogram.size());
   }
   // flatten_dendrogram for the owned level-0 vertices: level i's owners answer
   // for the ids the chain has reached

@@ -1,5 +1,7 @@
 """PageRank parity: HIP path (through the C ABI) vs the oracle and the reference's
 golden vectors.  Tolerance: 1e-6 relative vs the fp64 oracle (north_star)."""
+import functools
+
 import numpy as np
 import pytest
 
@@ -69,7 +71,10 @@ def test_invalid_alpha():
         plc().pagerank(h, G, None, None, None, None, 1.5, 1e-6, 100, False)
 
 
+@functools.lru_cache(maxsize=None)
 def rmat_graph(scale, weighted, symmetric=True, seed=42):
+    """Generated once per module (the RMAT-20 edge lists are shared by several
+    tests); callers must not modify the arrays."""
     s, d = rmat.rmat(scale, 16 << scale, seed=seed)
     w = rmat.rmat_weights(s.size, seed=seed + 1).astype(np.float64) if weighted else None
     if symmetric:
