@@ -398,15 +398,19 @@ constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 // Window bits: 13 (8K destinations, 64 KB of LDS) from 2^22 destinations up,
 // where the x~ lines a window re-reads dominate (RMAT-24: 0.065 instead of 0.091
 // distinct lines per entry); 12 below (RMAT-22 measured 0.204 vs 0.217
-// ms/iteration for 4K vs 8K).  CGX_PR_WIN_BITS overrides (12 or 13).
+// ms/iteration for 4K vs 8K).  CGX_PR_WIN_BITS overrides (12, 13, or 14: 16K
+// destinations, 128 KB of LDS, one block per CU -- push_blocks).
 inline int push_win_bits(int64_t n_rows)
 {
   if (char const* e = std::getenv("CGX_PR_WIN_BITS")) {
     int b = std::atoi(e);
-    if (b == 12 || b == 13) return b;
+    if (b == 12 || b == 13 || b == 14) return b;
   }
   return n_rows >= (int64_t(1) << 22) ? 13 : 12;
 }
+
+// persistent push blocks: two per CU, one per CU for 16K-destination windows
+inline int push_blocks(int win_bits) { return win_bits >= 14 ? kPushBlocks / 2 : kPushBlocks; }
 
 // 16-bit packed entries for unweighted graphs (push_body16); CGX_PR_PACKED=0 keeps
 // the 32-bit format (measurement / A-B only)
@@ -862,6 +866,19 @@ template <int WB, typename V, typename E, typename R, bool ENC, bool DD = false>
 __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
 {
   push_body16<WB, V, E, R, ENC, DD && sizeof(typename std::conditional<ENC, uint32_t, R>::type) == 4>(sa);
+}
+
+// 16K-destination windows: 128 KB of LDS, one block (16 waves) per CU, no 8-waves bound
+template <typename V, typename E, typename R, bool ENC>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
+{
+  push_body16<14, V, E, R, ENC, false>(sa);
+}
+
+template <typename V, typename E, typename R, bool WEIGHTED>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push_q_w14(push_args<V, E, R> sa)
+{
+  push_body<14, V, E, R, WEIGHTED>(sa);
 }
 
 template <typename V, typename E, typename R>
@@ -1549,7 +1566,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   // measured 0.199 -> 0.216, the last groups' imbalance outweighing the L2 hits).
   auto hu = to_host(units, nunits, s);
   bool const xcd_queues = xcd_queues_wanted;
-  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * item_share_div()));
+  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (push_blocks(pp.win_bits) * item_share_div()));
   std::vector<int64_t> item_u, item_e;
   for (int64_t u0 = 0; u0 < nunits;) {
     int64_t u1 = u0;
@@ -1758,7 +1775,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       pp.ent.release();
       pp.ew.release();
       if (SP.nslice > 1) build_items_sliced(s, pp, units, nunits, SP);
-      else build_items(s, pp, units, nunits, wb == 13, cp, ncut);
+      else build_items(s, pp, units, nunits, wb >= 13, cp, ncut);
       pp.nunits = nunits;
       HIP_CHECK(hipStreamSynchronize(s));
       return;
@@ -1795,7 +1812,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
   if (SP.nslice > 1) build_items_sliced(s, pp, units, nunits, SP);
-  else build_items(s, pp, units, nunits, wb == 13, cp, ncut);
+  else build_items(s, pp, units, nunits, wb >= 13, cp, ncut);
   pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -1917,6 +1934,10 @@ inline bool dedup_enabled()
 template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
+  if (pp.win_bits == 14) {
+    if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
+    return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
+  }
   if (pp.packed) {
     if (dedup_enabled()) {
       if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true, true> : k_pr_push16<12, V, E, R, true, true>;
@@ -2065,7 +2086,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     set_queue_args(sa, adj.pr, s);
     sa.win_multi = adj.pr.win_multi.data<uint8_t>();  // single GPU: stored windows are not cleared
     sa.win_bits  = adj.pr.win_bits;
-    nblk_push  = sa.nitems ? kPushBlocks : 0;
+    nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
   }
   // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
@@ -2431,7 +2452,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   // and re-zeroes them in place, no column collective
   bool const col_reduce = R_ > 1;
   sap.acc   = col_reduce ? acc_own.data() : sp.acc;
-  int const nblk_push  = sp.nitems ? kPushBlocks : 0;
+  int const nblk_push  = sp.nitems ? push_blocks(blk.pp.win_bits) : 0;
   auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);

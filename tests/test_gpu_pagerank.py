@@ -354,3 +354,21 @@ def test_source_dedup_bitwise_equal(graph, monkeypatch):
         out.append((host(v), host(r), h.last_iterations()))
     assert out[0][2] == out[1][2]
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("scale", [12, 20])
+def test_window_bits_bitwise_equal(scale, monkeypatch):
+    """4K, 8K and 16K-destination windows (CGX_PR_WIN_BITS 12 / 13 / 14; 14 runs one
+    128 KB-LDS block per CU) sum the same fixed-point terms: the same bits."""
+    s, d, _ = rmat_graph(scale, False, True)
+    out = []
+    for wb in ("12", "13", "14"):
+        monkeypatch.setenv("CGX_PR_WIN_BITS", wb)
+        for packed in ("1", "0"):
+            monkeypatch.setenv("CGX_PR_PACKED", packed)
+            h, G = make_graph(s, d, None, transposed=True, symmetric=True)
+            v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+            out.append((host(v), host(r), h.last_iterations()))
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
