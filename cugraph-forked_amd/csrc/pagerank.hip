@@ -395,18 +395,20 @@ constexpr int kMaxSliceRanges = 12;
 constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
 constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 
-// Window bits: 13 (8K destinations, 64 KB of LDS) from 2^22 destinations up,
-// where the x~ lines a window re-reads dominate (RMAT-24: 0.065 instead of 0.091
-// distinct lines per entry); 12 below (RMAT-22 measured 0.204 vs 0.217
-// ms/iteration for 4K vs 8K).  CGX_PR_WIN_BITS overrides (12, 13, or 14: 16K
-// destinations, 128 KB of LDS, one block per CU -- push_blocks).
+// Window bits: about 500-600 windows measured best -- fewer x~ line visits per
+// entry as windows grow, against the load balance of few windows.  14 (16K
+// destinations, 128 KB of LDS, one 1024-thread block per CU) from 2^23 destinations
+// up (RMAT-24, 542 windows: 0.709 ms/iteration against 0.786 with 13, same box),
+// 13 (8K, 64 KB, two blocks per CU) from 2^22, 12 below (RMAT-22, 586 windows:
+// 0.181 ms against 0.199 with 13 and 0.219 with 14).  CGX_PR_WIN_BITS overrides
+// (12, 13 or 14).
 inline int push_win_bits(int64_t n_rows)
 {
   if (char const* e = std::getenv("CGX_PR_WIN_BITS")) {
     int b = std::atoi(e);
     if (b == 12 || b == 13 || b == 14) return b;
   }
-  return n_rows >= (int64_t(1) << 22) ? 13 : 12;
+  return n_rows >= (int64_t(1) << 23) ? 14 : n_rows >= (int64_t(1) << 22) ? 13 : 12;
 }
 
 // persistent push blocks: two per CU, one per CU for 16K-destination windows

@@ -129,6 +129,7 @@ class _TorchComm:
         self.stage = memory == "host" or dist.get_backend(group) == "gloo"
         self._ops = {CGX_COMM_SUM: dist.ReduceOp.SUM, CGX_COMM_MIN: dist.ReduceOp.MIN,
                      CGX_COMM_MAX: dist.ReduceOp.MAX}
+        self._streams = {}
 
     # -- buffers
     def _view(self, ptr, count, dt):
@@ -142,72 +143,96 @@ class _TorchComm:
             return torch.empty(0, dtype=_torch_dtype(torch, dt), device="cuda")
         return torch.as_tensor(_CudaArray(ptr, count, dt), device="cuda")
 
-    def _sync(self):
-        if self.memory != "host":
-            self.torch.cuda.synchronize()
+    # The buffers belong to the library's stream (`stream`, the handle's HIP stream):
+    # staging copies run on that stream and only that stream is waited for -- no
+    # device-wide synchronize and no legacy-default-stream copies, whose implicit
+    # ordering against every other stream of the process is not needed here.  Host
+    # staging uses pinned tensors.
+    def _stream(self, ptr):
+        if self.memory == "host":
+            return None
+        st = self._streams.get(ptr)
+        if st is None:
+            st = self._streams[ptr] = self.torch.cuda.ExternalStream(int(ptr or 0))
+        return st
 
-    # Staging goes through pinned host tensors and explicit stream syncs, never a
-    # pageable hipMemcpy: with several ranks on one GPU the pageable path's shared
-    # staging buffer is where a rehearsal rank once stalled (tests/test_gpu_mg.py).
-    def _in(self, t):
+    def _sync(self, st):
+        if st is not None:
+            st.synchronize()
+
+    def _in(self, t, st):
         if not (self.stage and t.device.type != "cpu"):
-            return t.clone()
+            if st is None:
+                return t.clone()
+            with self.torch.cuda.stream(st):
+                out = t.clone()
+            self._sync(st)
+            return out
         h = self.torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
         if t.numel():
-            h.copy_(t, non_blocking=True)
-            self.torch.cuda.current_stream().synchronize()
+            with self.torch.cuda.stream(st):
+                h.copy_(t, non_blocking=True)
+            self._sync(st)
         return h
 
-    def _out(self, dst, t):
-        if dst.device.type != "cpu" and t.device.type == "cpu":
-            if t.numel():
-                h = t if t.is_pinned() else self.torch.empty(t.shape, dtype=t.dtype, pin_memory=True).copy_(t)
-                dst.copy_(h, non_blocking=True)
-        else:
+    def _out(self, dst, t, st):
+        if st is None:
             dst.copy_(t)
-        self._sync()
+            return
+        if t.device.type == "cpu" and t.numel() and not t.is_pinned():
+            t = self.torch.empty(t.shape, dtype=t.dtype, pin_memory=True).copy_(t)
+        elif t.device.type != "cpu":  # a device collective's result (nccl): its stream first
+            st.wait_stream(self.torch.cuda.current_stream())
+        with self.torch.cuda.stream(st):
+            dst.copy_(t, non_blocking=True)
+        self._sync(st)
 
-    # -- collectives (return 0 on success; exceptions never cross into C)
-    def allreduce(self, _ctx, send, recv, count, dt, op, _stream):
+    # -- collectives (return 0 on success; exceptions never cross into C).  The library
+    # calls them with its stream's work enqueued, so that stream is drained first.
+    def allreduce(self, _ctx, send, recv, count, dt, op, stream):
         try:
-            self._sync()
-            t = self._in(self._view(send, count, dt))
+            st = self._stream(stream)
+            self._sync(st)
+            t = self._in(self._view(send, count, dt), st)
             if count:
                 self.dist.all_reduce(t, op=self._ops[op], group=self.group)
-            self._out(self._view(recv, count, dt), t)
+            self._out(self._view(recv, count, dt), t, st)
             return 0
         except Exception:  # noqa: BLE001
             traceback.print_exc()
             return 1
 
-    def allgather(self, _ctx, send, recv, count, dt, _stream):
+    def allgather(self, _ctx, send, recv, count, dt, stream):
         try:
-            self._sync()
-            t = self._in(self._view(send, count, dt))
+            st = self._stream(stream)
+            self._sync(st)
+            t = self._in(self._view(send, count, dt), st)
             parts = [self.torch.empty_like(t) for _ in range(self.size)]
             self.dist.all_gather(parts, t, group=self.group)
-            self._out(self._view(recv, count * self.size, dt), self.torch.cat(parts))
+            self._out(self._view(recv, count * self.size, dt), self.torch.cat(parts), st)
             return 0
         except Exception:  # noqa: BLE001
             traceback.print_exc()
             return 1
 
-    def reduce_scatter(self, _ctx, send, recv, recvcount, dt, op, _stream):
+    def reduce_scatter(self, _ctx, send, recv, recvcount, dt, op, stream):
         try:
-            self._sync()
-            t = self._in(self._view(send, recvcount * self.size, dt))
+            st = self._stream(stream)
+            self._sync(st)
+            t = self._in(self._view(send, recvcount * self.size, dt), st)
             out = self.torch.empty(recvcount, dtype=t.dtype, device=t.device)
             if recvcount:
                 self.dist.reduce_scatter_tensor(out, t, op=self._ops[op], group=self.group)
-            self._out(self._view(recv, recvcount, dt), out)
+            self._out(self._view(recv, recvcount, dt), out, st)
             return 0
         except Exception:  # noqa: BLE001
             traceback.print_exc()
             return 1
 
-    def alltoallv(self, _ctx, send, sc, sd, recv, rc, rd, dt, _stream):
+    def alltoallv(self, _ctx, send, sc, sd, recv, rc, rd, dt, stream):
         try:
-            self._sync()
+            st = self._stream(stream)
+            self._sync(st)
             P = self.size
             scnt = [int(sc[q]) for q in range(P)]
             rcnt = [int(rc[q]) for q in range(P)]
@@ -215,10 +240,10 @@ class _TorchComm:
             rdis = [int(rd[q]) for q in range(P)]
             if sdis != _prefix(scnt) or rdis != _prefix(rcnt):
                 raise ValueError("alltoallv: only packed displacements are supported")
-            t = self._in(self._view(send, sum(scnt), dt))
+            t = self._in(self._view(send, sum(scnt), dt), st)
             out = self.torch.empty(sum(rcnt), dtype=t.dtype, device=t.device)
             self.dist.all_to_all_single(out, t, output_split_sizes=rcnt, input_split_sizes=scnt, group=self.group)
-            self._out(self._view(recv, sum(rcnt), dt), out)
+            self._out(self._view(recv, sum(rcnt), dt), out, st)
             return 0
         except Exception:  # noqa: BLE001
             traceback.print_exc()
