@@ -32,18 +32,25 @@ def _slice(rank, world, E):
     return rank * E // world, (rank + 1) * E // world
 
 
-def _rank_watchdog():
-    """In a worker: SIGUSR1 prints every thread's stack (from the signal handler, so
-    a rank blocked inside a C call still answers); _spawn sends it on a deadline."""
+def _rank_setup():
+    """In a worker, before its first HIP call:
+    * SIGUSR1 prints every thread's stack (from the signal handler, so a rank blocked
+      inside a C call still answers); _spawn sends it on a deadline;
+    * HSA_ENABLE_SDMA=0: copies run as blit kernels, not on the DMA engines.  Up to 8
+      rehearsal ranks share the one test GPU, and the world-8 Louvain rehearsal (the
+      most copy-heavy: hundreds of small staged collectives per rank) stalled in 3 of
+      5 runs with every rank waiting on its stream's copies (tests/test_gpu_mg.py
+      history).  A node runs one rank per GPU over RCCL instead."""
     import faulthandler
     import signal
     import sys
+    os.environ.setdefault("HSA_ENABLE_SDMA", "0")
     faulthandler.register(signal.SIGUSR1, file=sys.stderr, all_threads=True)
 
 
 def _spawn(fn, args, nprocs, deadline=150.0):
     """torch.multiprocessing.spawn with a deadline: on expiry every live rank prints
-    its stacks (SIGUSR1, see _rank_watchdog), all ranks are killed and the test
+    its stacks (SIGUSR1, see _rank_setup), all ranks are killed and the test
     fails naming them -- one hung rehearsal does not take the suite down with it."""
     import signal
     import time
@@ -83,7 +90,7 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_watchdog()
+    _rank_setup()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -188,7 +195,7 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_watchdog()
+    _rank_setup()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -291,7 +298,7 @@ def _pr_options_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_watchdog()
+    _rank_setup()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -363,7 +370,7 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_watchdog()
+    _rank_setup()
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -455,7 +462,7 @@ def _dask_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_watchdog()
+    _rank_setup()
     import pandas as pd
     import torch
     import torch.distributed as dist
