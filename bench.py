@@ -610,7 +610,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_pr_push16 (packed 16-bit entries; k_pr_push_q for weighted graphs) + k_pr_apply (one PageRank iteration): HIP events on the library stream around "
+            "kernel": ("k_pr_push16_w14 (16K-destination windows from 2^23 vertices, else k_pr_push16; packed 16-bit entries; k_pr_push_q* for weighted graphs) + k_pr_apply (one PageRank iteration): HIP events on the library stream around "
                        "each chunk of iterations in the timed region / iterations run (inter-kernel gaps "
                        "included)" if world == 1 else
                        "one MG PageRank iteration per rank (row allgather + push + column reduce-scatter + apply + "

@@ -31,7 +31,7 @@ with open(sys.argv[2], "w") as f:
     for r in rows:
         n = r["Kernel_Name"]
         if "k_pr_push" in n or "k_pr_apply" in n or "k_bu_probe" in n or "k_topdown" in n or "k_finish_pred" in n:
-            short = n.split("(")[0].split("<")[0].replace("void ", "").split("::")[-1]
+            short = n.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].replace("void ", "").split("::")[-1]
             f.write(f"{short},{r['Start_Timestamp']},{int(r['End_Timestamp']) - int(r['Start_Timestamp'])}\n")
 PY
 exit $rc
