@@ -135,6 +135,11 @@ struct pr_push_t {
   buffer win_multi;    // uint8[ngroups * nwin]: 1 = (group, window) summed by several items (flushes add),
                        // 0 = one item stores it
   int64_t src_head = -1;  // source partition over the XCDs: head size (-1: not partitioned)
+  // fused apply (pagerank.hip fused_finish): items per window, windows without items
+  buffer win_items;       // uint32[nwin]
+  buffer win_left;        // uint32[nwin]: win_items between iterations
+  buffer empty_wins;      // int64[nempty]
+  int64_t nempty = 0, nwin_items = 0;
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

@@ -49,8 +49,18 @@ struct pr_state {
   unsigned int ticket;
   int iter;
   int done;  // 0 running, 1 converged, 2 max_iterations reached
-  int pad;
+  unsigned int wticket;       // fused push + apply: windows applied this iteration
+  unsigned long long fdiff;   // ... and their (diff, dangling) sums, fixed point (kSumScale)
+  unsigned long long fdang;
 };
+
+// The L1 difference and the dangling mass of an iteration are summed in 64-bit fixed
+// point (scale 2^61; both are at most 2): integer adds, so the totals -- and the
+// next iteration's base, which depends on the dangling mass -- are the same bits
+// however the vertices are split over blocks (the fused push + apply, the separate
+// apply and the pull kernel all agree).
+constexpr double kSumScale    = 2305843009213693952.0;  // 2^61
+constexpr double kSumScaleInv = 1.0 / 2305843009213693952.0;
 
 template <typename V, typename E, typename R>
 struct pr_args {
@@ -69,7 +79,7 @@ struct pr_args {
   int max_iter;
   int64_t nv;         // vertices this process updates
   int64_t nv_global;  // |V| of the graph (teleport base)
-  double* partials;
+  double* partials;  // per-block (diff, dangling) partials (fixed-point words, see kSumScale)
   pr_state* st;
   double* mg_sums;  // multi-GPU: (diff, dangling) of this rank, allreduced before k_mg_finish
   int enc;          // x~ stored as fixed-point words (enc_fixed; single-GPU fp32 packed push only)
@@ -132,6 +142,23 @@ inline int next_chunk(pr_state const& st, double eps, int max_iter)
 
 namespace {
 
+__device__ __forceinline__ unsigned long long sum_fix(double x) { return (unsigned long long)__double2ll_rn(x * kSumScale); }
+
+// sum over an NT-thread block (NT a multiple of 64); result valid in thread 0; sm >= NT / 64 words
+template <int NT>
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long* sm)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long r = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < NT / 64; ++w) r += sm[w];
+  return r;
+}
+
 // next iteration's base, convergence flag and iteration count from the global
 // L1 difference d and dangling mass g (pagerank_impl.cuh:209-292)
 template <typename V, typename E, typename R>
@@ -158,36 +185,39 @@ __device__ void update_state(pr_args<V, E, R> const& a, double d, double g, bool
 // the last-arriving block reduces the per-block (diff, dangling) partials and
 // updates the iteration state (cdna_hip_programming.md §6 Guideline 16 ticket form)
 template <typename V, typename E, typename R>
-__device__ void finish_iteration(pr_args<V, E, R> const& a, double my_diff, double my_dang, bool count_iter)
+__device__ void finish_iteration(pr_args<V, E, R> const& a, unsigned long long my_diff, unsigned long long my_dang,
+                                 bool count_iter)
 {
-  __shared__ double sm[4];
+  __shared__ unsigned long long sm[8];
   __shared__ int s_last;
-  double bd = block_sum_256(my_diff, sm);
-  double bg = block_sum_256(my_dang, sm);
+  unsigned long long bd = block_sum_u64<256>(my_diff, sm);
+  unsigned long long bg = block_sum_u64<256>(my_dang, sm);
+  auto* part = reinterpret_cast<unsigned long long*>(a.partials);
   if (threadIdx.x == 0) {
     // write-through (sc1) partials: no agent release (an L2 write-back per block) needed
-    __hip_atomic_store(&a.partials[2 * blockIdx.x], bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.partials[2 * blockIdx.x + 1], bg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&part[2 * blockIdx.x], bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&part[2 * blockIdx.x + 1], bg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned t = __hip_atomic_fetch_add(&a.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last     = (t == gridDim.x - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  double d = 0, g = 0;
+  unsigned long long d = 0, g = 0;
   for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {  // sc1 loads: L1 bypassed
-    d += __hip_atomic_load(&a.partials[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g += __hip_atomic_load(&a.partials[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    d += __hip_atomic_load(&part[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g += __hip_atomic_load(&part[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  d = block_sum_256(d, sm);
-  g = block_sum_256(g, sm);
+  d = block_sum_u64<256>(d, sm);
+  g = block_sum_u64<256>(g, sm);
   if (threadIdx.x == 0) {
+    double const dd = (double)d * kSumScaleInv, gg = (double)g * kSumScaleInv;
     if (a.mg_sums) {
-      a.mg_sums[0] = d;
-      a.mg_sums[1] = g;
+      a.mg_sums[0] = dd;
+      a.mg_sums[1] = gg;
       a.st->ticket = 0;
     } else {
-      update_state<V, E, R>(a, d, g, count_iter);
+      update_state<V, E, R>(a, dd, gg, count_iter);
     }
   }
 }
@@ -203,18 +233,18 @@ __global__ void k_mg_finish(pr_args<V, E, R> a, bool count_iter)
 template <typename V, typename E, typename R>
 __global__ __launch_bounds__(256) void k_pr_init(pr_args<V, E, R> a)
 {
-  double dang = 0;
+  unsigned long long dang = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < a.nv; v += (int64_t)gridDim.x * blockDim.x) {
     R p  = a.pr[v];
     R ow = a.outw[v];
     if (ow == R(0)) {
-      dang += (double)p;
+      dang += sum_fix((double)p);
       store_x<R>(a.x_out, v, R(0), a.enc);
     } else {
       store_x<R>(a.x_out, v, (R)((double)p / (double)ow), a.enc);
     }
   }
-  finish_iteration<V, E, R>(a, 0.0, dang, false);
+  finish_iteration<V, E, R>(a, 0ull, dang, false);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -273,32 +303,32 @@ __device__ __forceinline__ double row_partial_block(pr_args<V, E, R> const& a, E
 
 template <typename V, typename E, typename R>
 __device__ __forceinline__ void vertex_update_from(pr_args<V, E, R> const& a, V v, double s, R old, R ow, double base,
-                                                   double pf, double& my_diff, double& my_dang)
+                                                   double pf, unsigned long long& my_diff, unsigned long long& my_dang)
 {
   double n = base + a.alpha * s;
   if (a.pers) n += pf * (double)a.pers[v];
   R nr     = (R)n;
   a.pr[v]  = nr;
-  my_diff += fabs((double)nr - (double)old);
+  my_diff += sum_fix(fabs((double)nr - (double)old));
   R xv = R(0);
-  if (ow == R(0)) my_dang += (double)nr;
+  if (ow == R(0)) my_dang += sum_fix((double)nr);
   else xv = (R)((double)nr / (double)ow);
   store_x<R>(a.x_out, v, xv, a.enc);
 }
 
 template <typename V, typename E, typename R>
 __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, double s, double base, double pf,
-                                              double& my_diff, double& my_dang)
+                                              unsigned long long& my_diff, unsigned long long& my_dang)
 {
   R old    = a.pr[v];
   double n = base + a.alpha * s;
   if (a.pers) n += pf * (double)a.pers[v];
   R nr     = (R)n;
   a.pr[v]  = nr;
-  my_diff += fabs((double)nr - (double)old);
+  my_diff += sum_fix(fabs((double)nr - (double)old));
   R ow = a.outw[v];
   R xv = R(0);
-  if (ow == R(0)) my_dang += (double)nr;
+  if (ow == R(0)) my_dang += sum_fix((double)nr);
   else xv = (R)((double)nr / (double)ow);
   store_x<R>(a.x_out, v, xv, a.enc);
 }
@@ -311,7 +341,7 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
   work_item const it = a.items[blockIdx.x];
   double const base  = a.st->base;
   double const pf    = a.st->pers_factor;
-  double my_diff = 0, my_dang = 0;
+  unsigned long long my_diff = 0, my_dang = 0;
   int const tid = threadIdx.x;
   if (it.width == 256) {
     for (int64_t p = it.begin; p < it.end; ++p) {
@@ -457,13 +487,21 @@ struct push_args {
   int64_t const* queue;     // item ids, queue by queue
   int64_t qoff[kQueues + 1];
   int64_t nitems;
-  unsigned int* tile_ctr;   // queue heads, kCtrStride apart (k_pr_apply resets them)
+  unsigned int* tile_ctr;   // queue heads, kCtrStride apart, two sets (iteration parity)
   uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
                             // its sums), 0 = stored whole; nullptr: clear every sum
   int win_bits;
   int ngroups;     // source groups: the apply sums acc[g * nacc + v] over g (pr_push_t::ngroups)
   int64_t nacc;    // per group
   int64_t nwin;    // windows (win_multi is [ngroups][nwin])
+  // fused apply (single GPU): the block that completes a window applies it
+  int fuse;
+  int parity;                  // queue-head set of this launch (launch index & 1)
+  uint32_t* win_left;          // items of each window still to finish this iteration
+  uint32_t const* win_items;   // items of each window (win_left's value between iterations)
+  int64_t const* empty_wins;   // windows without items: applied by the last window's block
+  int64_t nempty;
+  int64_t nwin_items;          // windows with items
 };
 
 template <typename T>
@@ -529,6 +567,120 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
   __syncthreads();
 }
 
+// ---- fused apply (single GPU, pagerank_impl): an item's block adds its LDS window to
+// the global sums and counts the item off its window; the block that finishes a
+// window's last item applies the window (k_pr_apply's per-vertex update) -- from
+// LDS when the item is the whole window, so such a window's sums never leave the
+// CU.  The diff / dangling sums go to the state in fixed point (order-free), and the
+// block of the last window applied (ticket) applies the windows without items,
+// updates the iteration state and clears the other parity's queue heads (unused
+// since the previous launch ended).  No separate apply launch, and the apply
+// overlaps the other blocks' pushes.
+template <int WB, typename V, typename E, typename R>
+__device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64_t w, unsigned long long* lds,
+                                             unsigned long long& my_diff, unsigned long long& my_dang)
+{
+  auto const& a     = sa.a;
+  double const base = a.st->base;
+  double const pf   = a.st->pers_factor;
+  int64_t const v0  = w << WB;
+  int const n       = (int)min((int64_t)1 << WB, a.nv - v0);
+  constexpr int kB  = 4;  // vertices' loads in flight per thread
+  for (int i0 = threadIdx.x; i0 < n; i0 += kB * kPushThreads) {
+    unsigned long long f[kB];
+    R old[kB], ow[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      int const i = i0 + j * kPushThreads;
+      if (i < n) {
+        f[j]   = lds ? lds[i] : sa.acc[v0 + i];
+        old[j] = a.pr[v0 + i];
+        ow[j]  = a.outw[v0 + i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      int const i = i0 + j * kPushThreads;
+      if (i < n) {
+        if (lds) lds[i] = 0ull;
+        else if (f[j]) sa.acc[v0 + i] = 0ull;  // zero again for the next iteration
+        vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf,
+                                    my_diff, my_dang);
+      }
+    }
+  }
+}
+
+template <int WB, typename V, typename E, typename R>
+__device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
+{
+  __shared__ unsigned long long s_red[kPushThreads / 64];
+  __shared__ int s_flag;
+  int const tid       = threadIdx.x;
+  int64_t const w     = win_w & kWinMask;
+  bool const whole    = (win_w & kWholeItem) != 0;
+  unsigned long long my_diff = 0, my_dang = 0;
+  __syncthreads();  // the item's LDS sums are complete
+  if (!whole) {
+    unsigned long long* g = sa.acc + (w << WB);
+    for (int i = tid; i < (1 << WB); i += kPushThreads) {
+      unsigned long long const v = acc[i];
+      if (v) {
+        atomicAdd(g + i, v);
+        acc[i] = 0ull;
+      }
+    }
+    __threadfence();  // release: this block's adds before its count
+    __syncthreads();
+    if (tid == 0) s_flag = atomicSub(sa.win_left + w, 1u) == 1u;
+    __syncthreads();
+    if (!s_flag) return;
+    __threadfence();  // acquire: the window's other items' adds
+    if (tid == 0) sa.win_left[w] = sa.win_items[w];
+  }
+  apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
+  unsigned long long const bd = block_sum_u64<kPushThreads>(my_diff, s_red);
+  unsigned long long const bg = block_sum_u64<kPushThreads>(my_dang, s_red);
+  if (tid == 0) {
+    atomicAdd(&sa.a.st->fdiff, bd);
+    atomicAdd(&sa.a.st->fdang, bg);
+    __threadfence();
+    s_flag = atomicAdd(&sa.a.st->wticket, 1u) == (unsigned)(sa.nwin_items - 1);
+  }
+  __syncthreads();
+  if (!s_flag) {
+    __syncthreads();  // (LDS of a whole window: cleared by apply_window before the next item)
+    return;
+  }
+  __threadfence();
+  my_diff = my_dang = 0;
+  for (int64_t k = 0; k < sa.nempty; ++k) apply_window<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, my_diff, my_dang);
+  unsigned long long const ed = block_sum_u64<kPushThreads>(my_diff, s_red);
+  unsigned long long const eg = block_sum_u64<kPushThreads>(my_dang, s_red);
+  if (tid == 0) {
+    unsigned long long const d = atomicExch(&sa.a.st->fdiff, 0ull) + ed;
+    unsigned long long const g = atomicExch(&sa.a.st->fdang, 0ull) + eg;
+    sa.a.st->wticket           = 0u;
+    update_state<V, E, R>(sa.a, (double)d * kSumScaleInv, (double)g * kSumScaleInv, true);
+  }
+  if (tid < kQueues) sa.tile_ctr[((sa.parity ^ 1) * kQueues + tid) * kCtrStride] = 0u;
+  __syncthreads();
+}
+
+// the end of an item: fused finish, or the global sums for k_pr_apply
+// (16K windows only: the 64-VGPR kernels of smaller windows would spill around it)
+template <int WB, typename V, typename E, typename R>
+__device__ __forceinline__ void end_item(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
+{
+  if constexpr (WB >= 14) {
+    if (sa.fuse) {
+      fused_finish<WB, V, E, R>(sa, acc, win_w);
+      return;
+    }
+  }
+  flush_window<WB, V, E, R>(sa, acc, win_w);
+}
+
 // The push: persistent blocks take items from their queue, then from the others.
 // The unit body is branch-free (masked lanes load x~[base] and add 0; the next
 // unit of the item is always prefetched, the last re-reading itself -- ent and ew
@@ -548,7 +700,7 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
     if (tid == 0) {
-      int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + q * kCtrStride, 1u);
+      int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + (sa.parity * kQueues + q) * kCtrStride, 1u);
       s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
     }
     __syncthreads();
@@ -608,7 +760,7 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
       n    = nn;
       base = bsn;
     }
-    flush_window<WB, V, E, R>(sa, acc, win);
+    end_item<WB, V, E, R>(sa, acc, win);
   }
 }
 
@@ -734,7 +886,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
     if (tid == 0) {
-      int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + q * kCtrStride, 1u);
+      int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + (sa.parity * kQueues + q) * kCtrStride, 1u);
       s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
     }
     __syncthreads();
@@ -860,7 +1012,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         base = __builtin_amdgcn_readfirstlane(b1);
       }
     }
-    flush_window<WB, V, E, R>(sa, acc, win);
+    end_item<WB, V, E, R>(sa, acc, win);
   }
 }
 
@@ -887,11 +1039,12 @@ template <typename V, typename E, typename R>
 __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 {
   auto const& a = sa.a;
-  if (sa.tile_ctr && blockIdx.x == 0 && threadIdx.x < kQueues) sa.tile_ctr[threadIdx.x * kCtrStride] = 0u;  // push done
+  if (sa.tile_ctr && blockIdx.x == 0 && threadIdx.x < kQueues)
+    sa.tile_ctr[(sa.parity * kQueues + threadIdx.x) * kCtrStride] = 0u;  // push done
   if (a.st->done) return;
   double const base = a.st->base;
   double const pf   = a.st->pers_factor;
-  double my_diff = 0, my_dang = 0;
+  unsigned long long my_diff = 0, my_dang = 0;
   int64_t const stride = (int64_t)gridDim.x * blockDim.x;
   int64_t v            = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   // kApplyBatch vertices per thread with all loads issued before the first store
@@ -1301,6 +1454,30 @@ inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std
     else multi[wu] = 1;
   }
   to_device(units, hu.data(), (size_t)nunits, s);
+  // items per window (fused apply); windows are the real ones only when ngroups == 1
+  if (pp.ngroups == 1) {
+    std::vector<uint32_t> cnt((size_t)std::max<int64_t>(pp.nwin, 1), 0u);
+    for (int64_t i = 0; i < nitems; ++i) {
+      int64_t const wu = hu[item_u[i]].win & kWinMask;
+      if (wu < pp.nwin) ++cnt[wu];
+    }
+    std::vector<int64_t> empty;
+    pp.nwin_items = 0;
+    for (int64_t w = 0; w < pp.nwin; ++w) {
+      if (cnt[w]) ++pp.nwin_items;
+      else empty.push_back(w);
+    }
+    pp.nempty = (int64_t)empty.size();
+    pp.win_items.set_stream(s);
+    pp.win_items.resize(cnt.size() * sizeof(uint32_t));
+    to_device(pp.win_items.data<uint32_t>(), cnt.data(), cnt.size(), s);
+    pp.win_left.set_stream(s);
+    pp.win_left.resize(cnt.size() * sizeof(uint32_t));
+    pp.empty_wins.set_stream(s);
+    pp.empty_wins.resize(std::max<size_t>(empty.size(), 1) * sizeof(int64_t));
+    if (!empty.empty()) to_device(pp.empty_wins.data<int64_t>(), empty.data(), empty.size(), s);
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
   pp.win_multi.set_stream(s);
   pp.win_multi.resize(multi.size());
   to_device(pp.win_multi.data<uint8_t>(), multi.data(), multi.size(), s);
@@ -1663,8 +1840,8 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.acc.resize(pp.ngroups * pp.nacc * sizeof(unsigned long long));
   HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.ngroups * pp.nacc * sizeof(unsigned long long), s));
   pp.tile_ctr.set_stream(s);
-  pp.tile_ctr.resize(kQueues * kCtrStride * sizeof(unsigned int));
-  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, kQueues * kCtrStride * sizeof(unsigned int), s));
+  pp.tile_ctr.resize(2 * kQueues * kCtrStride * sizeof(unsigned int));  // two sets: iteration parity
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
   pp.nunits = 0;
   pp.nitems = 0;
   pp.qoff.assign(kQueues + 1, 0);
@@ -1921,8 +2098,27 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.ngroups  = pp.ngroups;
   sa.nacc     = pp.nacc;
   sa.nwin     = pp.nwin;
-  HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, kQueues * kCtrStride * sizeof(unsigned int), s));
+  HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
+  sa.fuse   = 0;  // the caller opts in (fuse_apply)
+  sa.parity = 0;
+  if (!pp.win_items.empty()) {
+    sa.win_items  = pp.win_items.data<uint32_t>();
+    sa.win_left   = pp.win_left.data<uint32_t>();
+    sa.empty_wins = pp.empty_wins.data<int64_t>();
+    sa.nempty     = pp.nempty;
+    sa.nwin_items = pp.nwin_items;
+    HIP_CHECK(hipMemcpyAsync(sa.win_left, sa.win_items, pp.nwin * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  }
 
+}
+
+// fused apply (fused_finish) for a single-GPU schedule: 16K windows, one source group, items,
+// few windows without items (the last block applies those alone); CGX_PR_FUSE=0
+// keeps the separate k_pr_apply (A/B)
+inline bool fuse_apply(pr_push_t const& pp)
+{
+  return pp.win_bits >= 14 && pp.ngroups == 1 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
+         !env_is("CGX_PR_FUSE", "0");
 }
 
 // source dedup in the packed push (push_body16 DD); CGX_PR_DEDUP=0/1 (A/B)
@@ -2090,6 +2286,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.win_bits  = adj.pr.win_bits;
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
+    sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
   }
   // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
   // predicted remainder.  Profiling records one pair of pooled HIP events around each chunk -- an event
@@ -2113,9 +2310,10 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       a.x_in  = bufs[launched & 1];
       a.x_out = bufs[(launched + 1) & 1];
       if (push) {
-        sa.a = a;
+        sa.a      = a;
+        sa.parity = (int)(launched & 1);
         if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
-        hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sa);
+        if (!sa.fuse) hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sa);
       } else {
         hipLaunchKernelGGL(kernel, dim3(nblk_iter), dim3(kBlock), 0, s, a);
       }

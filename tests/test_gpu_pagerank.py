@@ -372,3 +372,52 @@ def test_window_bits_bitwise_equal(scale, monkeypatch):
     for o in out[1:]:
         assert o[2] == out[0][2]
         assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+
+
+def _empty_window_graph():
+    """Not renumbered, 16K windows: ids >= 2^15 only send (no in-edges), so windows 2
+    and 3 have no push items and are applied by the last window's block."""
+    rng = np.random.default_rng(3)
+    n_lo, n = 1 << 15, (1 << 15) + (1 << 14) + 100
+    hi = np.arange(n_lo, n, dtype=np.int32)
+    s = np.concatenate([hi, np.arange(n_lo, dtype=np.int32), rng.integers(0, n_lo, 200_000).astype(np.int32)])
+    d = np.concatenate([rng.integers(0, n_lo, hi.size).astype(np.int32), np.roll(np.arange(n_lo, dtype=np.int32), 1),
+                        rng.integers(0, n_lo, 200_000).astype(np.int32)])
+    pairs = np.unique(s.astype(np.int64) * n + d)
+    pairs = pairs[pairs // n != pairs % n]
+    return (pairs // n).astype(np.int32), (pairs % n).astype(np.int32), n
+
+
+@pytest.mark.parametrize("graph", ["rmat20", "empty_windows"])
+def test_fused_apply_bitwise_equal(graph, monkeypatch):
+    """The push with the apply fused in (pagerank.hip fused_finish: the block that
+    finishes a window applies it, from LDS for whole-window items; the last one
+    applies the windows without items and updates the state) gives the same bits
+    and iteration count as the separate k_pr_apply (CGX_PR_FUSE=0), with and
+    without whole-window items (CGX_PR_WHOLE=0)."""
+    monkeypatch.setenv("CGX_PR_WIN_BITS", "14")
+    if graph == "rmat20":
+        s, d, _ = rmat_graph(20, False, True)
+        kw = dict(renumber=True, symmetric=True)
+        n = None
+    else:
+        s, d, n = _empty_window_graph()
+        kw = dict(renumber=False, symmetric=False)
+    out = []
+    for fuse, whole in (("1", "1"), ("0", "1"), ("1", "0")):
+        monkeypatch.setenv("CGX_PR_FUSE", fuse)
+        monkeypatch.setenv("CGX_PR_WHOLE", whole)
+        h, G = make_graph(s, d, None, transposed=True, **kw)
+        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        # a second call on the same schedule: queue heads and window counts were reset
+        _, r2 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert np.array_equal(host(r), host(r2))
+        out.append((host(v), host(r), h.last_iterations()))
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+    if n is not None:
+        got = np.zeros(n)
+        got[out[0][0]] = out[0][1]
+        ref = opr.pagerank(n, s, d, None, 0.85, 1e-6, 500)
+        assert (np.abs(got[:n] - ref) / ref).max() < REL
