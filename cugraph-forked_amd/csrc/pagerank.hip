@@ -576,6 +576,19 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
 // updates the iteration state and clears the other parity's queue heads (unused
 // since the previous launch ended).  No separate apply launch, and the apply
 // overlaps the other blocks' pushes.
+//
+// No agent-scope fence anywhere: a fence's acquire half (buffer_inv sc1) drops the
+// XCD's cached lines -- the x~ lines every other block on the XCD is gathering -- and
+// with one per item the iteration took 1.31 instead of 0.71 ms (RMAT-24).  Every
+// hand-off here goes through device-scope atomics instead, which are performed at the
+// coherence point: a window's partial sums are u64 atomic adds, each thread waits for
+// its own (s_waitcnt vmcnt(0)) before the block counts the item off, and the
+// finishing block reads and clears the sums with atomic exchanges; the (diff,
+// dangling) sums are atomic adds waited for before the ticket, and read back by the
+// last block with exchanges.  Nothing else written in the launch is read in it
+// (pr / x~' / the queue heads of the other parity are read by the next launch).
+__device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 template <int WB, typename V, typename E, typename R>
 __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64_t w, unsigned long long* lds,
                                              unsigned long long& my_diff, unsigned long long& my_dang)
@@ -593,7 +606,12 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
     for (int j = 0; j < kB; ++j) {
       int const i = i0 + j * kPushThreads;
       if (i < n) {
-        f[j]   = lds ? lds[i] : sa.acc[v0 + i];
+        if (lds) {
+          f[j]   = lds[i];
+          lds[i] = 0ull;
+        } else {  // read and zero for the next iteration, at the coherence point
+          f[j] = __hip_atomic_exchange(sa.acc + v0 + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         old[j] = a.pr[v0 + i];
         ow[j]  = a.outw[v0 + i];
       }
@@ -601,12 +619,9 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       int const i = i0 + j * kPushThreads;
-      if (i < n) {
-        if (lds) lds[i] = 0ull;
-        else if (f[j]) sa.acc[v0 + i] = 0ull;  // zero again for the next iteration
+      if (i < n)
         vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf,
                                     my_diff, my_dang);
-      }
     }
   }
 }
@@ -626,41 +641,41 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
     for (int i = tid; i < (1 << WB); i += kPushThreads) {
       unsigned long long const v = acc[i];
       if (v) {
-        atomicAdd(g + i, v);
+        __hip_atomic_fetch_add(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         acc[i] = 0ull;
       }
     }
-    __threadfence();  // release: this block's adds before its count
+    wait_vmem();  // this thread's adds are performed before the item is counted off
     __syncthreads();
-    if (tid == 0) s_flag = atomicSub(sa.win_left + w, 1u) == 1u;
+    if (tid == 0)
+      s_flag = __hip_atomic_fetch_sub(sa.win_left + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
     __syncthreads();
     if (!s_flag) return;
-    __threadfence();  // acquire: the window's other items' adds
-    if (tid == 0) sa.win_left[w] = sa.win_items[w];
+    if (tid == 0)
+      __hip_atomic_store(sa.win_left + w, sa.win_items[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
   unsigned long long const bd = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const bg = block_sum_u64<kPushThreads>(my_dang, s_red);
   if (tid == 0) {
-    atomicAdd(&sa.a.st->fdiff, bd);
-    atomicAdd(&sa.a.st->fdang, bg);
-    __threadfence();
-    s_flag = atomicAdd(&sa.a.st->wticket, 1u) == (unsigned)(sa.nwin_items - 1);
+    __hip_atomic_fetch_add(&sa.a.st->fdiff, bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&sa.a.st->fdang, bg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wait_vmem();
+    s_flag = __hip_atomic_fetch_add(&sa.a.st->wticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned)(sa.nwin_items - 1);
   }
   __syncthreads();
-  if (!s_flag) {
-    __syncthreads();  // (LDS of a whole window: cleared by apply_window before the next item)
-    return;
-  }
-  __threadfence();
+  if (!s_flag) return;  // (a whole window's LDS was cleared by apply_window)
   my_diff = my_dang = 0;
   for (int64_t k = 0; k < sa.nempty; ++k) apply_window<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, my_diff, my_dang);
   unsigned long long const ed = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const eg = block_sum_u64<kPushThreads>(my_dang, s_red);
   if (tid == 0) {
-    unsigned long long const d = atomicExch(&sa.a.st->fdiff, 0ull) + ed;
-    unsigned long long const g = atomicExch(&sa.a.st->fdang, 0ull) + eg;
-    sa.a.st->wticket           = 0u;
+    unsigned long long const d =
+        __hip_atomic_exchange(&sa.a.st->fdiff, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ed;
+    unsigned long long const g =
+        __hip_atomic_exchange(&sa.a.st->fdang, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + eg;
+    __hip_atomic_store(&sa.a.st->wticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     update_state<V, E, R>(sa.a, (double)d * kSumScaleInv, (double)g * kSumScaleInv, true);
   }
   if (tid < kQueues) sa.tile_ctr[((sa.parity ^ 1) * kQueues + tid) * kCtrStride] = 0u;
