@@ -610,7 +610,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_pr_push16_w14 (16K-destination windows from 2^23 vertices, else k_pr_push16; packed 16-bit entries; k_pr_push_q* for weighted graphs) + k_pr_apply (one PageRank iteration): HIP events on the library stream around "
+            "kernel": ("k_pr_push16_w14 with the apply fused in (16K-destination windows from 2^23 vertices; below that k_pr_push16 + k_pr_apply; packed 16-bit entries; k_pr_push_q* for weighted graphs) = one PageRank iteration: HIP events on the library stream around "
                        "each chunk of iterations in the timed region / iterations run (inter-kernel gaps "
                        "included)" if world == 1 else
                        "one MG PageRank iteration per rank (row allgather + push + column reduce-scatter + apply + "
@@ -639,7 +639,7 @@ def main():
             tb, detail = pagerank_traffic(args)
             out["roofline"]["traffic"] = tb
             out["roofline"]["traffic_note"] = (
-                "HBM bytes per iteration (k_pr_push + k_pr_apply) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from separate "
+                "HBM bytes per iteration (k_pr_push [+ k_pr_apply when not fused]) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from separate "
                 f"rocprofv3 --pmc passes: {detail}")
         except Exception as e:  # noqa: BLE001
             out["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]

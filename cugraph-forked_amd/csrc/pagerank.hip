@@ -419,6 +419,9 @@ constexpr int kCtrStride   = 32;   // queue heads 128 B apart
 constexpr int kPushBlocks  = 512;  // persistent grid: two 1024-thread blocks per CU, 256 CUs
 constexpr int kSrcBinBits  = 14;   // source-range cut granularity: 16K sources
 constexpr int kMaxSliceRanges = 12;
+// LDS left beside a 16K-window push block's 128 KB of sums (163,840 B per workgroup on
+// gfx950, less the block's other shared words) for the hub x~ (push_body16 HUB)
+constexpr int kHubBytes = 32768 - 512;
 #ifndef CGX_APPLY_BATCH
 #define CGX_APPLY_BATCH 4
 #endif
@@ -502,6 +505,7 @@ struct push_args {
   int64_t const* empty_wins;   // windows without items: applied by the last window's block
   int64_t nempty;
   int64_t nwin_items;          // windows with items
+  int64_t nhub;                // sources whose x~ the 16K-window push stages in LDS (0: none)
 };
 
 template <typename T>
@@ -878,7 +882,13 @@ __device__ __forceinline__ void wave_max_scan_rows(uint32_t (&v)[N])
 // head's value with one ds_bpermute when the row is summed.  The texture path is
 // the push's busiest unit (RMAT-24: TA 71 %, TD 80 % busy, mostly stalled on L2),
 // and its work follows the active lanes.
-template <int WB, typename V, typename E, typename R, bool ENC, bool DD>
+// HUB (16K windows): the x~ of the first sa.nhub sources (the hubs: ids descend by
+// degree) are staged in the LDS left beside the window, once per launch, and a wave
+// segment whose sources are all hubs reads them there instead of gathering through
+// the texture path -- the push's busiest unit (TA 71 %, TD 80 % busy).  Sources are
+// sorted within a window, so almost every segment is all-hub or hub-free; a segment
+// that straddles the boundary gathers from global memory.
+template <int WB, typename V, typename E, typename R, bool ENC, bool DD, bool HUB = false>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -889,6 +899,8 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   constexpr int kRows       = kSegEntries / 64;
   static_assert(kRows == kPerThread, "a wave segment is one unit row per thread");
   __shared__ unsigned long long acc[kWin];
+  constexpr int kHub = HUB ? kHubBytes / (int)sizeof(xw_t) : 1;
+  __shared__ xw_t hub[kHub];
   __shared__ int64_t s_item;
   if (sa.a.st->done) return;
   int const tid  = threadIdx.x;
@@ -898,6 +910,9 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   using cunit_t        = __attribute__((address_space(4))) push_unit const;
   cunit_t* const units = (cunit_t*)sa.units;
   xw_t const* const x  = reinterpret_cast<xw_t const*>(sa.a.x_in);
+  uint32_t const nh    = HUB ? (uint32_t)min((int64_t)kHub, sa.nhub) : 0u;
+  if constexpr (HUB)
+    for (uint32_t i = tid; i < nh; i += kPushThreads) hub[i] = x[i];  // (the first item's barrier publishes it)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
     if (tid == 0) {
@@ -949,6 +964,22 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       }
       wave_incl_scan_rows<kRows>(sc);
       uint32_t run = base;
+      if constexpr (HUB) {
+        uint32_t src[kRows];
+#pragma unroll
+        for (int j = 0; j < kRows; ++j) {
+          src[j] = run + sc[j];
+          run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
+        }
+        if (run < nh) {  // wave-uniform: the segment's last source (lane 63 of row 7) is a hub
+#pragma unroll
+          for (int j = 0; j < kRows; ++j) xv[j] = hub[src[j]];
+        } else {
+#pragma unroll
+          for (int j = 0; j < kRows; ++j) xv[j] = x[src[j]];
+        }
+        return;
+      }
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const src = run + sc[j];
@@ -1041,7 +1072,7 @@ __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R
 template <typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
 {
-  push_body16<14, V, E, R, ENC, false>(sa);
+  push_body16<14, V, E, R, ENC, false, true>(sa);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -2302,6 +2333,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
     sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
+    sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
   // predicted remainder.  Profiling records one pair of pooled HIP events around each chunk -- an event

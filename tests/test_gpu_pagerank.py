@@ -421,3 +421,27 @@ def test_fused_apply_bitwise_equal(graph, monkeypatch):
         got[out[0][0]] = out[0][1]
         ref = opr.pagerank(n, s, d, None, 0.85, 1e-6, 500)
         assert (np.abs(got[:n] - ref) / ref).max() < REL
+
+
+@pytest.mark.parametrize("graph", ["rmat12", "rmat20", "star"])
+def test_hub_lds_bitwise_equal(graph, monkeypatch):
+    """The 16K-window push that reads the hubs' x~ from LDS (pagerank.hip push_body16
+    HUB: segments whose sources are all below the staged count) gives the same bits
+    as gathering every x~ from global memory (CGX_PR_HUB=0), with encoded and plain
+    float x~.  RMAT-12 has fewer vertices than the LDS holds (every segment reads
+    LDS); the star graph has long runs of one hub source."""
+    monkeypatch.setenv("CGX_PR_WIN_BITS", "14")
+    if graph == "star":
+        s, d = _star_plus_ring(300_000)
+    else:
+        s, d, _ = rmat_graph(int(graph[4:]), False, True)
+    out = []
+    for hub, enc in (("1", "1"), ("0", "1"), ("1", "0")):
+        monkeypatch.setenv("CGX_PR_HUB", hub)
+        monkeypatch.setenv("CGX_PR_ENC", enc)
+        h, G = make_graph(s, d, None, transposed=True, symmetric=graph != "star")
+        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        out.append((host(v), host(r), h.last_iterations()))
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
