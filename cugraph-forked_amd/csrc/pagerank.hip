@@ -506,6 +506,11 @@ struct push_args {
   int64_t nempty;
   int64_t nwin_items;          // windows with items
   int64_t nhub;                // sources whose x~ the 16K-window push stages in LDS (0: none)
+  // CGX_PR_TIMELINE (measurement only): per item {launch << 32 | block, item, start, end}
+  // in s_memrealtime ticks (100 MHz), tl[0] = records written
+  unsigned long long* tl;
+  int64_t tl_cap;
+  int launch;
 };
 
 template <typename T>
@@ -915,6 +920,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     for (uint32_t i = tid; i < nh; i += kPushThreads) hub[i] = x[i];  // (the first item's barrier publishes it)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
+    unsigned long long const t_fetch = sa.tl ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (tid == 0) {
       int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + (sa.parity * kQueues + q) * kCtrStride, 1u);
       s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
@@ -1059,6 +1065,17 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       }
     }
     end_item<WB, V, E, R>(sa, acc, win);
+    if (sa.tl && tid == 0) {
+      unsigned long long const t_end = __builtin_amdgcn_s_memrealtime();
+      unsigned long long const k     = atomicAdd(sa.tl, 1ull);
+      if ((int64_t)k < sa.tl_cap) {
+        unsigned long long* r = sa.tl + 1 + 4 * k;
+        r[0] = ((unsigned long long)sa.launch << 32) | blockIdx.x;
+        r[1] = (unsigned long long)it;
+        r[2] = t_fetch;
+        r[3] = t_end;
+      }
+    }
   }
 }
 
@@ -2335,6 +2352,15 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
+  // CGX_PR_TIMELINE=<file>: per-item timeline of the packed push (measurement only)
+  char const* tl_path = push ? std::getenv("CGX_PR_TIMELINE") : nullptr;
+  dbuf<unsigned long long> tl;
+  if (tl_path) {
+    sa.tl_cap = 1 << 20;
+    tl.resize(1 + 4 * sa.tl_cap, s);
+    HIP_CHECK(hipMemsetAsync(tl.data(), 0, sizeof(unsigned long long), s));
+    sa.tl = tl.data();
+  }
   // Chunked enqueue (next_chunk): a host check after 8 iterations, then after the
   // predicted remainder.  Profiling records one pair of pooled HIP events around each chunk -- an event
   // between every two iterations cost a ~10 us queue gap per iteration -- and
@@ -2359,6 +2385,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       if (push) {
         sa.a      = a;
         sa.parity = (int)(launched & 1);
+        sa.launch = (int)launched;
         if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
         if (!sa.fuse) hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sa);
       } else {
@@ -2374,6 +2401,22 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     if (hst.done) break;
   }
   h.last_iterations = (size_t)hst.iter;
+  if (tl_path) {
+    unsigned long long n = 0;
+    HIP_CHECK(hipMemcpyAsync(&n, tl.data(), sizeof(n), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    n = std::min<unsigned long long>(n, (unsigned long long)sa.tl_cap);
+    std::vector<unsigned long long> rec(4 * n);
+    if (n) HIP_CHECK(hipMemcpyAsync(rec.data(), tl.data() + 1, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (FILE* f = std::fopen(tl_path, "w")) {
+      std::fprintf(f, "launch,block,item,start,end\n");
+      for (unsigned long long i = 0; i < n; ++i)
+        std::fprintf(f, "%llu,%llu,%llu,%llu,%llu\n", rec[4 * i] >> 32, rec[4 * i] & 0xffffffffull, rec[4 * i + 1],
+                     rec[4 * i + 2], rec[4 * i + 3]);
+      std::fclose(f);
+    }
+  }
   if (h.profiling) {
     double tot = 0;
     for (size_t i = 0; i + 1 < ev.size(); i += 2) {

@@ -10,7 +10,7 @@ TAG=${TAG:-r03}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 if [ "${1:-}" != "skip-tests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread --durations=25 > $OUT/pytest.log 2>&1
+  CGX_TEST_CLOCK=1 timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread --durations=40 > $OUT/pytest.log 2>&1
   rc=$?; tail -3 $OUT/pytest.log
   # 1 = some test failed (the process itself ended normally): still take the bench
   # record; anything else (fault, abort, time limit) ends the call here
