@@ -140,6 +140,10 @@ struct pr_push_t {
   buffer win_left;        // uint32[nwin]: win_items between iterations
   buffer empty_wins;      // int64[nempty]
   int64_t nempty = 0, nwin_items = 0;
+  // measured-cost queues (pagerank.hip calibrate_queues): the first launch on a schedule
+  // records every item's duration, the host then re-deals the items by those costs
+  buffer item_ticks;      // uint32[nitems], s_memrealtime ticks
+  int calib = 0;          // 0 not yet, 1 recorded (re-deal pending), 2 done or off
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

@@ -511,6 +511,7 @@ struct push_args {
   unsigned long long* tl;
   int64_t tl_cap;
   int launch;
+  uint32_t* item_ticks;  // calibration launch: every item's duration (s_memrealtime ticks), else nullptr
 };
 
 template <typename T>
@@ -920,7 +921,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     for (uint32_t i = tid; i < nh; i += kPushThreads) hub[i] = x[i];  // (the first item's barrier publishes it)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
-    unsigned long long const t_fetch = sa.tl ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long const t_fetch = (sa.tl || sa.item_ticks) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (tid == 0) {
       int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + (sa.parity * kQueues + q) * kCtrStride, 1u);
       s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
@@ -1065,13 +1066,14 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       }
     }
     end_item<WB, V, E, R>(sa, acc, win);
+    if (sa.item_ticks && tid == 0) sa.item_ticks[it] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_fetch);
     if (sa.tl && tid == 0) {
       unsigned long long const t_end = __builtin_amdgcn_s_memrealtime();
       unsigned long long const k     = atomicAdd(sa.tl, 1ull);
       if ((int64_t)k < sa.tl_cap) {
         unsigned long long* r = sa.tl + 1 + 4 * k;
         r[0] = ((unsigned long long)sa.launch << 32) | blockIdx.x;
-        r[1] = (unsigned long long)it;
+        r[1] = ((unsigned long long)(units[ub - 1].k1 - units[ua].k0) << 32) | (unsigned long long)it;
         r[2] = t_fetch;
         r[3] = t_end;
       }
@@ -1832,7 +1834,14 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   item_u.push_back(nunits);
   std::vector<int64_t> queue;
   queue.reserve(nitems);
-  if (xcd_queues) {
+  char const* qmode = std::getenv("CGX_PR_QMODE");  // measurement: "global" / "lpt" single queue
+  if (xcd_queues && qmode && (std::string(qmode) == "global" || std::string(qmode) == "lpt")) {
+    for (int64_t i = 0; i < nitems; ++i) queue.push_back(i);
+    if (std::string(qmode) == "lpt")
+      std::stable_sort(queue.begin(), queue.end(), [&](int64_t a, int64_t b) { return item_e[a] > item_e[b]; });
+    pp.qoff[0] = 0;
+    for (int q = 1; q < kQueues; ++q) pp.qoff[q] = nitems;
+  } else if (xcd_queues) {
     int64_t const ngroups = (nitems + kGroupItems - 1) / kGroupItems;
     std::vector<int64_t> gsize(ngroups, 0), gorder(ngroups);
     for (int64_t i = 0; i < nitems; ++i) gsize[i / kGroupItems] += item_e[i];
@@ -1860,6 +1869,67 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   pp.qoff[kQueues] = (int64_t)queue.size();
   mark_whole_items(s, pp, units, hu, item_u, nitems);
   upload_items(s, pp, item_u, queue, nitems);
+}
+
+// Measured-cost queues.  An item's entries do not predict its time well: on RMAT-24
+// the items of the middle windows (low-degree destinations drawing sources from the
+// whole id range) take up to 2.3x the median for the same entries, and with the
+// groups dealt by entries the last items ended up to 140 us after most blocks had
+// run out of work (per-item timeline, CGX_PR_TIMELINE: blocks busy 83.5 % of a
+// launch).  So the first launch on a schedule records every item's duration
+// (item_ticks) and the host re-deals the items by those costs: groups of kCalGroup
+// consecutive items (neighbouring windows keep sharing x~ lines in their XCD's L2)
+// dealt longest-first to the least-loaded queue, each queue taking its groups
+// costliest-first, so what is left for the last blocks is short.  Queue order does
+// not change any sum (fixed-point adds), only who takes an item when.
+// CGX_PR_CALIB=0 keeps the entry-dealt queues; CGX_PR_DEAL=global puts every item in
+// one queue, longest-first (A/B).
+constexpr int kCalGroup = 16;
+
+inline bool calibration_wanted(pr_push_t const& pp)
+{
+  return pp.calib == 0 && pp.nitems > 0 && pp.win_bits >= 13 && pp.ngroups == 1 && pp.src_head < 0 &&
+         !env_is("CGX_PR_CALIB", "0") && !std::getenv("CGX_PR_QMODE");
+}
+
+inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
+{
+  int64_t const n = pp.nitems;
+  auto t          = to_host(pp.item_ticks.data<uint32_t>(), n, s);
+  std::vector<int64_t> queue;
+  queue.reserve(n);
+  if (env_is("CGX_PR_DEAL", "global")) {
+    for (int64_t i = 0; i < n; ++i) queue.push_back(i);
+    std::stable_sort(queue.begin(), queue.end(), [&](int64_t a, int64_t b) { return t[a] > t[b]; });
+    pp.qoff.assign(kQueues + 1, n);
+    pp.qoff[0] = 0;
+  } else {
+    int64_t const ng = (n + kCalGroup - 1) / kCalGroup;
+    std::vector<uint64_t> gc(ng, 0);
+    for (int64_t i = 0; i < n; ++i) gc[i / kCalGroup] += t[i];
+    std::vector<int64_t> go(ng);
+    for (int64_t g = 0; g < ng; ++g) go[g] = g;
+    std::stable_sort(go.begin(), go.end(), [&](int64_t a, int64_t b) { return gc[a] > gc[b]; });
+    std::vector<std::vector<int64_t>> qg(kQueues);
+    uint64_t load[kQueues] = {};
+    for (int64_t g : go) {  // costliest group first, to the least-loaded queue: each queue's list is costliest-first
+      int best = 0;
+      for (int q = 1; q < kQueues; ++q)
+        if (load[q] < load[best]) best = q;
+      qg[best].push_back(g);
+      load[best] += gc[g];
+    }
+    pp.qoff.assign(kQueues + 1, 0);
+    for (int q = 0; q < kQueues; ++q) {
+      pp.qoff[q] = (int64_t)queue.size();
+      for (int64_t g : qg[q])
+        for (int64_t i = g * kCalGroup; i < std::min(n, (g + 1) * kCalGroup); ++i) queue.push_back(i);
+    }
+    pp.qoff[kQueues] = n;
+  }
+  to_device(pp.queue.data<int64_t>(), queue.data(), queue.size(), s);  // same size: in place, stream-ordered
+  HIP_CHECK(hipStreamSynchronize(s));
+  pp.calib = 2;
 }
 
 // Push schedule of an edge list given as (row = destination, col = source) with
@@ -2352,6 +2422,16 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
+  // measured-cost queues: the first launch on this schedule records item durations
+  bool calibrating = push && adj.pr.packed && calibration_wanted(adj.pr);
+  if (calibrating) {
+    adj.pr.item_ticks.set_stream(s);
+    adj.pr.item_ticks.resize(adj.pr.nitems * sizeof(uint32_t));
+    HIP_CHECK(hipMemsetAsync(adj.pr.item_ticks.data(), 0, adj.pr.nitems * sizeof(uint32_t), s));
+    adj.pr.calib = 1;
+  } else if (push && adj.pr.calib == 0) {
+    adj.pr.calib = 2;
+  }
   // CGX_PR_TIMELINE=<file>: per-item timeline of the packed push (measurement only)
   char const* tl_path = push ? std::getenv("CGX_PR_TIMELINE") : nullptr;
   dbuf<unsigned long long> tl;
@@ -2383,9 +2463,10 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
       a.x_in  = bufs[launched & 1];
       a.x_out = bufs[(launched + 1) & 1];
       if (push) {
-        sa.a      = a;
-        sa.parity = (int)(launched & 1);
-        sa.launch = (int)launched;
+        sa.a          = a;
+        sa.parity     = (int)(launched & 1);
+        sa.launch     = (int)launched;
+        sa.item_ticks = calibrating && launched == 0 ? adj.pr.item_ticks.data<uint32_t>() : nullptr;
         if (nblk_push) hipLaunchKernelGGL(pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sa);
         if (!sa.fuse) hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sa);
       } else {
@@ -2398,6 +2479,11 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     HIP_CHECK(hipMemcpyAsync(hpin, st.data(), sizeof(pr_state), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     hst = *hpin;
+    if (calibrating) {  // re-deal the queues by the recorded costs (the stream is idle here)
+      calibrate_queues(s, adj.pr);
+      for (int q = 0; q <= kQueues; ++q) sa.qoff[q] = adj.pr.qoff[q];
+      calibrating = false;
+    }
     if (hst.done) break;
   }
   h.last_iterations = (size_t)hst.iter;
@@ -2410,10 +2496,14 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     if (n) HIP_CHECK(hipMemcpyAsync(rec.data(), tl.data() + 1, rec.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (FILE* f = std::fopen(tl_path, "w")) {
-      std::fprintf(f, "launch,block,item,start,end\n");
-      for (unsigned long long i = 0; i < n; ++i)
-        std::fprintf(f, "%llu,%llu,%llu,%llu,%llu\n", rec[4 * i] >> 32, rec[4 * i] & 0xffffffffull, rec[4 * i + 1],
-                     rec[4 * i + 2], rec[4 * i + 3]);
+      std::fprintf(f, "launch,block,item,entries,window,start,end\n");
+      auto hu = to_host(adj.pr.units.data<push_unit>(), adj.pr.nunits, s);
+      auto hi = to_host(adj.pr.items.data<int64_t>(), adj.pr.nitems + 1, s);
+      for (unsigned long long i = 0; i < n; ++i) {
+        unsigned long long const it = rec[4 * i + 1] & 0xffffffffull;
+        std::fprintf(f, "%llu,%llu,%llu,%llu,%lld,%llu,%llu\n", rec[4 * i] >> 32, rec[4 * i] & 0xffffffffull, it,
+                     rec[4 * i + 1] >> 32, (long long)(hu[hi[it]].win & kWinMask), rec[4 * i + 2], rec[4 * i + 3]);
+      }
       std::fclose(f);
     }
   }

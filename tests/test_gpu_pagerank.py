@@ -445,3 +445,26 @@ def test_hub_lds_bitwise_equal(graph, monkeypatch):
     for o in out[1:]:
         assert o[2] == out[0][2]
         assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+
+
+@pytest.mark.parametrize("deal", ["xcd", "global"])
+def test_calibrated_queues_bitwise_equal(deal, monkeypatch):
+    """Measured-cost queues (pagerank.hip calibrate_queues): the first call on a
+    schedule records every item's duration and re-deals the queues after its first
+    chunk; that call, a later one on the re-dealt queues, and entry-dealt queues
+    (CGX_PR_CALIB=0) give the same bits and iteration counts, for 8K and 16K windows."""
+    s, d, _ = rmat_graph(20, False, True)
+    if deal == "global":
+        monkeypatch.setenv("CGX_PR_DEAL", "global")
+    for wb in ("13", "14"):
+        monkeypatch.setenv("CGX_PR_WIN_BITS", wb)
+        out = []
+        for calib in ("1", "0"):
+            monkeypatch.setenv("CGX_PR_CALIB", calib)
+            h, G = make_graph(s, d, None, transposed=True, symmetric=True)
+            for _ in range(2):  # calibrating call, then a call on the re-dealt queues
+                v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+                out.append((host(v), host(r), h.last_iterations()))
+        for o in out[1:]:
+            assert o[2] == out[0][2]
+            assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
