@@ -608,7 +608,9 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
   double const pf   = a.st->pers_factor;
   int64_t const v0  = w << WB;
   int const n       = (int)min((int64_t)1 << WB, a.nv - v0);
-  constexpr int kB  = 4;  // vertices' loads in flight per thread
+  // half the window's vertices' loads in flight at once (8 per thread for 16K windows;
+  // 16 would spill): two memory round trips per window instead of four
+  constexpr int kB = (1 << WB) / kPushThreads / 2;
   for (int i0 = threadIdx.x; i0 < n; i0 += kB * kPushThreads) {
     unsigned long long f[kB];
     R old[kB], ow[kB];
