@@ -608,9 +608,7 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
   double const pf   = a.st->pers_factor;
   int64_t const v0  = w << WB;
   int const n       = (int)min((int64_t)1 << WB, a.nv - v0);
-  // half the window's vertices' loads in flight at once (8 per thread for 16K windows;
-  // 16 would spill): two memory round trips per window instead of four
-  constexpr int kB = (1 << WB) / kPushThreads / 2;
+  constexpr int kB = 4;  // (8, two passes for a 16K window: the same time, and the kernel spilled)
   for (int i0 = threadIdx.x; i0 < n; i0 += kB * kPushThreads) {
     unsigned long long f[kB];
     R old[kB], ow[kB];
@@ -718,6 +716,7 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
   constexpr int kWin = 1 << WB;
   __shared__ unsigned long long acc[kWin];
   __shared__ int64_t s_item;
+  __shared__ unsigned long long s_t0;
   if (sa.a.st->done) return;
   int const tid = threadIdx.x;
   for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
@@ -727,6 +726,7 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
     if (tid == 0) {
+      if (sa.item_ticks) s_t0 = __builtin_amdgcn_s_memrealtime();  // (in LDS: no register across the item)
       int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + (sa.parity * kQueues + q) * kCtrStride, 1u);
       s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
     }
@@ -788,6 +788,8 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
       base = bsn;
     }
     end_item<WB, V, E, R>(sa, acc, win);
+    // (the item id from LDS too: s_item holds it until thread 0 takes the next)
+    if (sa.item_ticks && tid == 0) sa.item_ticks[s_item] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - s_t0);
   }
 }
 
@@ -910,6 +912,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   constexpr int kHub = HUB ? kHubBytes / (int)sizeof(xw_t) : 1;
   __shared__ xw_t hub[kHub];
   __shared__ int64_t s_item;
+  __shared__ unsigned long long s_t0;
   if (sa.a.st->done) return;
   int const tid  = threadIdx.x;
   int const lane = tid & 63;
@@ -923,8 +926,10 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     for (uint32_t i = tid; i < nh; i += kPushThreads) hub[i] = x[i];  // (the first item's barrier publishes it)
   int q                = (int)(blockIdx.x % kQueues);
   for (int tries = 0; tries < kQueues;) {
-    unsigned long long const t_fetch = (sa.tl || sa.item_ticks) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (tid == 0) {
+      // item start time in LDS: a 64-bit register live across the item made the
+      // 16K-window kernel spill (127 VGPRs + 12 B scratch)
+      if (sa.tl || sa.item_ticks) s_t0 = __builtin_amdgcn_s_memrealtime();
       int64_t const i = (int64_t)atomicAdd(sa.tile_ctr + (sa.parity * kQueues + q) * kCtrStride, 1u);
       s_item          = i < sa.qoff[q + 1] - sa.qoff[q] ? sa.queue[sa.qoff[q] + i] : -1;
     }
@@ -1068,15 +1073,17 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       }
     }
     end_item<WB, V, E, R>(sa, acc, win);
-    if (sa.item_ticks && tid == 0) sa.item_ticks[it] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_fetch);
+    // (the item id from LDS too: s_item holds it until thread 0 takes the next)
+    if (sa.item_ticks && tid == 0) sa.item_ticks[s_item] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - s_t0);
     if (sa.tl && tid == 0) {
       unsigned long long const t_end = __builtin_amdgcn_s_memrealtime();
       unsigned long long const k     = atomicAdd(sa.tl, 1ull);
       if ((int64_t)k < sa.tl_cap) {
         unsigned long long* r = sa.tl + 1 + 4 * k;
         r[0] = ((unsigned long long)sa.launch << 32) | blockIdx.x;
-        r[1] = ((unsigned long long)(units[ub - 1].k1 - units[ua].k0) << 32) | (unsigned long long)it;
-        r[2] = t_fetch;
+        int64_t const iu = s_item;
+        r[1] = ((unsigned long long)(units[sa.items[iu + 1] - 1].k1 - units[sa.items[iu]].k0) << 32) | (unsigned long long)iu;
+        r[2] = s_t0;
         r[3] = t_end;
       }
     }
@@ -2425,7 +2432,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // measured-cost queues: the first launch on this schedule records item durations
-  bool calibrating = push && adj.pr.packed && calibration_wanted(adj.pr);
+  bool calibrating = push && calibration_wanted(adj.pr);
   if (calibrating) {
     adj.pr.item_ticks.set_stream(s);
     adj.pr.item_ticks.resize(adj.pr.nitems * sizeof(uint32_t));
