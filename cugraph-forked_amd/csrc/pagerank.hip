@@ -1897,7 +1897,7 @@ constexpr int kCalGroup = 16;
 
 inline bool calibration_wanted(pr_push_t const& pp)
 {
-  return pp.calib == 0 && pp.nitems > 0 && pp.win_bits >= 13 && pp.ngroups == 1 && pp.src_head < 0 &&
+  return pp.calib == 0 && pp.nitems > 0 && pp.ngroups == 1 && pp.src_head < 0 &&
          !env_is("CGX_PR_CALIB", "0") && !std::getenv("CGX_PR_QMODE");
 }
 
@@ -1907,7 +1907,9 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
   auto t          = to_host(pp.item_ticks.data<uint32_t>(), n, s);
   std::vector<int64_t> queue;
   queue.reserve(n);
-  if (env_is("CGX_PR_DEAL", "global")) {
+  // below 2^22 rows the items are tiles of <= 8 units in one queue (build_items): that
+  // queue, longest-first
+  if (env_is("CGX_PR_DEAL", "global") || pp.win_bits < 13) {
     for (int64_t i = 0; i < n; ++i) queue.push_back(i);
     std::stable_sort(queue.begin(), queue.end(), [&](int64_t a, int64_t b) { return t[a] > t[b]; });
     pp.qoff.assign(kQueues + 1, n);

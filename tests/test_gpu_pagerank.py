@@ -452,11 +452,12 @@ def test_calibrated_queues_bitwise_equal(deal, monkeypatch):
     """Measured-cost queues (pagerank.hip calibrate_queues): the first call on a
     schedule records every item's duration and re-deals the queues after its first
     chunk; that call, a later one on the re-dealt queues, and entry-dealt queues
-    (CGX_PR_CALIB=0) give the same bits and iteration counts, for 8K and 16K windows."""
+    (CGX_PR_CALIB=0) give the same bits and iteration counts, for 4K (one queue of
+    tiles, re-sorted longest-first), 8K and 16K windows."""
     s, d, _ = rmat_graph(20, False, True)
     if deal == "global":
         monkeypatch.setenv("CGX_PR_DEAL", "global")
-    for wb in ("13", "14"):
+    for wb in ("12", "13", "14"):
         monkeypatch.setenv("CGX_PR_WIN_BITS", wb)
         out = []
         for calib in ("1", "0"):
