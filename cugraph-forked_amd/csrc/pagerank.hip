@@ -2848,6 +2848,17 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
 
+  // measured-cost queues (calibrate_queues), per rank for its own block: no collective
+  bool calibrating = nblk_push && blk.pp.nunits && calibration_wanted(blk.pp);
+  if (calibrating) {
+    blk.pp.item_ticks.set_stream(s);
+    blk.pp.item_ticks.resize(blk.pp.nitems * sizeof(uint32_t));
+    HIP_CHECK(hipMemsetAsync(blk.pp.item_ticks.data(), 0, blk.pp.nitems * sizeof(uint32_t), s));
+    blk.pp.calib = 1;
+  } else if (blk.pp.calib == 0) {
+    blk.pp.calib = 2;
+  }
+  size_t launched = 0;
   std::vector<hipEvent_t> ev;
   pr_state hst{};
   pr_state* hpin = h.pinned_as<pr_state>();
@@ -2863,6 +2874,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       int const chunk = next_chunk(hst, eps, a.max_iter);
       for (int i = 0; i < chunk; ++i) {
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
+        sp.item_ticks = calibrating && launched++ == 0 ? blk.pp.item_ticks.data<uint32_t>() : nullptr;
         if (nblk_push && blk.pp.nunits)
           hipLaunchKernelGGL(mg_pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
         CGX_LAUNCH_CHECK();
@@ -2880,6 +2892,11 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       HIP_CHECK(hipMemcpyAsync(hpin, st.data(), sizeof(pr_state), hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
       hst = *hpin;
+      if (calibrating) {
+        calibrate_queues(s, blk.pp);
+        for (int q = 0; q <= kQueues; ++q) sp.qoff[q] = blk.pp.qoff[q];
+        calibrating = false;
+      }
       if (hst.done) break;
     }
   }

@@ -116,6 +116,10 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
     if algo == "pagerank":
         v, x = plc.pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
         mine = (v.cpu().numpy(), x.cpu().numpy())
+        # the first call re-dealt this rank's push queues by measured item cost
+        # (pagerank.hip calibrate_queues): a second call on them gives the same bits
+        v2, x2 = plc.pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert np.array_equal(v2.cpu().numpy(), mine[0]) and np.array_equal(x2.cpu().numpy(), mine[1])
     else:
         root = int(np.unique(s)[0])
         src = np.array([root], np.int64) if rank == world - 1 else np.zeros(0, np.int64)
