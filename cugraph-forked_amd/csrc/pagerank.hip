@@ -664,7 +664,11 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
     if (tid == 0)
       __hip_atomic_store(sa.win_left + w, sa.win_items[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
+  if (sa.fuse == 2 && whole) {  // measurement only (CGX_PR_ABLATE_APPLY=1): no apply, wrong ranks
+    for (int i = tid; i < (1 << WB); i += kPushThreads) acc[i] = 0ull;
+  } else {
+    apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
+  }
   unsigned long long const bd = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const bg = block_sum_u64<kPushThreads>(my_dang, s_red);
   if (tid == 0) {
@@ -2430,7 +2434,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.win_bits  = adj.pr.win_bits;
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
-    sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
+    sa.fuse    = fuse_apply(adj.pr) ? (env_is("CGX_PR_ABLATE_APPLY", "1") ? 2 : 1) : 0;
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // measured-cost queues: the first launch on this schedule records item durations
