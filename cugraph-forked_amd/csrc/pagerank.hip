@@ -1919,9 +1919,10 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
     pp.qoff.assign(kQueues + 1, n);
     pp.qoff[0] = 0;
   } else {
-    int64_t const ng = (n + kCalGroup - 1) / kCalGroup;
+    int64_t const G  = std::max<int64_t>(1, env_i64("CGX_PR_CALGROUP", kCalGroup));  // (measurement override)
+    int64_t const ng = (n + G - 1) / G;
     std::vector<uint64_t> gc(ng, 0);
-    for (int64_t i = 0; i < n; ++i) gc[i / kCalGroup] += t[i];
+    for (int64_t i = 0; i < n; ++i) gc[i / G] += t[i];
     std::vector<int64_t> go(ng);
     for (int64_t g = 0; g < ng; ++g) go[g] = g;
     std::stable_sort(go.begin(), go.end(), [&](int64_t a, int64_t b) { return gc[a] > gc[b]; });
@@ -1938,7 +1939,7 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
     for (int q = 0; q < kQueues; ++q) {
       pp.qoff[q] = (int64_t)queue.size();
       for (int64_t g : qg[q])
-        for (int64_t i = g * kCalGroup; i < std::min(n, (g + 1) * kCalGroup); ++i) queue.push_back(i);
+        for (int64_t i = g * G; i < std::min(n, (g + 1) * G); ++i) queue.push_back(i);
     }
     pp.qoff[kQueues] = n;
   }
