@@ -53,8 +53,19 @@ struct bfs_ctr_hdr {
 // That lets the bottom-up probe run on larger grids.
 constexpr int kCtrParts = 16;
 struct bfs_ctr : bfs_ctr_hdr {
-  unsigned long long part[kCtrParts][32];  // [p][0]: vertices, [p][1]: edges
+  unsigned long long part[kCtrParts][32];  // [p][0]: vertices, [p][1]: edges, [p][2]: residual sub-queue length
 };
+
+// The bottom-up probe's misses (rows longer than the probe, no frontier neighbour in
+// it) go to kCtrParts sub-queues, chunk c's to sub-queue c % kCtrParts, each with its
+// length in its own partial counter: one queue with one counter serialised every
+// wave's append at the memory side -- RMAT-24 root 7's first bottom-up level (a
+// frontier of a few vertices, nearly every vertex a miss: ~139K appends) took 579 us
+// in the probe.  Sub-queue p holds at most the 64 vertices of each of its chunks.
+__host__ __device__ __forceinline__ int64_t residual_cap(int64_t nv)
+{
+  return ((((nv + 63) >> 6) + kCtrParts - 1) / kCtrParts) * 64;
+}
 
 // (next_n, next_m) of a block with the partial counters folded in; lanes 0..15 of
 // one wave read the parts, every lane gets the totals; zero: clear the parts
@@ -68,6 +79,7 @@ __device__ __forceinline__ void fold_parts(bfs_ctr* c, bool zero, unsigned long 
     if (zero) {
       c->part[lane][0] = 0ull;
       c->part[lane][1] = 0ull;
+      c->part[lane][2] = 0ull;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -545,6 +557,7 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
   unsigned long long my_n = 0, my_m = 0;
   int64_t const nchunks = (a.nv + 63) >> 6;
   int64_t const stride  = (int64_t)gridDim.x * (kBlock / 64);
+  int64_t const rcap    = residual_cap(a.nv);
   for (int64_t c = blockIdx.x * (int64_t)(kBlock / 64) + (threadIdx.x >> 6); c < nchunks; c += stride) {
     int64_t const v  = (c << 6) + lane;
     bool const in    = v < a.nv;
@@ -605,9 +618,10 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
     if (mm) {
       unsigned long long base = 0;
       int const leader = __ffsll((long long)mm) - 1;
-      if (lane == leader) base = atomicAdd(&a.ctr->qlen[0], (unsigned long long)__popcll(mm));
+      int const sq = (int)(c % kCtrParts);
+      if (lane == leader) base = atomicAdd(&a.ctr->part[sq][2], (unsigned long long)__popcll(mm));
       base = __shfl(base, leader, 64);
-      if (more) res[base + __popcll(mm & ((1ull << lane) - 1ull))] = (V)v;
+      if (more) res[sq * rcap + (int64_t)base + __popcll(mm & ((1ull << lane) - 1ull))] = (V)v;
     }
   }
   flush_counts(a.ctr, my_n, my_m);
@@ -621,11 +635,21 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
   int const tid    = threadIdx.x;
   int const lane   = tid & (w - 1);
   int const gbase  = (tid & 63) & ~(w - 1);
-  int64_t const n  = (int64_t)a.ctr->qlen[0];  // written by k_bu_probe (earlier launch)
-  int64_t const ng = (int64_t)gridDim.x * (kBlock / w);
+  // the probe's sub-queues (written by an earlier launch), concatenated
+  __shared__ unsigned long long s_pre[kCtrParts + 1];
+  if (tid == 0) {
+    s_pre[0] = 0ull;
+    for (int p = 0; p < kCtrParts; ++p) s_pre[p + 1] = s_pre[p] + a.ctr->part[p][2];
+  }
+  __syncthreads();
+  int64_t const n    = (int64_t)s_pre[kCtrParts];
+  int64_t const rcap = residual_cap(a.nv);
+  int64_t const ng   = (int64_t)gridDim.x * (kBlock / w);
   unsigned long long my_n = 0, my_m = 0;
   for (int64_t i = blockIdx.x * (int64_t)(kBlock / w) + tid / w; i < n; i += ng) {
-    V const v     = res[i];
+    int p = 0;
+    while ((unsigned long long)i >= s_pre[p + 1]) ++p;
+    V const v     = res[p * rcap + (i - (int64_t)s_pre[p])];
     E const beg0  = a.off[v];
     E const end   = a.off[v + 1];
     for (E base = beg0 + kProbe; base < end; base += w) {
@@ -786,7 +810,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   dbuf<V> qa[3], qb[3];
   for (int c = 0; c < 3; ++c) {
     qa[c].resize(nv, s);
-    qb[c].resize(nv, s);
+    qb[c].resize(c == 0 ? std::max<int64_t>(nv, kCtrParts * residual_cap(nv)) : nv, s);  // qb[0]: residual sub-queues too
   }
   // ctr2: queue lengths of a bitmap -> queues conversion; ctr3: a speculative level's counters
   // one allocation and one memset for the three counter blocks; k_publish_seq
