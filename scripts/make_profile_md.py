@@ -35,7 +35,11 @@ def live_avg_ns(kernel):
         return None, 0, 0
     med = sorted(d)[len(d) // 2]
     live = [x for x in d if x >= 0.1 * med]
+    live_med[kernel] = sorted(live)[len(live) // 2]
     return sum(live) / len(live), len(live), len(d)
+
+
+live_med = {}
 
 
 push_live, push_n, push_all = live_avg_ns("k_pr_push16_w14" if fused else "k_pr_push16")
@@ -62,6 +66,8 @@ out = [
     (f"- Without the post-convergence no-op launches ({push_all - push_n} of {push_all} push launches under 10 % of "
      f"the median, from `profiles/{tag}_pr_launches.csv`): push {push_ns / 1e3:.1f} µs, apply {app_ns / 1e3:.1f} µs."
      if push_live else "- (no per-launch trace extract: averages include the no-op launches)"),
+    (f"- Median live push launch {live_med.get('k_pr_push16_w14' if fused else 'k_pr_push16', 0) / 1e3:.1f} µs: the average also holds each "
+     "graph's first chunk, which runs before the queues are re-dealt by measured cost." if push_live else ""),
     f"- rocprof push{'' if fused else ' + apply'} = {pa:.1f} µs per iteration{' (apply fused into the push)' if fused else ''}. The bench's HIP events around the launches (gap",
     f"  included) give {ev:.1f} µs; the two agree within {abs(ev - pa) / pa * 100:.1f} %.",
     f"- Algorithmic bytes per iteration: 4E + 16V = {r['algorithmic_bytes_per_launch'] / 1e6:.1f} MB, giving {r['achieved']:.0f} GB/s =",
