@@ -121,20 +121,16 @@ struct pr_push_t {
   buffer seg_base;     // uint32[nunits * 16]: running source before each 512-entry wave segment
   buffer units;        // push_unit[nunits], in (window, source) order
   int64_t nunits = 0;
-  buffer acc;          // u64[ngroups * nacc] fixed-point sums by row, one nacc block per source group;
-                       // windows stored whole by one item are overwritten each iteration, the others
-                       // (win_multi) are cleared by the apply
+  buffer acc;          // u64[nacc] fixed-point sums by row; windows stored whole by one item are
+                       // overwritten each iteration, the others (win_multi) are cleared by the apply
   int64_t nacc = 0;
-  int ngroups = 1;     // source groups (pagerank.hip "source slices"): 1, or 9 when sliced
   buffer items;        // int64[nitems + 1]: first unit of every item (a window or a share of one)
   buffer queue;        // int64[nitems]: item ids of queue 0, 1, ..., 7
   std::vector<int64_t> qoff;  // queue q = queue[qoff[q], qoff[q + 1])
   int64_t nitems = 0;
   int64_t nwin   = 0;
   buffer tile_ctr;     // uint32 queue heads (128 B apart); zero between iterations
-  buffer win_multi;    // uint8[ngroups * nwin]: 1 = (group, window) summed by several items (flushes add),
-                       // 0 = one item stores it
-  int64_t src_head = -1;  // source partition over the XCDs: head size (-1: not partitioned)
+  buffer win_multi;    // uint8[nwin]: 1 = window summed by several items (flushes add), 0 = one item stores it
   // fused apply (pagerank.hip fused_finish): items per window, windows without items
   buffer win_items;       // uint32[nwin]
   buffer win_left;        // uint32[nwin]: win_items between iterations

@@ -477,6 +477,27 @@ extern "C" cugraph_error_code_t cugraph_amd_graph_get_adjacency(const cugraph_re
   });
 }
 
+extern "C" cugraph_error_code_t cugraph_amd_graph_get_out_weight_sums(const cugraph_resource_handle_t* handle,
+                                                                     cugraph_graph_t* graph,
+                                                                     cugraph_type_erased_device_array_t** sums,
+                                                                     cugraph_error_t** error)
+{
+  *error = nullptr;
+  *sums  = nullptr;
+  return guarded(error, [&] {
+    auto& h = *H(handle);
+    auto& g = *G(graph);
+    CGX_EXPECTS(!g.multi_gpu, CUGRAPH_NOT_IMPLEMENTED, "out-weight sums export is single-GPU only");
+    size_t const nv = (size_t)g.num_vertices;
+    void const* src = nv ? out_weight_sums(h, g) : nullptr;
+    auto a          = new device_array_t(nv, g.weight_type, h.stream);
+    if (nv)
+      HIP_CHECK(hipMemcpyAsync(a->buf.data(), src, nv * dtype_size(g.weight_type), hipMemcpyDeviceToDevice, h.stream));
+    HIP_CHECK(hipStreamSynchronize(h.stream));
+    *sums = reinterpret_cast<cugraph_type_erased_device_array_t*>(a);
+  });
+}
+
 // ============================================================== extensions: measurement
 extern "C" void cugraph_amd_set_profiling(cugraph_resource_handle_t* handle, bool_t enable)
 {

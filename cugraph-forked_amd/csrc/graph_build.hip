@@ -154,13 +154,94 @@ __global__ void k_bin_starts(E const* offsets, V const* order, int64_t nv, int64
   out[b] = lo;  // end of bin b (exclusive) == start of bin b+1
 }
 
-template <typename V, typename E, typename W>
-__global__ void k_row_weight_sums(E const* offsets, W const* w, int64_t nv, W* out)
+// ---- per-row weight sums over a CSR (compute_out_weight_sums, pagerank_impl.cuh:158-164)
+// Edge tiles, not rows, are the unit of work, so a hub row (RMAT-24: 406K edges)
+// is spread over ~200 blocks instead of one thread's loop (68.8 ms per call as a
+// thread-per-row kernel).  Tile b = edges [bT, bT + T):
+//  * the rows whose first edge lies in the tile (rows [lbs[b], lbs[b + 1]), found by
+//    one binary search per tile beforehand) are summed from the tile's weights in
+//    LDS, one thread per row, in edge order;
+//  * the row that runs past the tile end leaves its in-tile partial in tail[b], and
+//    the part of a row that started in an earlier tile its partial in head[b];
+//  * k_row_sums_spill then adds, for each such row, tail[first tile] + head[...]
+//    in tile order.
+// fp64 sums in a fixed order: deterministic, rounded once to weight_t.
+constexpr int kRsTile = 2048;  // edges per tile (8 per thread)
+
+template <typename E>
+__global__ void k_row_sum_tile_rows(E const* off, int64_t nv, int64_t ntiles, int64_t* lbs)
 {
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-    double s = 0;
-    for (E e = offsets[v]; e < offsets[v + 1]; ++e) s += (double)w[e];
-    out[v] = static_cast<W>(s);
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b <= ntiles; b += (int64_t)gridDim.x * blockDim.x) {
+    if (b == ntiles) {
+      lbs[b] = nv;
+      continue;
+    }
+    int64_t const x = b * kRsTile;
+    int64_t lo = 0, hi = nv;  // first row with off[row] >= x
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)off[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    lbs[b] = lo;
+  }
+}
+
+template <typename E, typename W>
+__global__ __launch_bounds__(256) void k_row_sums_tiles(E const* off, W const* w, int64_t ne, int64_t const* lbs,
+                                                        W* out, double* head, double* tail)
+{
+  __shared__ double t_w[kRsTile];
+  __shared__ double sm[4];
+  int64_t const b  = blockIdx.x;
+  int64_t const t0 = b * kRsTile;
+  int64_t const t1 = min(ne, t0 + kRsTile);
+  int const n      = (int)(t1 - t0);
+#pragma unroll
+  for (int j = 0; j < kRsTile / 256; ++j) {
+    int const i = j * 256 + threadIdx.x;
+    t_w[i]      = i < n ? (double)w[t0 + i] : 0.0;
+  }
+  __syncthreads();
+  int64_t const r0 = lbs[b], r1 = lbs[b + 1];
+  // head: the edges [t0, first owned row's start) belong to a row that began earlier
+  int64_t const h_end = r0 < r1 ? min((int64_t)off[r0], t1) : t1;
+  double hs = 0.0;
+  for (int i = threadIdx.x; i < (int)(h_end - t0); i += 256) hs += t_w[i];
+  hs = block_sum_256(hs, sm);
+  if (threadIdx.x == 0) head[b] = hs;
+  // rows owned by the tile: complete ones summed here, the last may spill past t1
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+    int64_t const a = (int64_t)off[r], e = (int64_t)off[r + 1];
+    if (e > t1) continue;  // the spill row: block partial below
+    double s = 0.0;
+    for (int64_t k = a; k < e; ++k) s += t_w[k - t0];
+    out[r] = static_cast<W>(s);
+  }
+  double ts = 0.0;
+  bool const spill = r0 < r1 && (int64_t)off[r1] > t1;
+  if (spill) {
+    int64_t const a = (int64_t)off[r1 - 1];
+    for (int i = (int)(a - t0) + threadIdx.x; i < n; i += 256) ts += t_w[i];
+  }
+  ts = block_sum_256(ts, sm);
+  if (threadIdx.x == 0) tail[b] = spill ? ts : 0.0;
+}
+
+// rows that span tiles: tail of their first tile + head of every later tile they reach
+template <typename E, typename W>
+__global__ void k_row_sums_spill(E const* off, int64_t ntiles, int64_t const* lbs, double const* head,
+                                 double const* tail, W* out)
+{
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < ntiles; b += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const r0 = lbs[b], r1 = lbs[b + 1];
+    int64_t const t1 = (b + 1) * kRsTile;
+    if (r0 >= r1 || (int64_t)off[r1] <= t1) continue;
+    int64_t const r  = r1 - 1;
+    int64_t const be = ((int64_t)off[r + 1] - 1) / kRsTile;
+    double s         = tail[b];
+    for (int64_t t = b + 1; t <= be; ++t) s += head[t];
+    out[r] = static_cast<W>(s);
   }
 }
 
@@ -495,8 +576,23 @@ void outw_impl(handle_t& h, graph_t& g)
   if (g.out) {
     E const* off = g.out->offsets.data<E>();
     if (g.weighted) {
-      hipLaunchKernelGGL((k_row_weight_sums<V, E, W>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off,
-                         g.out->weights.data<W>(), nv, out);
+      int64_t const ne     = g.num_edges;
+      int64_t const ntiles = (ne + kRsTile - 1) / kRsTile;
+      if (ntiles == 0) {
+        fill<W>(out, nv, W(0), s);
+      } else {
+        dbuf<int64_t> lbs(ntiles + 1, s);
+        dbuf<double> head(ntiles, s), tail(ntiles, s);
+        hipLaunchKernelGGL((k_row_sum_tile_rows<E>), dim3(grid_for(ntiles + 1, kBlock, 8192)), dim3(kBlock), 0, s, off,
+                           nv, ntiles, lbs.data());
+        CGX_LAUNCH_CHECK();
+        // rows of degree 0 past the last edge belong to no tile's edges: the last tile owns them
+        hipLaunchKernelGGL((k_row_sums_tiles<E, W>), dim3((unsigned)ntiles), dim3(256), 0, s, off,
+                           g.out->weights.data<W>(), ne, lbs.data(), out, head.data(), tail.data());
+        CGX_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_row_sums_spill<E, W>), dim3(grid_for(ntiles, kBlock, 8192)), dim3(kBlock), 0, s, off,
+                           ntiles, lbs.data(), head.data(), tail.data(), out);
+      }
     } else {
       hipLaunchKernelGGL((k_degrees<E, W>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off, nv, out);
     }

@@ -55,10 +55,13 @@ struct pr_state {
 };
 
 // The L1 difference and the dangling mass of an iteration are summed in 64-bit fixed
-// point (scale 2^61; both are at most 2): integer adds, so the totals -- and the
-// next iteration's base, which depends on the dangling mass -- are the same bits
-// however the vertices are split over blocks (the fused push + apply, the separate
-// apply and the pull kernel all agree).
+// point (scale 2^61; both are at most 2 when the out-weights are the graph's own, so
+// the rank mass stays 1): integer adds, so the totals -- and the next iteration's
+// base, which depends on the dangling mass -- are the same bits however the vertices
+// are split over blocks (the fused push + apply and the separate apply agree).  The
+// pull path (user-supplied out-weights, which may understate the graph's and let the
+// mass grow past any fixed range) sums in fp64 instead, per block in a fixed tree and
+// over the blocks in block order: deterministic too.
 constexpr double kSumScale    = 2305843009213693952.0;  // 2^61
 constexpr double kSumScaleInv = 1.0 / 2305843009213693952.0;
 
@@ -81,8 +84,10 @@ struct pr_args {
   int64_t nv_global;  // |V| of the graph (teleport base)
   double* partials;  // per-block (diff, dangling) partials (fixed-point words, see kSumScale)
   pr_state* st;
-  double* mg_sums;  // multi-GPU: (diff, dangling) of this rank, allreduced before k_mg_finish
+  unsigned long long* mg_sums;  // multi-GPU: this rank's (diff, dangling) fixed-point sums, allreduced (u64,
+                                // exact: the totals are SG's bit for bit) before k_mg_finish
   int enc;          // x~ stored as fixed-point words (enc_fixed; single-GPU fp32 packed push only)
+  int fp64;         // (diff, dangling) summed in fp64 (the pull path: user out-weights bound no sum)
 };
 
 // x~ as the push consumes it: the 64-bit fixed-point value RNE(x * 2^62) of an fp32
@@ -143,6 +148,8 @@ inline int next_chunk(pr_state const& st, double eps, int max_iter)
 namespace {
 
 __device__ __forceinline__ unsigned long long sum_fix(double x) { return (unsigned long long)__double2ll_rn(x * kSumScale); }
+__device__ __forceinline__ void acc_add(unsigned long long& s, double x) { s += sum_fix(x); }
+__device__ __forceinline__ void acc_add(double& s, double x) { s += x; }
 
 // sum over an NT-thread block (NT a multiple of 64); result valid in thread 0; sm >= NT / 64 words
 template <int NT>
@@ -211,40 +218,78 @@ __device__ void finish_iteration(pr_args<V, E, R> const& a, unsigned long long m
   d = block_sum_u64<256>(d, sm);
   g = block_sum_u64<256>(g, sm);
   if (threadIdx.x == 0) {
-    double const dd = (double)d * kSumScaleInv, gg = (double)g * kSumScaleInv;
     if (a.mg_sums) {
-      a.mg_sums[0] = dd;
-      a.mg_sums[1] = gg;
+      a.mg_sums[0] = d;
+      a.mg_sums[1] = g;
       a.st->ticket = 0;
     } else {
-      update_state<V, E, R>(a, dd, gg, count_iter);
+      update_state<V, E, R>(a, (double)d * kSumScaleInv, (double)g * kSumScaleInv, count_iter);
     }
   }
+}
+
+// the same in fp64 (pull path, pr_args::fp64): 256-thread blocks
+template <typename V, typename E, typename R>
+__device__ void finish_iteration(pr_args<V, E, R> const& a, double my_diff, double my_dang, bool count_iter)
+{
+  __shared__ double sm[4];
+  __shared__ int s_last;
+  double const bd = block_sum_256(my_diff, sm);
+  double const bg = block_sum_256(my_dang, sm);
+  auto* part = reinterpret_cast<unsigned long long*>(a.partials);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&part[2 * blockIdx.x], (unsigned long long)__double_as_longlong(bd), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&part[2 * blockIdx.x + 1], (unsigned long long)__double_as_longlong(bg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(&a.st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last     = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double d = 0, g = 0;
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+    d += __longlong_as_double((long long)__hip_atomic_load(&part[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    g += __longlong_as_double(
+      (long long)__hip_atomic_load(&part[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  d = block_sum_256(d, sm);
+  g = block_sum_256(g, sm);
+  if (threadIdx.x == 0) update_state<V, E, R>(a, d, g, count_iter);  // (single GPU only)
 }
 
 // multi-GPU: the state update from the allreduced (diff, dangling)
 template <typename V, typename E, typename R>
 __global__ void k_mg_finish(pr_args<V, E, R> a, bool count_iter)
 {
-  if (threadIdx.x == 0 && blockIdx.x == 0) update_state<V, E, R>(a, a.mg_sums[0], a.mg_sums[1], count_iter);
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    update_state<V, E, R>(a, (double)a.mg_sums[0] * kSumScaleInv, (double)a.mg_sums[1] * kSumScaleInv, count_iter);
 }
 
 // init: x~ = pr / outw, dangling mass of the initial vector
-template <typename V, typename E, typename R>
-__global__ __launch_bounds__(256) void k_pr_init(pr_args<V, E, R> a)
+template <typename V, typename E, typename R, typename Acc>
+__device__ __forceinline__ void init_body(pr_args<V, E, R> const& a)
 {
-  unsigned long long dang = 0;
+  Acc dang = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < a.nv; v += (int64_t)gridDim.x * blockDim.x) {
     R p  = a.pr[v];
     R ow = a.outw[v];
     if (ow == R(0)) {
-      dang += sum_fix((double)p);
+      acc_add(dang, (double)p);
       store_x<R>(a.x_out, v, R(0), a.enc);
     } else {
       store_x<R>(a.x_out, v, (R)((double)p / (double)ow), a.enc);
     }
   }
-  finish_iteration<V, E, R>(a, 0ull, dang, false);
+  finish_iteration<V, E, R>(a, Acc(0), dang, false);
+}
+
+template <typename V, typename E, typename R>
+__global__ __launch_bounds__(256) void k_pr_init(pr_args<V, E, R> a)
+{
+  if (a.fp64) init_body<V, E, R, double>(a);
+  else init_body<V, E, R, unsigned long long>(a);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -301,36 +346,26 @@ __device__ __forceinline__ double row_partial_block(pr_args<V, E, R> const& a, E
   return (s0 + s1) + (s2 + s3);
 }
 
-template <typename V, typename E, typename R>
+template <typename V, typename E, typename R, typename Acc = unsigned long long>
 __device__ __forceinline__ void vertex_update_from(pr_args<V, E, R> const& a, V v, double s, R old, R ow, double base,
-                                                   double pf, unsigned long long& my_diff, unsigned long long& my_dang)
+                                                   double pf, Acc& my_diff, Acc& my_dang)
 {
   double n = base + a.alpha * s;
   if (a.pers) n += pf * (double)a.pers[v];
   R nr     = (R)n;
   a.pr[v]  = nr;
-  my_diff += sum_fix(fabs((double)nr - (double)old));
+  acc_add(my_diff, fabs((double)nr - (double)old));
   R xv = R(0);
-  if (ow == R(0)) my_dang += sum_fix((double)nr);
+  if (ow == R(0)) acc_add(my_dang, (double)nr);
   else xv = (R)((double)nr / (double)ow);
   store_x<R>(a.x_out, v, xv, a.enc);
 }
 
-template <typename V, typename E, typename R>
+template <typename V, typename E, typename R, typename Acc = unsigned long long>
 __device__ __forceinline__ void vertex_update(pr_args<V, E, R> const& a, V v, double s, double base, double pf,
-                                              unsigned long long& my_diff, unsigned long long& my_dang)
+                                              Acc& my_diff, Acc& my_dang)
 {
-  R old    = a.pr[v];
-  double n = base + a.alpha * s;
-  if (a.pers) n += pf * (double)a.pers[v];
-  R nr     = (R)n;
-  a.pr[v]  = nr;
-  my_diff += sum_fix(fabs((double)nr - (double)old));
-  R ow = a.outw[v];
-  R xv = R(0);
-  if (ow == R(0)) my_dang += sum_fix((double)nr);
-  else xv = (R)((double)nr / (double)ow);
-  store_x<R>(a.x_out, v, xv, a.enc);
+  vertex_update_from<V, E, R, Acc>(a, v, s, a.pr[v], a.outw[v], base, pf, my_diff, my_dang);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -341,14 +376,14 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
   work_item const it = a.items[blockIdx.x];
   double const base  = a.st->base;
   double const pf    = a.st->pers_factor;
-  unsigned long long my_diff = 0, my_dang = 0;
+  double my_diff = 0, my_dang = 0;  // fp64 (pr_args::fp64)
   int const tid = threadIdx.x;
   if (it.width == 256) {
     for (int64_t p = it.begin; p < it.end; ++p) {
       V v      = a.order ? a.order[p] : (V)p;
       double s = row_partial_block<V, E, R, WEIGHTED>(a, a.off[v], a.off[v + 1], tid);
       s        = block_sum_256(s, sm);
-      if (tid == 0) vertex_update<V, E, R>(a, v, s, base, pf, my_diff, my_dang);
+      if (tid == 0) vertex_update<V, E, R, double>(a, v, s, base, pf, my_diff, my_dang);
     }
   } else {
     int const w      = it.width;
@@ -365,7 +400,7 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
         s = row_partial<V, E, R, WEIGHTED>(a, a.off[v], a.off[v + 1], lane, w);
       }
       for (int o = w >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-      if (valid && lane == 0) vertex_update<V, E, R>(a, v, s, base, pf, my_diff, my_dang);
+      if (valid && lane == 0) vertex_update<V, E, R, double>(a, v, s, base, pf, my_diff, my_dang);
     }
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
@@ -417,8 +452,6 @@ constexpr int kTileUnits   = 8;    // units per tile below 2^22 rows (RMAT-22: 8
 constexpr int kGroupItems  = 128;  // items per group dealt to a queue
 constexpr int kCtrStride   = 32;   // queue heads 128 B apart
 constexpr int kPushBlocks  = 512;  // persistent grid: two 1024-thread blocks per CU, 256 CUs
-constexpr int kSrcBinBits  = 14;   // source-range cut granularity: 16K sources
-constexpr int kMaxSliceRanges = 12;
 // LDS left beside a 16K-window push block's 128 KB of sums (163,840 B per workgroup on
 // gfx950, less the block's other shared words) for the hub x~ (push_body16 HUB)
 constexpr int kHubBytes = 32768 - 512;
@@ -455,14 +488,9 @@ inline bool env_is(char const* name, char const* value)
   return e && std::string(e) == value;
 }
 
-// items per push block on average (a window larger than 1.5 x E / (kPushBlocks x this)
-// is cut into shares); CGX_PR_SHARE_DIV overrides (measurement only)
-inline int64_t item_share_div()
-{
-  char const* e = std::getenv("CGX_PR_SHARE_DIV");
-  int64_t const d = e ? std::atoll(e) : 0;
-  return d > 0 ? d : 4;
-}
+// items per push block on average: a window larger than 1.5 x E / (blocks x this) is
+// cut into shares
+constexpr int64_t kShareDiv = 4;
 
 inline bool packed_enabled()
 {
@@ -492,11 +520,9 @@ struct push_args {
   int64_t nitems;
   unsigned int* tile_ctr;   // queue heads, kCtrStride apart, two sets (iteration parity)
   uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
-                            // its sums), 0 = stored whole; nullptr: clear every sum
+                            // its sums), 0 = stored whole; nullptr: clear every sum (MG)
   int win_bits;
-  int ngroups;     // source groups: the apply sums acc[g * nacc + v] over g (pr_push_t::ngroups)
-  int64_t nacc;    // per group
-  int64_t nwin;    // windows (win_multi is [ngroups][nwin])
+  int64_t nwin;
   // fused apply (single GPU): the block that completes a window applies it
   int fuse;
   int parity;                  // queue-head set of this launch (launch index & 1)
@@ -664,11 +690,7 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
     if (tid == 0)
       __hip_atomic_store(sa.win_left + w, sa.win_items[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (sa.fuse == 2 && whole) {  // measurement only (CGX_PR_ABLATE_APPLY=1): no apply, wrong ranks
-    for (int i = tid; i < (1 << WB); i += kPushThreads) acc[i] = 0ull;
-  } else {
-    apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
-  }
+  apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
   unsigned long long const bd = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const bg = block_sum_u64<kPushThreads>(my_dang, s_red);
   if (tid == 0) {
@@ -873,36 +895,14 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
 // 16-byte load, sources as a running sum plus one wave scan, 6 DPP adds per 8
 // entries instead of 48 -- were 20 % slower: each gather then spans the whole
 // 512-entry segment, and the gathers' cost follows the distinct lines each touches.)
-// inclusive max-scan over the 64 lanes of a wave, N rows interleaved (as wave_incl_scan_rows)
-template <int N>
-__device__ __forceinline__ void wave_max_scan_rows(uint32_t (&v)[N])
-{
-#pragma unroll
-  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x111, 0xf, 0xf, false));
-#pragma unroll
-  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x112, 0xf, 0xf, false));
-#pragma unroll
-  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x114, 0xf, 0xf, false));
-#pragma unroll
-  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x118, 0xf, 0xf, false));
-#pragma unroll
-  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x142, 0xa, 0xf, false));
-#pragma unroll
-  for (int j = 0; j < N; ++j) v[j] = max(v[j], (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[j], 0x143, 0xc, 0xf, false));
-}
-
-// DD (source dedup): only the lanes that start a run of equal sources in their row
-// gather x~ (exec-masked: ~1/4 of the lanes on RMAT); the others take their run
-// head's value with one ds_bpermute when the row is summed.  The texture path is
-// the push's busiest unit (RMAT-24: TA 71 %, TD 80 % busy, mostly stalled on L2),
-// and its work follows the active lanes.
+//
 // HUB (16K windows): the x~ of the first sa.nhub sources (the hubs: ids descend by
 // degree) are staged in the LDS left beside the window, once per launch, and a wave
 // segment whose sources are all hubs reads them there instead of gathering through
 // the texture path -- the push's busiest unit (TA 71 %, TD 80 % busy).  Sources are
 // sorted within a window, so almost every segment is all-hub or hub-free; a segment
 // that straddles the boundary gathers from global memory.
-template <int WB, typename V, typename E, typename R, bool ENC, bool DD, bool HUB = false>
+template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -962,23 +962,12 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     auto entry = [&](u32x4_t const& w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
     // decode a segment's sources (DPP scan of the deltas + the running base) and
     // issue its 8 gathers; jumps and padding read a valid source and are masked when summed
-    // (DD) the run head of every lane, 6 bits per row, rows 0-3 / 4-7 in hp[0] / hp[1]
-    auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows], uint32_t (&hp)[2]) {
+    auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows]) {
       uint32_t sc[kRows];
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const e = entry(w, j);
         sc[j]            = (e >> WB) == kJump ? (e & kLow) : (e >> WB);
-      }
-      if constexpr (DD) {  // four rows at a time (registers)
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          uint32_t hl[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) hl[j] = (sc[4 * g + j] != 0u || lane == 0) ? (uint32_t)lane : 0u;
-          wave_max_scan_rows<4>(hl);
-          hp[g] = hl[0] | (hl[1] << 6) | (hl[2] << 12) | (hl[3] << 18);
-        }
       }
       wave_incl_scan_rows<kRows>(sc);
       uint32_t run = base;
@@ -1002,22 +991,14 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       for (int j = 0; j < kRows; ++j) {
         uint32_t const src = run + sc[j];
         run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-        if constexpr (DD) {
-          if (((hp[j >> 2] >> ((j & 3) * 6)) & 63u) == (uint32_t)lane) xv[j] = x[src];  // run heads only
-        } else {
-          xv[j] = x[src];
-        }
+        xv[j] = x[src];
       }
     };
-    auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows], uint32_t const (&hp)[2]) {
+    auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows]) {
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const e = entry(w, j);
-        xw_t v           = xv[j];
-        if constexpr (DD) {
-          uint32_t const h = (hp[j >> 2] >> ((j & 3) * 6)) & 63u;
-          v = __builtin_bit_cast(xw_t, __builtin_amdgcn_ds_bpermute((int)(h << 2), __builtin_bit_cast(int, v)));
-        }
+        xw_t const v     = xv[j];
         unsigned long long fix;
         if constexpr (ENC) fix = dec_fixed(v);
         else fix = fixed_of(v);
@@ -1029,52 +1010,30 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     // on its gathers: SQ_WAIT_ANY 52 % of the wave cycles, issue 9 %), and the entries
     // of the unit after that are prefetched.
     int64_t const u1 = ua + 1 < ub ? ua + 1 : ua;
-    if constexpr (!DD) {
-      int nA      = seg_n(ua);
-      int nB      = seg_n(u1);
-      uint32_t bB = __builtin_amdgcn_readfirstlane(sa.seg_base[u1 * kSegsPerUnit + wave]);
-      u32x4_t wA  = nt_load(seg_ptr(ua));  // padded: the stream has a unit past its end
-      u32x4_t wB  = nt_load(seg_ptr(u1));
-      xw_t xA[kRows];
-      uint32_t hA[2] = {0u, 0u};
-      if (nA > 0) gather(wA, __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]), xA, hA);
-      for (int64_t un = ua; un < ub; ++un) {
-        bool const actB = un + 1 < ub && nB > 0;  // wave-uniform
-        xw_t xB[kRows];
-        uint32_t hB[2] = {0u, 0u};
-        if (actB) gather(wB, bB, xB, hB);
-        int64_t const u2  = un + 2 < ub ? un + 2 : un;
-        int const n2      = seg_n(u2);
-        uint32_t const b2 = sa.seg_base[u2 * kSegsPerUnit + wave];
-        u32x4_t const e2  = nt_load(seg_ptr(u2));
-        __builtin_amdgcn_sched_barrier(0);  // keep the next gathers and the prefetch ahead of the sums
-        if (nA > 0) sum(wA, xA, hA);
-        wA = wB;
+    int nA      = seg_n(ua);
+    int nB      = seg_n(u1);
+    uint32_t bB = __builtin_amdgcn_readfirstlane(sa.seg_base[u1 * kSegsPerUnit + wave]);
+    u32x4_t wA  = nt_load(seg_ptr(ua));  // padded: the stream has a unit past its end
+    u32x4_t wB  = nt_load(seg_ptr(u1));
+    xw_t xA[kRows];
+    if (nA > 0) gather(wA, __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]), xA);
+    for (int64_t un = ua; un < ub; ++un) {
+      bool const actB = un + 1 < ub && nB > 0;  // wave-uniform
+      xw_t xB[kRows];
+      if (actB) gather(wB, bB, xB);
+      int64_t const u2  = un + 2 < ub ? un + 2 : un;
+      int const n2      = seg_n(u2);
+      uint32_t const b2 = sa.seg_base[u2 * kSegsPerUnit + wave];
+      u32x4_t const e2  = nt_load(seg_ptr(u2));
+      __builtin_amdgcn_sched_barrier(0);  // keep the next gathers and the prefetch ahead of the sums
+      if (nA > 0) sum(wA, xA);
+      wA = wB;
 #pragma unroll
-        for (int j = 0; j < kRows; ++j) xA[j] = xB[j];
-        nA = actB ? nB : 0;
-        wB = e2;
-        nB = n2;
-        bB = __builtin_amdgcn_readfirstlane(b2);
-      }
-    } else {  // (DD needs those registers: one unit at a time, entries one unit ahead)
-      int n         = seg_n(ua);
-      uint32_t base = __builtin_amdgcn_readfirstlane(sa.seg_base[ua * kSegsPerUnit + wave]);
-      u32x4_t w0    = nt_load(seg_ptr(ua));
-      for (int64_t un = ua; un < ub; ++un) {
-        xw_t xv[kRows];
-        uint32_t hp[2] = {0u, 0u};
-        if (n > 0) gather(w0, base, xv, hp);
-        int64_t const u1n = un + 1 < ub ? un + 1 : un;
-        int const n1      = seg_n(u1n);
-        uint32_t const b1 = sa.seg_base[u1n * kSegsPerUnit + wave];
-        u32x4_t const e1  = nt_load(seg_ptr(u1n));
-        __builtin_amdgcn_sched_barrier(0);
-        if (n > 0) sum(w0, xv, hp);
-        w0   = e1;
-        n    = n1;
-        base = __builtin_amdgcn_readfirstlane(b1);
-      }
+      for (int j = 0; j < kRows; ++j) xA[j] = xB[j];
+      nA = actB ? nB : 0;
+      wB = e2;
+      nB = n2;
+      bB = __builtin_amdgcn_readfirstlane(b2);
     }
     end_item<WB, V, E, R>(sa, acc, win);
     // (the item id from LDS too: s_item holds it until thread 0 takes the next)
@@ -1094,17 +1053,17 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   }
 }
 
-template <int WB, typename V, typename E, typename R, bool ENC, bool DD = false>
+template <int WB, typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
 {
-  push_body16<WB, V, E, R, ENC, DD && sizeof(typename std::conditional<ENC, uint32_t, R>::type) == 4>(sa);
+  push_body16<WB, V, E, R, ENC>(sa);
 }
 
 // 16K-destination windows: 128 KB of LDS, one block (16 waves) per CU, no 8-waves bound
 template <typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
 {
-  push_body16<14, V, E, R, ENC, false, true>(sa);
+  push_body16<14, V, E, R, ENC, true>(sa);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -1137,19 +1096,6 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
       old[j] = a.pr[v + j * stride];
       ow[j]  = a.outw[v + j * stride];
     }
-    if (sa.ngroups > 1) {  // sliced sources: one partial sum per group, integer adds (order-free)
-      unsigned long long fg[kApplyBatch];
-      for (int g = 1; g < sa.ngroups; ++g) {
-#pragma unroll
-        for (int j = 0; j < kApplyBatch; ++j) fg[j] = sa.acc[g * sa.nacc + v + j * stride];
-#pragma unroll
-        for (int j = 0; j < kApplyBatch; ++j) {
-          int64_t const vj = v + j * stride;
-          if (fg[j] && sa.win_multi[g * sa.nwin + (vj >> sa.win_bits)]) sa.acc[g * sa.nacc + vj] = 0ull;
-          f[j] += fg[j];
-        }
-      }
-    }
 #pragma unroll
     for (int j = 0; j < kApplyBatch; ++j) {
       int64_t const vj = v + j * stride;
@@ -1159,12 +1105,8 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
     }
   }
   for (; v < a.nv; v += stride) {
-    unsigned long long f = 0;
-    for (int g = 0; g < sa.ngroups; ++g) {
-      unsigned long long const x = sa.acc[g * sa.nacc + v];
-      if (x && (!sa.win_multi || sa.win_multi[g * sa.nwin + (v >> sa.win_bits)])) sa.acc[g * sa.nacc + v] = 0ull;
-      f += x;
-    }
+    unsigned long long const f = sa.acc[v];
+    if (f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
     vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
@@ -1193,43 +1135,6 @@ __global__ void k_push_keys(C const* cols, uint32_t const* rows, int64_t ne, int
     keys[e] = ((uint64_t)(rows[e] >> wb) << 32) | (uint32_t)cols[e];
     vals[e] = (uint32_t)e;
   }
-}
-
-// Source slices (see plan_slices): the key's high word is the virtual window
-// w * nslice + slice(source); slices are source ranges, so (virtual window, source)
-// order is (window, source) order with every window's entries grouped by slice
-struct slice_table {
-  int n;                 // ranges
-  uint32_t lo[kMaxSliceRanges + 1];  // range r = [lo[r], lo[r + 1]) of source ids
-  int sidx[kMaxSliceRanges];
-};
-
-template <typename C>
-__global__ void k_push_keys_sliced(C const* cols, uint32_t const* rows, int64_t ne, int wb, slice_table t, int nslice,
-                                   uint64_t* keys, uint32_t* vals)
-{
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t const c = (uint32_t)cols[e];
-    int r            = 0;
-    while (r + 1 < t.n && c >= t.lo[r + 1]) ++r;
-    uint64_t const vw = (uint64_t)(rows[e] >> wb) * (uint64_t)nslice + (uint64_t)t.sidx[r];
-    keys[e]           = (vw << 32) | c;
-    vals[e]           = (uint32_t)e;
-  }
-}
-
-// entries per 2^kSrcBinBits-source bin (the out-degree histogram of the push)
-template <typename C>
-__global__ void k_src_hist(C const* cols, int64_t ne, int nbins, unsigned long long* cnt)
-{
-  extern __shared__ unsigned int h_bins[];
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) h_bins[b] = 0u;
-  __syncthreads();
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&h_bins[(uint32_t)cols[e] >> kSrcBinBits], 1u);
-  __syncthreads();
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x)
-    if (h_bins[b]) atomicAdd(cnt + b, (unsigned long long)h_bins[b]);
 }
 
 // first position of every window w in [0, nwin] among the sorted keys
@@ -1299,12 +1204,12 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
 // jumps in front of real entry k: its source gap D to the previous entry of the
 // window (0 before the window's first) is coded in the entry when D <= dmax,
 // else by ceil(D / pmax) jumps and an entry of delta 0
-__global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t const* vlo, int nsl,
-                              uint32_t dmax, uint32_t pmax, uint32_t* mj)
+__global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t dmax, uint32_t pmax,
+                              uint32_t* mj)
 {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t const w     = (int64_t)(keys[k] >> 32);
-    uint32_t const prev = k == ws[w] ? vlo[w % nsl] : (uint32_t)keys[k - 1];
+    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
     uint32_t const D    = (uint32_t)keys[k] - prev;
     mj[k]               = D > dmax ? (D + pmax - 1) / pmax : 0u;
   }
@@ -1313,14 +1218,14 @@ __global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* w
 // real entry k at k + cm[k] (cm = inclusive prefix of the jump counts), its jumps
 // right before it
 __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, int64_t ne,
-                         int64_t const* ws, uint32_t const* vlo, int nsl, uint32_t const* mj,
-                         unsigned long long const* cm, unsigned long long const* pb, int wb, uint32_t pmax,
+                         int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
+                         unsigned long long const* pb, int wb, uint32_t pmax,
                          uint16_t* ent16)
 {
   uint32_t const jump = (1u << (16 - wb)) - 1, low = (1u << wb) - 1;
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
     int64_t const w     = (int64_t)(keys[k] >> 32);
-    uint32_t const prev = k == ws[w] ? vlo[w % nsl] : (uint32_t)keys[k - 1];
+    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
     uint32_t const D    = (uint32_t)keys[k] - prev;
     uint32_t const m    = mj[k];
     int64_t const pos   = k + (int64_t)cm[k] + (int64_t)pb[w];
@@ -1386,8 +1291,8 @@ __global__ void k_packed_unit_heads(uint32_t const* flag, uint32_t const* uid, i
 
 // running source before the first entry of every (unit, wave segment)
 __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t const* keys, int64_t ne,
-                            int64_t const* ws, uint32_t const* vlo, int nsl, uint32_t const* mj,
-                            unsigned long long const* cm, unsigned long long const* pb, uint32_t dmax, uint32_t pmax,
+                            int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
+                            unsigned long long const* pb, uint32_t dmax, uint32_t pmax,
                             uint32_t* seg_base)
 {
   int64_t const n = nunits * kSegsPerUnit;
@@ -1406,110 +1311,13 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
       uint32_t const m    = mj[k];
       int64_t const w     = (int64_t)(keys[k] >> 32);
       int64_t const j     = p - (k + (int64_t)cm[k] + (int64_t)pb[w] - m);
-      uint32_t const prev = k == ws[w] ? vlo[w % nsl] : (uint32_t)keys[k - 1];
+      uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
       uint32_t const src  = (uint32_t)keys[k];
       uint32_t const D    = src - prev;
       base = j < (int64_t)m ? prev + pmax * (uint32_t)j : src - (m ? 0u : (D <= dmax ? D : 0u));
     }
     seg_base[i] = base;
   }
-}
-
-// ---- source partition over the XCDs (opt-in, see srcpart_enabled): entries of the 2^16..2^21
-// highest-ranked sources (the head; RMAT: most entries, ~2 MB of x~) are dealt to
-// any XCD, the tail sources are cut into 8 equal id ranges and range k's entries of
-// every window go to XCD k's queue -- each XCD's L2 then holds the head plus 1/8 of
-// the tail's x~ (offline LRU model, RMAT-24 / 8K windows: 12.9M -> 0.4M L2 misses
-// per iteration).
-constexpr int kSrcParts   = kQueues;
-
-// entries per 2^kSrcBinBits-source bin: thread per (window, bin), two binary searches
-__global__ void k_src_bin_counts(uint64_t const* keys, int64_t const* ws, int64_t nwin, int64_t nbins,
-                                 unsigned long long* cnt)
-{
-  int64_t const n = nwin * nbins;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t const w = i / nbins, b = i % nbins;
-    int64_t const a = ws[w], e = ws[w + 1];
-    if (a == e) continue;
-    auto lb = [&](uint64_t key) {
-      int64_t lo = a, hi = e;
-      while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (keys[mid] < key) lo = mid + 1;
-        else hi = mid;
-      }
-      return lo;
-    };
-    uint64_t const wk = (uint64_t)w << 32;
-    int64_t const c   = lb(wk | (uint64_t)((b + 1) << kSrcBinBits)) - lb(wk | (uint64_t)(b << kSrcBinBits));
-    if (c) atomicAdd(cnt + b, (unsigned long long)c);
-  }
-}
-
-// first position (entry stream; packed: the first jump of that entry) of every
-// window's first entry with source >= cut[c]; -1 when that is the window's start or end
-__global__ void k_src_cut_positions(uint64_t const* keys, int64_t const* ws, int64_t nwin, int64_t const* cut, int ncut,
-                                    unsigned long long const* cm, int64_t* pos)
-{
-  int64_t const n = nwin * ncut;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t const w = i / ncut;
-    int64_t const a = ws[w], e = ws[w + 1];
-    uint64_t const key = ((uint64_t)w << 32) | (uint64_t)cut[i % ncut];
-    int64_t lo = a, hi = e;
-    while (lo < hi) {
-      int64_t mid = (lo + hi) >> 1;
-      if (keys[mid] < key) lo = mid + 1;
-      else hi = mid;
-    }
-    pos[i] = (lo == a || lo == e) ? -1 : (cm ? lo + (int64_t)cm[lo - 1] : lo);
-  }
-}
-
-__global__ void k_mark_positions(int64_t const* pos, int64_t n, uint32_t* flag)
-{
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    if (pos[i] >= 0) flag[pos[i]] = 1u;
-}
-
-// Off by default: measured on RMAT-24 it cut the push's FETCH_SIZE from 2.05 to
-// 1.44 GB per launch (L2 hits 11.7M -> 25.5M) but raised WRITE_SIZE from 174 to
-// 320 MB -- every window is flushed by ~9 items instead of ~1, each a near-full
-// 8K-slot set of global 64-bit atomics -- and the iteration went from 0.815 to
-// 0.866 ms (RMAT-22: 0.190 -> 0.313).  CGX_PR_SRCPART=1 turns it on (A/B, tests).
-inline bool srcpart_enabled()
-{
-  char const* e = std::getenv("CGX_PR_SRCPART");
-  return e && e[0] == '1';
-}
-
-// Head size and tail cuts from the per-bin entry counts: the smallest head (2^16 ..
-// 2^21 sources) for which no tail range holds more than 1/8 of the entries, so the
-// head items can level the queues.  Empty: no partition.
-inline std::vector<int64_t> plan_source_cuts(std::vector<unsigned long long> const& bins, int64_t n_cols, int64_t ne)
-{
-  std::vector<int64_t> none;
-  int64_t const nb = (int64_t)bins.size();
-  if (!srcpart_enabled() || n_cols < (int64_t)kSrcParts << (kSrcBinBits + 2)) return none;
-  std::vector<int64_t> pre(nb + 1, 0);
-  for (int64_t b = 0; b < nb; ++b) pre[b + 1] = pre[b] + (int64_t)bins[b];
-  for (int hb = 16; hb <= 21; ++hb) {
-    int64_t const H  = (int64_t)1 << hb;
-    int64_t const h0 = H >> kSrcBinBits;
-    if (h0 + kSrcParts > nb) break;
-    std::vector<int64_t> cut{H};
-    int64_t worst = 0;
-    int64_t prev  = h0;
-    for (int k = 1; k <= kSrcParts; ++k) {
-      int64_t const bk = k == kSrcParts ? nb : h0 + (nb - h0) * k / kSrcParts;
-      worst            = std::max(worst, pre[bk] - pre[prev]);
-      if (k < kSrcParts) cut.push_back(bk << kSrcBinBits);
-      prev = bk;
-    }
-    if (worst * kSrcParts <= ne * 49 / 50) return cut;  // 2 % slack for the head to level
-  }
-  return none;
 }
 
 // Whole items (all of a window's units): kWholeItem on the item's first unit (the
@@ -1519,7 +1327,7 @@ inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std
 {
   int64_t const nunits = (int64_t)hu.size();
   bool const no_whole  = env_is("CGX_PR_WHOLE", "0");  // A/B: every flush adds, the apply clears every sum
-  std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.ngroups * pp.nwin, 1), 0);
+  std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.nwin, 1), 0);
   for (int64_t i = 0; i < nitems; ++i) {
     int64_t const u = item_u[i], last = item_u[i + 1] - 1;
     // the flag may already sit on an earlier item's first unit: compare and index
@@ -1532,8 +1340,8 @@ inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std
     else multi[wu] = 1;
   }
   to_device(units, hu.data(), (size_t)nunits, s);
-  // items per window (fused apply); windows are the real ones only when ngroups == 1
-  if (pp.ngroups == 1) {
+  // items per window (fused apply)
+  {
     std::vector<uint32_t> cnt((size_t)std::max<int64_t>(pp.nwin, 1), 0u);
     for (int64_t i = 0; i < nitems; ++i) {
       int64_t const wu = hu[item_u[i]].win & kWinMask;
@@ -1574,247 +1382,10 @@ inline void upload_items(hipStream_t s, pr_push_t& pp, std::vector<int64_t> cons
   pp.nitems = nitems;
 }
 
-// Source-partitioned items: a unit's part is the number of its window's cut
-// positions at or before it (0 = head, k + 1 = tail range k); an item is a run of a
-// window's units of one part, split in shares of about tg entries.  Tail items go to
-// queue k, head items (in window order) to the least-loaded queue.
-inline void build_items_srcpart(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, int64_t ne,
-                                std::vector<int64_t> const& cutpos, int ncut)
-{
-  auto hu           = to_host(units, nunits, s);
-  int64_t const tg  = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * 4));
-  auto part_of      = [&](int64_t u) {
-    int p = 0;
-    for (int c = 0; c < ncut; ++c) {
-      int64_t const q = cutpos[hu[u].win * ncut + c];
-      if (q >= 0 && q <= hu[u].k0) p = c + 1;
-    }
-    return p;
-  };
-  std::vector<int64_t> item_u, item_e;
-  std::vector<int> item_p;
-  for (int64_t u0 = 0; u0 < nunits;) {
-    int const p0 = part_of(u0);
-    int64_t u1   = u0 + 1;
-    while (u1 < nunits && hu[u1].win == hu[u0].win && part_of(u1) == p0) ++u1;
-    int64_t const size = hu[u1 - 1].k1 - hu[u0].k0;
-    int64_t const n    = std::max<int64_t>(1, (size + tg / 2) / tg);
-    int64_t k          = 0;
-    for (int64_t u = u0; u < u1; ++u) {
-      int64_t const done = hu[u].k0 - hu[u0].k0;
-      if (u == u0 || (k < n && done * n >= k * size)) {
-        item_u.push_back(u);
-        item_e.push_back(0);
-        item_p.push_back(p0);
-        ++k;
-      }
-      item_e.back() += hu[u].k1 - hu[u].k0;
-    }
-    u0 = u1;
-  }
-  int64_t const nitems = (int64_t)item_u.size();
-  item_u.push_back(nunits);
-  std::vector<int> iq(nitems, 0);
-  int64_t load[kQueues] = {};
-  for (int64_t i = 0; i < nitems; ++i)
-    if (item_p[i] > 0) {
-      iq[i] = (item_p[i] - 1) % kQueues;
-      load[iq[i]] += item_e[i];
-    }
-  for (int64_t i = 0; i < nitems; ++i)
-    if (item_p[i] == 0) {
-      int best = 0;
-      for (int q = 1; q < kQueues; ++q)
-        if (load[q] < load[best]) best = q;
-      iq[i] = best;
-      load[best] += item_e[i];
-    }
-  std::vector<int64_t> queue;
-  queue.reserve(nitems);
-  for (int q = 0; q < kQueues; ++q) {
-    pp.qoff[q] = (int64_t)queue.size();
-    for (int64_t i = 0; i < nitems; ++i)
-      if (iq[i] == q) queue.push_back(i);
-  }
-  pp.qoff[kQueues] = (int64_t)queue.size();
-  mark_whole_items(s, pp, units, hu, item_u, nitems);
-  upload_items(s, pp, item_u, queue, nitems);
-}
-
-// ---- source slices (default from 2^21 sources; CGX_PR_SLICE=0/1 overrides)
-// The push moves every x~ line a window needs from beyond the XCD's L2, and those
-// line fills are its bound (profiles/r03_counters.md: 128-B fills at up to 7.3 TB/s;
-// RMAT-24 33.9M (window, line) pairs per iteration, 4.1 GB).  Slicing the sources
-// keeps each XCD's x~ working set in its 4 MB L2:
-//   head  = sources [0, H)        (the hubs, ~1 MB of x~; ~2/3 of the entries)
-//   mid_k = 8 source ranges after the head, k = 0..7, each <= F sources of x~ and
-//           about 1/8 of the mid entries
-//   tail  = the rest              (low degree: few entries, little reuse anyway)
-// Every window's entries are grouped (head, tail, mid_0, ..., mid_7) -- virtual
-// windows w * 10 + slice, each its own run of packed segments -- and summed in
-// 9 groups: group k < 8 = mid_k, group 8 = head + tail.  All group-k items (every
-// window's mid_k entries) are queued on XCD k, so that XCD reads mid_k's x~ lines
-// from its own L2; head + tail items are dealt to level the queues.  Each item
-// stores its LDS window into its group's partial sums (acc block g; shares of a
-// large (window, group) add), and k_pr_apply adds the 9 partials: integer sums, so
-// the ranks are bitwise those of the unsliced push.  Cost: 8 more V-sized u64
-// arrays written by the push and read by the apply.
-struct slice_plan {
-  int nslice  = 1;
-  int ngroups = 1;
-  int nmid    = 0;  // mid slices (groups 0 .. nmid - 1); group nmid = head + tail
-  slice_table t{};
-  std::vector<int> group_of_sidx{0};
-};
-
-inline int64_t env_i64(char const* name, int64_t dflt)
-{
-  char const* e = std::getenv(name);
-  return e ? std::atoll(e) : dflt;
-}
-
-// Off by default: measured RMAT-24 0.974 vs 0.794 ms/iteration, RMAT-22 0.260 vs
-// 0.176 (the x~ misses it removes cost ~0.18 ms of RMAT-24's iteration, less than
-// the 8 extra partial-sum arrays, the per-item flushes and the 9-way apply).
-// CGX_PR_SLICE=1 turns it on (A/B, tests).
-inline bool slices_wanted(int64_t)
-{
-  char const* e = std::getenv("CGX_PR_SLICE");
-  return e && e[0] == '1';
-}
-
-inline slice_plan plan_slices(std::vector<unsigned long long> const& bins, int64_t n_cols)
-{
-  slice_plan P;
-  P.t.n      = 1;
-  P.t.lo[0]  = 0;
-  P.t.lo[1]  = (uint32_t)n_cols;
-  P.t.sidx[0] = 0;
-  int64_t const nb = (int64_t)bins.size();
-  int64_t const H  = env_i64("CGX_PR_SLICE_HEAD", int64_t(1) << 18);     // head sources (1 MB of x~)
-  int64_t const F  = env_i64("CGX_PR_SLICE_SRC", int64_t(640) << 10);    // sources per mid slice (2.5 MB)
-  // mid slices: 8 (one per XCD), or 4 / 2 (each read by 2 / 4 XCDs: fewer partial
-  // sums for the apply to add, less of the source range sliced); CGX_PR_SLICE_MID
-  int64_t const nm = env_i64("CGX_PR_SLICE_MID", kQueues);
-  int const nmid   = (nm == 2 || nm == 4) ? (int)nm : kQueues;
-  int64_t const h0 = H >> kSrcBinBits, fb = std::max<int64_t>(F >> kSrcBinBits, 1);
-  if (h0 + nmid > nb) return P;  // too few sources to slice
-  unsigned long long mid = 0;
-  for (int64_t b = h0; b < nb; ++b) mid += bins[b];
-  unsigned long long const T = (mid + nmid - 1) / nmid;
-  std::vector<int64_t> cut{h0};
-  int64_t b = h0;
-  for (int k = 0; k < nmid; ++k) {
-    int64_t const b0 = b;
-    unsigned long long acc = 0;
-    while (b < nb && (b == b0 || (acc < T && b - b0 < fb))) acc += bins[b++];
-    cut.push_back(b);
-  }
-  // ranges: head -> slice 0, mid_k -> slice 2 + k, tail -> slice 1
-  P.nmid    = nmid;
-  P.nslice  = 2 + nmid;
-  P.ngroups = nmid + 1;
-  P.group_of_sidx.assign(P.nslice, 0);
-  P.group_of_sidx[0] = nmid;
-  P.group_of_sidx[1] = nmid;
-  for (int k = 0; k < nmid; ++k) P.group_of_sidx[2 + k] = k;
-  int n = 0;
-  P.t.lo[n]     = 0;
-  P.t.sidx[n++] = 0;
-  for (int k = 0; k < nmid; ++k) {
-    if (cut[k + 1] == cut[k]) continue;
-    P.t.lo[n]     = (uint32_t)(cut[k] << kSrcBinBits);
-    P.t.sidx[n++] = 2 + k;
-  }
-  if (cut[nmid] < nb) {
-    P.t.lo[n]     = (uint32_t)(cut[nmid] << kSrcBinBits);
-    P.t.sidx[n++] = 1;
-  }
-  P.t.n     = n;
-  P.t.lo[n] = (uint32_t)n_cols;
-  return P;
-}
-
-// Items and queues of a sliced schedule: units carry virtual windows; their flush
-// key becomes group * nwin + window (so flush_window lands in the group's block of
-// acc); an item is a run of units with one flush key (split in shares of ~tg
-// entries); group k < 8 -> queue k, group 8 items dealt in runs to level the queues.
-inline void build_items_sliced(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, slice_plan const& SP)
-{
-  auto hu          = to_host(units, nunits, s);
-  int64_t const nw = pp.nwin;
-  int const S      = SP.nslice;
-  for (auto& u : hu) u.win = (int64_t)SP.group_of_sidx[u.win % S] * nw + u.win / S;
-  int64_t const ne = nunits ? hu[nunits - 1].k1 : 0;
-  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (kPushBlocks * item_share_div()));
-  std::vector<int64_t> item_u, item_e, item_g;
-  for (int64_t u0 = 0; u0 < nunits;) {
-    int64_t u1 = u0;
-    while (u1 < nunits && hu[u1].win == hu[u0].win) ++u1;
-    int64_t const size = hu[u1 - 1].k1 - hu[u0].k0;
-    int64_t const n    = std::max<int64_t>(1, (size + tg / 2) / tg);
-    int64_t k          = 0;
-    for (int64_t u = u0; u < u1; ++u) {
-      int64_t const done = hu[u].k0 - hu[u0].k0;
-      if (u == u0 || (k < n && done * n >= k * size)) {
-        item_u.push_back(u);
-        item_e.push_back(0);
-        item_g.push_back(hu[u0].win / nw);
-        ++k;
-      }
-      item_e.back() += hu[u].k1 - hu[u].k0;
-    }
-    u0 = u1;
-  }
-  int64_t const nitems = (int64_t)item_u.size();
-  item_u.push_back(nunits);
-  std::vector<int> iq(nitems, 0);
-  int64_t load[kQueues] = {};
-  int const per = kQueues / std::max(SP.nmid, 1);  // XCDs per mid slice
-  for (int64_t i = 0; i < nitems; ++i)
-    if (item_g[i] < SP.nmid) {  // mid slice k: XCDs k * per .. k * per + per - 1, windows dealt round robin
-      int64_t const win = hu[item_u[i]].win % nw;
-      iq[i]             = (int)(item_g[i] * per + win % per);
-      load[iq[i]] += item_e[i];
-    }
-  // head + tail items in runs of kGroupItems consecutive ones, largest run first
-  std::vector<int64_t> hi;
-  for (int64_t i = 0; i < nitems; ++i)
-    if (item_g[i] == SP.nmid) hi.push_back(i);
-  int64_t const nruns = ((int64_t)hi.size() + kGroupItems - 1) / kGroupItems;
-  std::vector<int64_t> rsize(nruns, 0), rorder(nruns);
-  for (size_t j = 0; j < hi.size(); ++j) rsize[j / kGroupItems] += item_e[hi[j]];
-  for (int64_t r = 0; r < nruns; ++r) rorder[r] = r;
-  std::stable_sort(rorder.begin(), rorder.end(), [&](int64_t a, int64_t b) { return rsize[a] > rsize[b]; });
-  for (int64_t r : rorder) {
-    int best = 0;
-    for (int q = 1; q < kQueues; ++q)
-      if (load[q] < load[best]) best = q;
-    for (int64_t j = r * kGroupItems; j < std::min<int64_t>((int64_t)hi.size(), (r + 1) * kGroupItems); ++j)
-      iq[hi[j]] = best;
-    load[best] += rsize[r];
-  }
-  std::vector<int64_t> queue;
-  queue.reserve(nitems);
-  for (int q = 0; q < kQueues; ++q) {
-    pp.qoff[q] = (int64_t)queue.size();
-    for (int64_t i = 0; i < nitems; ++i)
-      if (iq[i] == q) queue.push_back(i);
-  }
-  pp.qoff[kQueues] = (int64_t)queue.size();
-  mark_whole_items(s, pp, units, hu, item_u, nitems);
-  upload_items(s, pp, item_u, queue, nitems);
-}
-
 // Items and queues over the units (host logic, once per graph)
-inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, bool xcd_queues_wanted,
-                        std::vector<int64_t> const& cutpos = {}, int ncut = 0)
+inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, bool xcd_queues)
 {
   int64_t const ne = nunits ? to_host(&units[nunits - 1].k1, 1, s)[0] : 0;
-  if (ncut > 0) {
-    build_items_srcpart(s, pp, units, nunits, ne, cutpos, ncut);
-    return;
-  }
   // Items and queues.  From 2^22 rows (8K windows): an item is a window's units,
   // or an equal share of a window of more than 1.5 tg entries; groups of
   // kGroupItems consecutive items are dealt to the 8 queues by longest-processing-
@@ -1822,8 +1393,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   // Below: one queue of tiles of <= 8 units of a window (RMAT-22: the XCD queues
   // measured 0.199 -> 0.216, the last groups' imbalance outweighing the L2 hits).
   auto hu = to_host(units, nunits, s);
-  bool const xcd_queues = xcd_queues_wanted;
-  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (push_blocks(pp.win_bits) * item_share_div()));
+  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (push_blocks(pp.win_bits) * kShareDiv));
   std::vector<int64_t> item_u, item_e;
   for (int64_t u0 = 0; u0 < nunits;) {
     int64_t u1 = u0;
@@ -1847,14 +1417,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   item_u.push_back(nunits);
   std::vector<int64_t> queue;
   queue.reserve(nitems);
-  char const* qmode = std::getenv("CGX_PR_QMODE");  // measurement: "global" / "lpt" single queue
-  if (xcd_queues && qmode && (std::string(qmode) == "global" || std::string(qmode) == "lpt")) {
-    for (int64_t i = 0; i < nitems; ++i) queue.push_back(i);
-    if (std::string(qmode) == "lpt")
-      std::stable_sort(queue.begin(), queue.end(), [&](int64_t a, int64_t b) { return item_e[a] > item_e[b]; });
-    pp.qoff[0] = 0;
-    for (int q = 1; q < kQueues; ++q) pp.qoff[q] = nitems;
-  } else if (xcd_queues) {
+  if (xcd_queues) {
     int64_t const ngroups = (nitems + kGroupItems - 1) / kGroupItems;
     std::vector<int64_t> gsize(ngroups, 0), gorder(ngroups);
     for (int64_t i = 0; i < nitems; ++i) gsize[i / kGroupItems] += item_e[i];
@@ -1901,8 +1464,7 @@ constexpr int kCalGroup = 16;
 
 inline bool calibration_wanted(pr_push_t const& pp)
 {
-  return pp.calib == 0 && pp.nitems > 0 && pp.ngroups == 1 && pp.src_head < 0 &&
-         !env_is("CGX_PR_CALIB", "0") && !std::getenv("CGX_PR_QMODE");
+  return pp.calib == 0 && pp.nitems > 0 && !env_is("CGX_PR_CALIB", "0");
 }
 
 inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
@@ -1919,7 +1481,7 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
     pp.qoff.assign(kQueues + 1, n);
     pp.qoff[0] = 0;
   } else {
-    int64_t const G  = std::max<int64_t>(1, env_i64("CGX_PR_CALGROUP", kCalGroup));  // (measurement override)
+    int64_t const G  = kCalGroup;
     int64_t const ng = (n + G - 1) / G;
     std::vector<uint64_t> gc(ng, 0);
     for (int64_t i = 0; i < n; ++i) gc[i / G] += t[i];
@@ -1953,7 +1515,7 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
 // or one MG 2D block.
 template <typename C, typename R>
 void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
-                         int64_t n_cols, pr_push_t& pp, bool allow_slices = false)
+                         int64_t n_cols, pr_push_t& pp)
 {
   pp.built = true;
   pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
@@ -1964,30 +1526,9 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   pp.win_bits        = wb;
   pp.nwin            = nwin;
   pp.nacc            = nwin << wb;
-  // source slices (single GPU, see plan_slices): virtual windows w * nslice + slice
-  slice_plan SP;
-  if (allow_slices && ne > 0 && (uint64_t)n_cols < (1ull << 32) && slices_wanted(n_cols)) {
-    int const nbins = (int)((n_cols + (int64_t(1) << kSrcBinBits) - 1) >> kSrcBinBits);
-    if (nbins * sizeof(unsigned int) <= 64 * 1024) {  // the histogram lives in LDS
-      dbuf<unsigned long long> bc(nbins, s);
-      fill<unsigned long long>(bc.data(), nbins, 0ull, s);
-      hipLaunchKernelGGL(k_src_hist<C>, dim3(grid_for(ne, kBlock, 2048)), dim3(kBlock), nbins * sizeof(unsigned int),
-                         s, cols, ne, nbins, bc.data());
-      CGX_LAUNCH_CHECK();
-      SP = plan_slices(to_host(bc.data(), nbins, s), n_cols);
-    }
-  }
-  int64_t const nvw = nwin * SP.nslice;  // virtual windows (== nwin unsliced)
-  // a virtual window's first entry is coded relative to its slice's first source
-  std::vector<uint32_t> vlo_h(SP.nslice, 0u);
-  for (int r = 0; r < SP.t.n; ++r) vlo_h[SP.t.sidx[r]] = SP.t.lo[r];
-  dbuf<uint32_t> vlo(SP.nslice, s);
-  to_device(vlo.data(), vlo_h.data(), (size_t)SP.nslice, s);
-  int const nsl = SP.nslice;
-  pp.ngroups        = SP.ngroups;
   pp.acc.set_stream(s);
-  pp.acc.resize(pp.ngroups * pp.nacc * sizeof(unsigned long long));
-  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.ngroups * pp.nacc * sizeof(unsigned long long), s));
+  pp.acc.resize(pp.nacc * sizeof(unsigned long long));
+  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
   pp.tile_ctr.set_stream(s);
   pp.tile_ctr.resize(2 * kQueues * kCtrStride * sizeof(unsigned int));  // two sets: iteration parity
   HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
@@ -2000,51 +1541,16 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   {
     dbuf<uint64_t> keys(ne, s);
     dbuf<uint32_t> vals(ne, s);
-    if (SP.nslice > 1)
-      hipLaunchKernelGGL(k_push_keys_sliced<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne,
-                         wb, SP.t, SP.nslice, keys.data(), vals.data());
-    else
-      hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
-                         keys.data(), vals.data());
+    hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
+                       keys.data(), vals.data());
     CGX_LAUNCH_CHECK();
     radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
-                                         32 + bits_for((unsigned long long)std::max<int64_t>(nvw - 1, 1)), s);
+                                         32 + bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)), s);
   }
-  // from here on the windows are the virtual windows (a unit never mixes slices)
-  dbuf<int64_t> ws(nvw + 1, s);
-  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nvw + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                     nvw, ws.data());
+  dbuf<int64_t> ws(nwin + 1, s);
+  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
+                     nwin, ws.data());
   CGX_LAUNCH_CHECK();
-  // source partition cuts (empty: window items only)
-  std::vector<int64_t> cuts;
-  pp.src_head = -1;
-  {
-    int64_t const nbins = (n_cols + (int64_t(1) << kSrcBinBits) - 1) >> kSrcBinBits;
-    // (32-bit entries only: its cuts would break the packed format's whole segments)
-    if (SP.nslice == 1 && n_cols >= (int64_t)kSrcParts << (kSrcBinBits + 2) && srcpart_enabled() &&
-        (w || !packed_enabled())) {
-      dbuf<unsigned long long> bc(nbins, s);
-      fill<unsigned long long>(bc.data(), nbins, 0ull, s);
-      hipLaunchKernelGGL(k_src_bin_counts, dim3(grid_for(nvw * nbins, kBlock, 16384)), dim3(kBlock), 0, s,
-                         keys_out.data(), ws.data(), nvw, nbins, bc.data());
-      CGX_LAUNCH_CHECK();
-      cuts = plan_source_cuts(to_host(bc.data(), nbins, s), n_cols, ne);
-      if (!cuts.empty()) pp.src_head = cuts[0];
-    }
-  }
-  int const ncut = (int)cuts.size();
-  dbuf<int64_t> cutd(std::max(ncut, 1), s), cutpos(std::max<int64_t>(nvw * ncut, 1), s);
-  if (ncut) to_device(cutd.data(), cuts.data(), ncut, s);
-  auto cut_positions = [&](unsigned long long const* cm, uint32_t* flag) {
-    if (!ncut) return std::vector<int64_t>{};
-    hipLaunchKernelGGL(k_src_cut_positions, dim3(grid_for(nvw * ncut, kBlock, 4096)), dim3(kBlock), 0, s,
-                       keys_out.data(), ws.data(), nvw, cutd.data(), ncut, cm, cutpos.data());
-    CGX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_mark_positions, dim3(grid_for(nvw * ncut, kBlock, 4096)), dim3(kBlock), 0, s, cutpos.data(),
-                       nvw * ncut, flag);
-    CGX_LAUNCH_CHECK();
-    return to_host(cutpos.data(), (size_t)(nvw * ncut), s);
-  };
   pp.packed = false;
   if (!w && packed_enabled()) {  // 16-bit entries unless the jumps would grow the entries by more than half
     uint32_t const dmax = (1u << (16 - wb)) - 2;  // coded deltas 0 .. dmax; dmax + 1 marks a jump
@@ -2052,19 +1558,19 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     dbuf<uint32_t> mj(ne + 1, s);
     dbuf<unsigned long long> ex(ne + 1, s);
     hipLaunchKernelGGL(k_jump_counts, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                       ws.data(), vlo.data(), nsl, dmax, pmax, mj.data());
+                       ws.data(), dmax, pmax, mj.data());
     CGX_LAUNCH_CHECK();
     fill<uint32_t>(mj.data() + ne, 1, 0u, s);
     exclusive_scan<uint32_t, unsigned long long>(mj.data(), ex.data(), ne + 1, s);
     int64_t const total0 = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
     unsigned long long const* cm = ex.data() + 1;  // inclusive prefix
     // windows padded to whole wave segments (k_packed_pads)
-    dbuf<unsigned long long> pad(nvw + 1, s), pb(nvw + 1, s);
-    hipLaunchKernelGGL(k_packed_pads, dim3(grid_for(nvw + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nvw,
+    dbuf<unsigned long long> pad(nwin + 1, s), pb(nwin + 1, s);
+    hipLaunchKernelGGL(k_packed_pads, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nwin,
                        total0, pad.data());
     CGX_LAUNCH_CHECK();
-    exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nvw + 1, s);
-    int64_t const total = total0 + (int64_t)to_host(pb.data() + nvw, 1, s)[0];
+    exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nwin + 1, s);
+    int64_t const total = total0 + (int64_t)to_host(pb.data() + nwin, 1, s)[0];
     if (total <= ne + ne / 2 && (uint64_t)total < (1ull << 32)) {
       uint16_t const pad_code = (uint16_t)(((1u << (16 - wb)) - 1) << wb);  // a jump of 0: no edge
       pp.packed = true;
@@ -2072,38 +1578,36 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // + a unit: the kernel prefetches whole units
       fill<uint16_t>(pp.ent16.data<uint16_t>(), (size_t)(total + kPushUnit), pad_code, s);
       hipLaunchKernelGGL(k_pack16, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(),
-                         vals_out.data(), rows, ne, ws.data(), vlo.data(), nsl, mj.data(), cm, pb.data(), wb, pmax,
+                         vals_out.data(), rows, ne, ws.data(), mj.data(), cm, pb.data(), wb, pmax,
                          pp.ent16.data<uint16_t>());
       CGX_LAUNCH_CHECK();
-      dbuf<int64_t> nws(nvw + 1, s);
-      hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nvw + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
-                         cm, pb.data(), nvw, total0, nws.data());
+      dbuf<int64_t> nws(nwin + 1, s);
+      hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
+                         cm, pb.data(), nwin, total0, nws.data());
       dbuf<uint32_t> pflag(total + 1, s), puid(total + 1, s);
       fill<uint32_t>(pflag.data(), (size_t)(total + 1), 0u, s);
-      hipLaunchKernelGGL(k_packed_unit_marks, dim3(grid_for(nvw, 64, 4096)), dim3(64), 0, s, nws.data(), nvw,
+      hipLaunchKernelGGL(k_packed_unit_marks, dim3(grid_for(nwin, 64, 4096)), dim3(64), 0, s, nws.data(), nwin,
                          pflag.data());
       CGX_LAUNCH_CHECK();
-      std::vector<int64_t> const cp;  // no source partition with packed entries
       exclusive_scan<uint32_t, uint32_t>(pflag.data(), puid.data(), total + 1, s);
       int64_t const nunits = (int64_t)to_host(puid.data() + total, 1, s)[0];
       pp.units.set_stream(s);
       pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
       push_unit* units = pp.units.data<push_unit>();
       hipLaunchKernelGGL(k_packed_unit_heads, dim3(grid_for(total, kBlock, 16384)), dim3(kBlock), 0, s, pflag.data(),
-                         puid.data(), total, nws.data(), nvw, units);
+                         puid.data(), total, nws.data(), nwin, units);
       CGX_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, total);
       CGX_LAUNCH_CHECK();
       pp.seg_base.set_stream(s);
       pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
       hipLaunchKernelGGL(k_seg_bases, dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0, s, units,
-                         nunits, keys_out.data(), ne, ws.data(), vlo.data(), nsl, mj.data(), cm, pb.data(), dmax,
-                         pmax, pp.seg_base.data<uint32_t>());
+                         nunits, keys_out.data(), ne, ws.data(), mj.data(), cm, pb.data(), dmax, pmax,
+                         pp.seg_base.data<uint32_t>());
       CGX_LAUNCH_CHECK();
       pp.ent.release();
       pp.ew.release();
-      if (SP.nslice > 1) build_items_sliced(s, pp, units, nunits, SP);
-      else build_items(s, pp, units, nunits, wb >= 13, cp, ncut);
+      build_items(s, pp, units, nunits, wb >= 13);
       pp.nunits = nunits;
       HIP_CHECK(hipStreamSynchronize(s));
       return;
@@ -2113,7 +1617,6 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
   hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
                      ws.data(), sb, flag.data());
   CGX_LAUNCH_CHECK();
-  auto const cp = cut_positions(nullptr, flag.data());
   fill<uint32_t>(flag.data() + ne, 1, 0u, s);
   exclusive_scan<uint32_t, uint32_t>(flag.data(), uid.data(), ne + 1, s);
   int64_t const nunits = (int64_t)to_host(uid.data() + ne, 1, s)[0];
@@ -2139,8 +1642,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
                      w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
-  if (SP.nslice > 1) build_items_sliced(s, pp, units, nunits, SP);
-  else build_items(s, pp, units, nunits, wb >= 13, cp, ncut);
+  build_items(s, pp, units, nunits, wb >= 13);
   pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -2191,7 +1693,7 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_
                        nv, ne, rows.data());
   CGX_LAUNCH_CHECK();
   build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), use_weights ? adj.weights.data<R>() : nullptr, ne,
-                            nv, nv, adj.pr, /*allow_slices=*/true);
+                            nv, nv, adj.pr);
 }
 
 template <typename V, typename R>
@@ -2244,8 +1746,6 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.nitems   = pp.nitems;
   for (int q = 0; q <= kQueues; ++q) sa.qoff[q] = q < (int)pp.qoff.size() ? pp.qoff[q] : 0;
   sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
-  sa.ngroups  = pp.ngroups;
-  sa.nacc     = pp.nacc;
   sa.nwin     = pp.nwin;
   HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
   sa.fuse   = 0;  // the caller opts in (fuse_apply)
@@ -2266,15 +1766,8 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 // keeps the separate k_pr_apply (A/B)
 inline bool fuse_apply(pr_push_t const& pp)
 {
-  return pp.win_bits >= 14 && pp.ngroups == 1 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
+  return pp.win_bits >= 14 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
          !env_is("CGX_PR_FUSE", "0");
-}
-
-// source dedup in the packed push (push_body16 DD); CGX_PR_DEDUP=0/1 (A/B)
-inline bool dedup_enabled()
-{
-  char const* e = std::getenv("CGX_PR_DEDUP");
-  return e && e[0] == '1';
 }
 
 // the push kernel for the schedule's window bits and entry format
@@ -2286,10 +1779,6 @@ auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
     return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
   }
   if (pp.packed) {
-    if (dedup_enabled()) {
-      if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true, true> : k_pr_push16<12, V, E, R, true, true>;
-      return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false, true> : k_pr_push16<12, V, E, R, false, true>;
-    }
     if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true> : k_pr_push16<12, V, E, R, true>;
     return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false> : k_pr_push16<12, V, E, R, false>;
   }
@@ -2420,7 +1909,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj, push_w);
   push = push && adj.pr.ok;
   // fp32 packed push: x~ as enc_fixed words (CGX_PR_ENC=0: plain floats, A/B)
-  a.enc = push && adj.pr.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
+  a.enc  = push && adj.pr.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
+  a.fp64 = push ? 0 : 1;
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
 
@@ -2435,7 +1925,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     sa.win_bits  = adj.pr.win_bits;
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
-    sa.fuse    = fuse_apply(adj.pr) ? (env_is("CGX_PR_ABLATE_APPLY", "1") ? 2 : 1) : 0;
+    sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // measured-cost queues: the first launch on this schedule records item durations
@@ -2586,7 +2076,8 @@ template <typename V, typename E, typename R>
 __global__ void k_mg_finish_guarded(pr_args<V, E, R> a, bool count_iter)
 {
   // after convergence the (stale) sums are allreduced again: never touch a finished state
-  if (threadIdx.x == 0 && blockIdx.x == 0 && !a.st->done) update_state<V, E, R>(a, a.mg_sums[0], a.mg_sums[1], count_iter);
+  if (threadIdx.x == 0 && blockIdx.x == 0 && !a.st->done)
+    update_state<V, E, R>(a, (double)a.mg_sums[0] * kSumScaleInv, (double)a.mg_sums[1] * kSumScaleInv, count_iter);
 }
 
 template <typename V, typename E, typename R>
@@ -2814,7 +2305,8 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   fill<R>(x_send.data(), std::max<int64_t>(blk.nmax_row, 1), R(0), s);
   dbuf<unsigned long long> acc_own(std::max<int64_t>(blk.nmax_col, 1), s);
   fill<unsigned long long>(acc_own.data(), std::max<int64_t>(blk.nmax_col, 1), 0ull, s);
-  dbuf<double> partials(2 * 4096, s), sums(2, s);
+  dbuf<double> partials(2 * 4096, s);
+  dbuf<unsigned long long> sums(2, s);
   dbuf<pr_state> st(1, s);
   HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(pr_state), s));
 
@@ -2835,7 +2327,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   int const nblk_init = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 1024);
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
-  ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
+  ctx.world->allreduce<unsigned long long>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
   hipLaunchKernelGGL((k_mg_finish<V, E, R>), dim3(1), dim3(64), 0, s, a, false);
   CGX_LAUNCH_CHECK();
   if (max_iter == 0) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
@@ -2889,7 +2381,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
         }
         hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
         CGX_LAUNCH_CHECK();
-        ctx.world->allreduce<double>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
+        ctx.world->allreduce<unsigned long long>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
         hipLaunchKernelGGL((k_mg_finish_guarded<V, E, R>), dim3(1), dim3(64), 0, s, a, true);
         CGX_LAUNCH_CHECK();
       }

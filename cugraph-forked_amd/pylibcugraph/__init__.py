@@ -126,6 +126,13 @@ class _GPUGraph:
                DeviceArray(w.value).to_tensor(h) if w.value else None)
         return out
 
+    def out_weight_sums(self, resource_handle):
+        """Per-vertex out-weight sums in internal order (weight dtype; out-degrees when
+        unweighted), as PageRank computes them (MI355X build extension)."""
+        a = ctypes.c_void_p()
+        _lib.call("cugraph_amd_graph_get_out_weight_sums", resource_handle.ptr, self.c_graph_ptr, ctypes.byref(a))
+        return DeviceArray(a.value).to_tensor(resource_handle.ptr)
+
 
 def _check_bool(name, v):
     if not isinstance(v, (int, bool)):

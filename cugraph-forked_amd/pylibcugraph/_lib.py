@@ -131,6 +131,7 @@ _proto("cugraph_amd_graph_get_number_of_vertices", ctypes.c_int64, P)
 _proto("cugraph_amd_graph_get_number_of_edges", ctypes.c_int64, P)
 _proto("cugraph_amd_graph_is_symmetric", c_int, P)
 _proto("cugraph_amd_graph_get_adjacency", c_int, P, P, c_int, PP, PP, PP, PP)
+_proto("cugraph_amd_graph_get_out_weight_sums", c_int, P, P, PP, PP)
 _proto("cugraph_amd_device_array_views_copy", c_int, P, c_size_t, P, P, PP)
 _proto("cugraph_amd_set_profiling", None, P, c_int)
 _proto("cugraph_amd_last_iterations", c_size_t, P)

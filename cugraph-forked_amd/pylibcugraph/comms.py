@@ -115,10 +115,26 @@ def init_rccl(row_comm_size=None):
     return MGContext(ctx.value, C)
 
 
-class _TorchComm:
-    """Collectives of one torch.distributed group over buffers handed in by libcugraph_c."""
+_OP_TAGS = {"allreduce": 1, "allgather": 2, "reduce_scatter": 3, "alltoallv": 4}
 
-    def __init__(self, group, memory):
+
+class CollectiveMismatch(RuntimeError):
+    """Ranks of one group entered different collectives (or the same one with other
+    arguments) at the same call number."""
+
+
+class _TorchComm:
+    """Collectives of one torch.distributed group over buffers handed in by libcugraph_c.
+
+    Every call first checks, on every rank of the group, that all ranks are at the same
+    call number of this group and in the same operation with the same element type,
+    reduction and (except for alltoallv) element count: one all_gather of 5 int64.  A
+    rank that skipped or reordered a collective then fails with CollectiveMismatch
+    naming every rank's call, instead of pairing its buffers with another operation's
+    (gloo would hang or mix data).  This adapter is the multi-rank rehearsal path; the
+    RCCL context does not pay for the check."""
+
+    def __init__(self, group, memory, check=True):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -130,6 +146,25 @@ class _TorchComm:
         self._ops = {CGX_COMM_SUM: dist.ReduceOp.SUM, CGX_COMM_MIN: dist.ReduceOp.MIN,
                      CGX_COMM_MAX: dist.ReduceOp.MAX}
         self._streams = {}
+        self.check = check
+        self.seq = 0  # calls made on this group
+
+    def _check(self, name, count, dt, op=-1):
+        """The per-call agreement check (class doc)."""
+        self.seq += 1
+        if not self.check or self.size == 1:
+            return
+        torch = self.torch
+        dev = "cpu" if self.stage else "cuda"
+        mine = torch.tensor([self.seq, _OP_TAGS[name], int(count), int(dt), int(op)], dtype=torch.int64, device=dev)
+        rows = [torch.empty_like(mine) for _ in range(self.size)]
+        self.dist.all_gather(rows, mine, group=self.group)
+        got = [r.cpu().tolist() for r in rows]
+        if any(g != got[0] for g in got):
+            names = {v: k for k, v in _OP_TAGS.items()}
+            desc = ", ".join(f"rank {q}: call {g[0]} {names.get(g[1], g[1])}(count={g[2]}, dtype={g[3]}, op={g[4]})"
+                             for q, g in enumerate(got))
+            raise CollectiveMismatch(f"collective mismatch in a group of {self.size}: {desc}")
 
     # -- buffers
     def _view(self, ptr, count, dt):
@@ -191,6 +226,7 @@ class _TorchComm:
     # calls them with its stream's work enqueued, so that stream is drained first.
     def allreduce(self, _ctx, send, recv, count, dt, op, stream):
         try:
+            self._check("allreduce", count, dt, op)
             st = self._stream(stream)
             self._sync(st)
             t = self._in(self._view(send, count, dt), st)
@@ -204,6 +240,7 @@ class _TorchComm:
 
     def allgather(self, _ctx, send, recv, count, dt, stream):
         try:
+            self._check("allgather", count, dt)
             st = self._stream(stream)
             self._sync(st)
             t = self._in(self._view(send, count, dt), st)
@@ -217,6 +254,7 @@ class _TorchComm:
 
     def reduce_scatter(self, _ctx, send, recv, recvcount, dt, op, stream):
         try:
+            self._check("reduce_scatter", recvcount, dt, op)
             st = self._stream(stream)
             self._sync(st)
             t = self._in(self._view(send, recvcount * self.size, dt), st)
@@ -231,6 +269,7 @@ class _TorchComm:
 
     def alltoallv(self, _ctx, send, sc, sd, recv, rc, rd, dt, stream):
         try:
+            self._check("alltoallv", -1, dt)  # (counts differ per rank by design)
             st = self._stream(stream)
             self._sync(st)
             P = self.size

@@ -79,6 +79,17 @@ cugraph_error_code_t cugraph_amd_graph_get_adjacency(const cugraph_resource_hand
                                                      cugraph_error_t** error);
 
 /*
+ * Copy the graph's per-vertex out-weight sums (weight_t[V], internal order; the
+ * out-degree for unweighted graphs) -- compute_out_weight_sums of
+ * pagerank_impl.cuh:158-164, as PageRank computes and caches them -- to a new
+ * device array (for tests).
+ */
+cugraph_error_code_t cugraph_amd_graph_get_out_weight_sums(const cugraph_resource_handle_t* handle,
+                                                           cugraph_graph_t* graph,
+                                                           cugraph_type_erased_device_array_t** sums,
+                                                           cugraph_error_t** error);
+
+/*
  * Copy n device array views (dst[i] <- src[i], same type and size) with one
  * stream synchronize at the end: the batched form of
  * cugraph_type_erased_device_array_view_copy (array.h) for result extraction.

@@ -1,4 +1,5 @@
-"""ctypes loader for the compiled CPU restatement (oracle/cpu_baseline.c).
+"""ctypes loader for the compiled CPU restatements (oracle/cpu_baseline.c,
+oracle/cpu_louvain.c).
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): bench.py's cpu_baseline leg
 times it as the secondary CPU baseline of SURVEY.md §8d.  Built by
@@ -29,6 +30,8 @@ def lib():
                                           ctypes.c_int, P]
         _lib.cpu_bfs.restype = ctypes.c_double
         _lib.cpu_bfs.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int, P, P]
+        _lib.cpu_louvain.restype = ctypes.c_int
+        _lib.cpu_louvain.argtypes = [ctypes.c_int64, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_int, P, P, P]
     return _lib
 
 
@@ -76,3 +79,20 @@ def pagerank_f64(offsets, indices, alpha=0.85, epsilon=1e-6, max_iterations=500,
     if it == -1:
         raise RuntimeError("PageRank failed to converge.")
     return pr, it
+
+
+def louvain(offsets, indices, weights, max_level=100, resolution=1.0, threads=0):
+    """The oracle Louvain (oracle/louvain.py semantics) on a CSR in internal ids,
+    compiled with OpenMP.  Returns (clustering int64[V], modularity, levels)."""
+    off = np.ascontiguousarray(offsets, dtype=np.int64)
+    idx = np.ascontiguousarray(indices, dtype=np.int32)
+    w = np.ascontiguousarray(weights, dtype=np.float64)
+    nv = off.size - 1
+    c = np.empty(max(nv, 1), dtype=np.int64)
+    q = ctypes.c_double(0.0)
+    lv = ctypes.c_int(0)
+    rc = lib().cpu_louvain(nv, _p(off), _p(idx), _p(w), int(max_level), float(resolution), int(threads), _p(c),
+                           ctypes.byref(q), ctypes.byref(lv))
+    if rc == -2:
+        raise MemoryError("cpu_louvain allocation failed")
+    return c[:nv], q.value, lv.value

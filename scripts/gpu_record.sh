@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-3 record: pytest -m gpu, the default bench line, a rocprofv3 kernel-trace +
+# Round record: pytest -m gpu, the default bench line, a rocprofv3 kernel-trace +
 # stats profile of the bench (kernel stats + the PageRank launches' durations, so the
 # summary can drop the post-convergence no-op launches), each step under its own limit.
-# usage: TAG=r03e bash scripts/gpu_round3.sh [skip-tests]
+# usage: TAG=r04a bash scripts/gpu_record.sh [skip-tests]
 set -o pipefail
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 if [ "${1:-}" != "skip-tests" ]; then

@@ -1,11 +1,13 @@
-"""The compiled CPU restatement (oracle/cpu_baseline.c, bench.py's secondary CPU
-baseline) agrees with the numpy oracle: PageRank iterates converge to the
-oracle's ranks and BFS distances are exact, single-threaded and with OpenMP."""
+"""The compiled CPU restatements (oracle/cpu_baseline.c, bench.py's secondary CPU
+baseline, and oracle/cpu_louvain.c) agree with the numpy oracle: PageRank iterates
+converge to the oracle's ranks, BFS distances are exact, single-threaded and with
+OpenMP, and Louvain gives the oracle's clustering, modularity and levels."""
 import numpy as np
 import pytest
 
 from conftest import dataset_path
 from oracle import bfs as obfs
+from oracle import louvain as olv
 from oracle import graph as og
 from oracle import pagerank as opr
 from oracle import rmat
@@ -56,3 +58,31 @@ def test_pagerank_f64_equals_numpy_oracle():
     pr, it = cpu.pagerank_f64(g.offsets, g.indices, 0.85, 1e-6, 500, threads=4)
     assert it == it_ref
     assert np.max(np.abs(pr - ref) / ref) < 1e-12
+
+
+@pytest.mark.parametrize("case", ["karate", "rmat10_int", "rmat12_int", "rmat12_frac", "rmat11_int_selfloops"])
+@pytest.mark.parametrize("threads", [1, 4])
+def test_louvain_matches_oracle(case, threads):
+    """Integer weights: every sum is exact, so clustering, Q and level count are the
+    numpy oracle's bit for bit; fractional weights: sums in another order, Q within
+    1e-12 relative."""
+    if case == "karate":
+        s, d, w = og.read_csv(dataset_path("karate.csv"))
+        s, d, w = og.symmetrize_dedup(s, d, np.asarray(w, np.float64))
+    else:
+        scale = int(case[4:6])
+        s, d = rmat.rmat(scale, 16 << scale, seed=7)
+        w = rmat.rmat_weights(s.size, seed=8).astype(np.float64)
+        if "int" in case:
+            w = np.floor(w * 8.0) + 1.0
+        s, d, w = og.symmetrize_dedup(s, d, w)
+        if "selfloops" not in case:
+            keep = s != d
+            s, d, w = s[keep], d[keep], w[keep]
+    G = og.create_graph(s, d, w, renumber=True)
+    oc, oq, olevels = olv.louvain(G.num_vertices, *G.coo())
+    c, q, levels = cpu.louvain(G.offsets, G.indices, G.weights, threads=threads)
+    if case == "rmat12_frac":
+        assert abs(q - oq) <= 1e-12 * abs(oq)
+    else:
+        assert np.array_equal(c, oc) and q == oq and levels == olevels

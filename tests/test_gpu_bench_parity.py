@@ -8,7 +8,9 @@
   external id (create_graph_from_edgelist_impl.cuh:557-776,
   renumber_edgelist_impl.cuh:384-390, symmetrize.py:78-93); rows are strictly
   increasing (sorted, no multi-edges).
-* PageRank on RMAT-22 (configs[1]) and RMAT-24 (the headline): the HIP path
+* PageRank on RMAT-22 (configs[1]), RMAT-24 (the headline) and RMAT-26 (the graph
+  of configs[3], here on one GPU: V 32.8M, E 2.10G, the packed format's largest
+  jump overhead and edge counts within 2.3 % of INT32_MAX): the HIP path
   against the fp64 oracle (oracle/cpu_baseline.c cpu_pagerank_f64 -- the numpy
   oracle's arithmetic compiled with OpenMP, checked against it in
   tests/test_cpu_baseline.py) at 1e-6 relative per vertex, same iteration count
@@ -94,6 +96,13 @@ def rmat24():
     b.close()
 
 
+@pytest.fixture(scope="module")
+def rmat26():
+    b = _Bench(26)
+    yield b
+    b.close()
+
+
 def _check_structure(b, transposed):
     """The library's adjacency against an independent torch rebuild of the
     symmetrised, de-duplicated edge set of the same generator output."""
@@ -161,7 +170,7 @@ def _pagerank_vs_oracle(b, g, weighted):
     assert abs(got.sum() - 1.0) < 1e-4
 
 
-@pytest.mark.parametrize("scale", [22, 24])
+@pytest.mark.parametrize("scale", [22, 24, 26])
 def test_pagerank_bench_graph_vs_fp64_oracle(scale, request):
     b = request.getfixturevalue(f"rmat{scale}")
     _pagerank_vs_oracle(b, b.g, False)
@@ -239,38 +248,62 @@ def test_bfs_rmat24_all_bench_roots(rmat24):
     torch.cuda.synchronize()
 
 
-def test_louvain_bench_graph_modularity():
-    """Louvain on the bench graph (RMAT-23, fp32 [0,1) weights, bench.py louvain_leg):
-    the reported Q is the modularity of the returned partition, recomputed on the
-    device in fp64 from the library's own adjacency (compute_modularity,
-    common_methods.cuh:121-170): internal weight / m - sum_c a_c^2 / m^2."""
+def _louvain_q_recomputed(scale):
+    """Louvain on a bench graph (symmetric R-MAT, fp32 [0,1) weights, bench.py
+    louvain_leg): the reported Q is the modularity of the returned partition,
+    recomputed on the device in fp64 from the library's own adjacency
+    (compute_modularity, common_methods.cuh:121-170): internal weight / m -
+    sum_c a_c^2 / m^2, over edge chunks."""
     import torch
     bench, p = _bench()
     h = p.ResourceHandle()
-    g, _, _ = bench.build_rmat_graph(p, h, 23, weighted=True, transposed=False)
+    g, _, _ = bench.build_rmat_graph(p, h, scale, weighted=True, transposed=False)
     v, c, q = p.louvain(h, g, 100, 1.0, False)
+    levels = h.last_louvain_levels()
+    del v
     off, idx, w = g.adjacency(h, transposed=False)
+    g = None
     V = off.numel() - 1
     c = c.to(torch.int64)
-    deg = (off[1:] - off[:-1]).to(torch.int64)
-    rows = torch.repeat_interleave(torch.arange(V, device=off.device), deg)
-    w64 = w.to(torch.float64)
-    m = w64.sum()
-    internal = torch.where(c[rows] == c[idx.to(torch.int64)], w64, torch.zeros_like(w64)).sum()
-    # row sums from a prefix sum (an index_add_ of 259M fp64 atomics onto the hub rows
-    # took ~2 minutes)
-    cs = torch.cat([torch.zeros(1, dtype=torch.float64, device=off.device), torch.cumsum(w64, 0)])
     off64 = off.to(torch.int64)
-    k = cs[off64[1:]] - cs[off64[:-1]]
-    a = torch.zeros(int(c.max()) + 1, dtype=torch.float64, device=off.device).index_add_(0, c, k)
+    del off
+    E = idx.numel()
+    internal = torch.zeros((), dtype=torch.float64, device=idx.device)
+    chunk = 1 << 28
+    for lo in range(0, E, chunk):
+        hi = min(E, lo + chunk)
+        # rows of edges [lo, hi): searchsorted on the offsets (no E-sized row array)
+        rows = torch.searchsorted(off64, torch.arange(lo, hi, device=idx.device, dtype=torch.int64), right=True) - 1
+        wc = w[lo:hi].to(torch.float64)
+        internal += torch.where(c[rows] == c[idx[lo:hi].to(torch.int64)], wc, torch.zeros_like(wc)).sum()
+        del rows, wc
+    # vertex weights k from a prefix sum of 2^32 fixed-point weights (exact integer
+    # differences; an index_add_ of E fp64 atomics onto the hub rows took minutes and a
+    # fp64 prefix sum loses the small rows' bits to cancellation)
+    wf = torch.round(w.to(torch.float64) * 2.0**32).to(torch.int64)
+    cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=idx.device), torch.cumsum(wf, 0)])
+    del wf
+    k = (cs[off64[1:]] - cs[off64[:-1]]).to(torch.float64) * 2.0**-32
+    m = cs[-1].to(torch.float64) * 2.0**-32
+    del cs
+    a = torch.zeros(int(c.max()) + 1, dtype=torch.float64, device=idx.device).index_add_(0, c, k)
     Q = float(internal / m - (a * a).sum() / (m * m))
-    print(f"RMAT-23 Louvain: Q reported {q:.12f} recomputed {Q:.12f}, levels {h.last_louvain_levels()}, "
+    print(f"RMAT-{scale} Louvain: V={V} E={E} Q reported {q:.12f} recomputed {Q:.12f}, levels {levels}, "
           f"clusters {int(torch.unique(c).numel())}")
-    assert abs(Q - q) <= 1e-9 * abs(q)
-    assert q > 0.05
-    del g, off, idx, w, rows, w64
+    del off64, idx, w, c, k, a
     torch.cuda.synchronize()
     p.trim_device_cache()
+    torch.cuda.empty_cache()
+    return q, Q
+
+
+@pytest.mark.parametrize("scale", [23, 26])
+def test_louvain_bench_graph_modularity(scale):
+    """RMAT-23 (bench.py's N=1 Louvain leg) and RMAT-26 (the graph of configs[4], here
+    on one GPU): reported Q == recomputed Q to 1e-9 relative."""
+    q, Q = _louvain_q_recomputed(scale)
+    assert abs(Q - q) <= 1e-9 * abs(q)
+    assert q > 0.05
 
 
 def test_louvain_hash_equals_sort_rmat20(monkeypatch):

@@ -262,3 +262,30 @@ def test_rmat14_quality_vs_networkx(self_loops):
     assert q > 0.82 * q_nx
     assert abs(q - q_ref) < 1e-4
     assert abs(q - q_part_nx) < (5e-4 if self_loops else 1e-4)
+
+
+def test_rmat20_integer_vs_compiled_oracle():
+    """The reference's Louvain usecase size (cpp/tests/community/louvain_test.cpp:430-442,
+    RMAT(20, 32) symmetric): integer weights in [1, 4] keep every sum below 2^53
+    (sum_c a_c^2 <= m^2 ~ 5.6e15), so the local-move gains, cluster weights and Q are
+    exact in any order and the GPU must reproduce the oracle exactly: same clustering,
+    same Q bits, same level count.  The oracle here is oracle/cpu_louvain.c (the numpy
+    oracle's arithmetic compiled with OpenMP; tests/test_cpu_baseline.py pins the two
+    together) on the oracle's own graph construction (oracle/graph.py)."""
+    from oracle import cpu_native
+    s, d = rmat.rmat(20, 16 << 20, seed=42)
+    w = np.floor(rmat.rmat_weights(s.size, seed=43).astype(np.float64) * 4.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    OG = og.create_graph(s, d, w, renumber=True)
+    m = float(OG.weights.sum())
+    assert m * m < 2.0**53
+    h, G = make_graph(s, d, w.astype(np.float32), renumber=True, symmetric=True)
+    v, c, q = run(h, G)
+    levels = h.last_louvain_levels()
+    assert np.array_equal(v, OG.number_map)
+    oc, oq, olevels = cpu_native.louvain(OG.offsets, OG.indices, OG.weights, threads=16)
+    print(f"RMAT-20 integer Louvain: V={OG.num_vertices} E={OG.num_edges} Q gpu {q!r} oracle {oq!r}, "
+          f"levels {levels}/{olevels}, clusters {np.unique(c).size}")
+    assert levels == olevels
+    assert q == oq
+    assert np.array_equal(c, oc)

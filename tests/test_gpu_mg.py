@@ -32,10 +32,16 @@ def _slice(rank, world, E):
     return rank * E // world, (rank + 1) * E // world
 
 
-def _rank_setup():
+def _stack_file(port, rank):
+    return f"/tmp/cgx_stacks_{port}_{rank}.txt"
+
+
+def _rank_setup(port=None, rank=None):
     """In a worker, before its first HIP call:
-    * SIGUSR1 prints every thread's stack (from the signal handler, so a rank blocked
-      inside a C call still answers); _spawn sends it on a deadline;
+    * SIGUSR1 writes every thread's stack (from the signal handler, so a rank blocked
+      inside a C call still answers) to the rank's own file, which _spawn prints rank
+      by rank on a deadline (8 ranks writing one stderr interleaved their stacks
+      beyond reading);
     * HSA_ENABLE_SDMA=0: copies run as blit kernels, not on the DMA engines.  Up to 8
       rehearsal ranks share the one test GPU, and the world-8 Louvain rehearsal (the
       most copy-heavy: hundreds of small staged collectives per rank) stalled in 3 of
@@ -45,7 +51,8 @@ def _rank_setup():
     import signal
     import sys
     os.environ.setdefault("HSA_ENABLE_SDMA", "0")
-    faulthandler.register(signal.SIGUSR1, file=sys.stderr, all_threads=True)
+    out = sys.stderr if port is None else open(_stack_file(port, rank), "w")
+    faulthandler.register(signal.SIGUSR1, file=out, all_threads=True)
 
 
 def _spawn(fn, args, nprocs, deadline=150.0):
@@ -67,6 +74,12 @@ def _spawn(fn, args, nprocs, deadline=150.0):
         except OSError:
             pass
     time.sleep(3.0)
+    port = args[1]
+    for r in alive:
+        try:
+            print(f"===== rank {r} stacks =====\n" + open(_stack_file(port, r)).read(), flush=True)
+        except OSError:
+            print(f"===== rank {r}: no stack file", flush=True)
     for p in ctx.processes:
         if p.is_alive():
             p.kill()
@@ -90,7 +103,7 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_setup()
+    _rank_setup(port, rank)
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -199,7 +212,7 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_setup()
+    _rank_setup(port, rank)
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -302,7 +315,7 @@ def _pr_options_worker(rank, world, port, C):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_setup()
+    _rank_setup(port, rank)
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -374,7 +387,7 @@ def _sssp_worker(rank, world, port, C, scale, symmetric, cutoff):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_setup()
+    _rank_setup(port, rank)
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -455,18 +468,120 @@ def test_mg_world8_reference_grid(algo, C):
         _spawn(_worker, (8, port, C, 11, False, algo), 8)
 
 
-def _dask_worker(rank, world, port, C):
-    """cugraph.dask (one process per GPU): each rank passes its partition of a raw
-    edge list (duplicates, both directions, spread over the ranks) to
-    Graph.from_dask_cudf_edgelist; PageRank / BFS / Louvain partitions, gathered, must
-    match single-GPU cugraph on the whole edge list (the reference's
-    python/cugraph/cugraph/tests/mg/test_mg_pagerank.py pattern)."""
+def _mg_sg_worker(rank, world, port, C, scale):
+    """MG against the single-GPU library on the same graph (the reference's MG tests:
+    cpp/tests/link_analysis/mg_pagerank_test.cpp:258-270,333-347 compares MG with SG
+    on RMAT(20, 32); cpp/tests/traversal/mg_bfs_test.cpp:160-225):
+    * PageRank bit for bit per external id, same iteration count -- the push sums are
+      u64 fixed point and the (diff, dangling) totals are allreduced as u64, so the
+      partition changes no bit;
+    * BFS (direction-optimising) distances equal to SG's;
+    * BFS predecessors equal to SG's on the graph renumbered by the MG number map (the
+      reference's MG-test method, mg_louvain_test.cpp:69-90): both take the frontier
+      neighbour with the smallest id, and with the MG numbering those ids agree.
+      (On SG's own numbering the predecessor is another valid parent, checked by
+      tests/test_gpu_bench_parity.py's rule.)"""
     import sys
     sys.path.insert(0, PKG)
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    _rank_setup()
+    _rank_setup(port, rank)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pylibcugraph as plc
+
+    s, d, _ = _graph(scale, False, seed=17)
+    E = s.size
+    lo, hi = _slice(rank, world, E)
+    ctx = plc.comms.init_torch(C)
+    h = plc.ResourceHandle(ctx.ptr)
+    props = plc.GraphProperties(is_symmetric=True, is_multigraph=False)
+    dev = lambda a: torch.as_tensor(np.ascontiguousarray(a).astype(np.int32), device="cuda")  # noqa: E731
+    Gp = plc.MGGraph(h, props, dev(s[lo:hi]), dev(d[lo:hi]), None, store_transposed=True, num_edges=E)
+    v, x = plc.pagerank(h, Gp, None, None, None, None, 0.85, 1e-6, 500, False)
+    it = h.last_iterations()
+    Gp = None
+    Gb = plc.MGGraph(h, props, dev(s[lo:hi]), dev(d[lo:hi]), None, store_transposed=False, num_edges=E)
+    root = int(s[np.argmax(np.bincount(s))])  # a hub: the traversal switches to bottom-up early
+    srct = dev([root] if rank == 0 else [])
+    dd, pp, vb = plc.bfs(h, Gb, srct, True, 0, True, False)
+    bu = h.last_bfs_bottom_up_steps()
+    mine = (v.cpu().numpy(), x.cpu().numpy(), it, vb.cpu().numpy(), dd.cpu().numpy(), pp.cpu().numpy(), bu)
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    if rank == 0:
+        vv = np.concatenate([a[0] for a in allr]).astype(np.int64)
+        xx = np.concatenate([a[1] for a in allr])
+        assert all(a[2] == it for a in allr)
+        # single GPU, default numbering
+        h1 = plc.ResourceHandle()
+        G1 = plc.SGGraph(h1, props, dev(s), dev(d), None, store_transposed=True, renumber=True)
+        v1, x1 = plc.pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
+        it1 = h1.last_iterations()
+        v1, x1 = v1.cpu().numpy().astype(np.int64), x1.cpu().numpy()
+        n = int(max(vv.max(), v1.max())) + 1
+        a_mg, a_sg = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        a_mg[vv], a_sg[v1] = xx, x1
+        print(f"RMAT-{scale} MG {world // C}x{C}: V={vv.size} E={E} PageRank iterations MG {it} SG {it1}, "
+              f"equal bits {np.mean(a_mg[v1] == a_sg[v1]):.6f}; BFS bottom-up steps {[a[6] for a in allr]}")
+        assert it == it1
+        assert np.array_equal(a_mg.view(np.int32), a_sg.view(np.int32))
+        G1 = None
+        vb_all = np.concatenate([a[3] for a in allr]).astype(np.int64)  # MG global id order
+        db_all = np.concatenate([a[4] for a in allr])
+        pb_all = np.concatenate([a[5] for a in allr]).astype(np.int64)
+        assert max(a[6] for a in allr) > 0  # the direction-optimising switch happened
+        Gs = plc.SGGraph(h1, props, dev(s), dev(d), None, store_transposed=False, renumber=True)
+        d1, _, u1 = plc.bfs(h1, Gs, dev([root]), True, 0, True, False)
+        dist_sg = np.full(n, -7, np.int64)
+        dist_sg[u1.cpu().numpy()] = d1.cpu().numpy()
+        assert np.array_equal(db_all, dist_sg[vb_all])
+        Gs = None
+        inv = np.zeros(n, dtype=np.int64)
+        inv[vb_all] = np.arange(vb_all.size)
+        Gm = plc.SGGraph(h1, props, dev(inv[s]), dev(inv[d]), None, store_transposed=False, renumber=False)
+        d2, p2, u2 = plc.bfs(h1, Gm, dev([inv[root]]), True, 0, True, False)
+        assert np.array_equal(u2.cpu().numpy(), np.arange(vb_all.size))
+        assert np.array_equal(d2.cpu().numpy(), db_all)
+        pm = np.where(pb_all >= 0, inv[np.maximum(pb_all, 0)], -1)
+        assert np.array_equal(p2.cpu().numpy().astype(np.int64), pm)
+    dist.barrier()
+    h = None
+    Gb = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C,scale", [(8, 2, 18), (8, 8, 16), (2, 1, 16)])
+def test_mg_equals_sg(world, C, scale):
+    """The reference's 8-GPU grid (4 x 2) at RMAT-18 and the flat 1 x 8 grid, rehearsed
+    with 8 ranks on the one test GPU (torch.distributed/gloo callbacks)."""
+    _spawn(_mg_sg_worker, (world, _free_port(), C, scale), world, deadline=300.0)
+
+
+def _dask_worker(rank, world, port, C):
+    """cugraph.dask (one process per GPU): each rank passes its partition of a raw
+    edge list (duplicates, both directions, spread over the ranks) to
+    Graph.from_dask_cudf_edgelist; PageRank / BFS / Louvain partitions, gathered, must
+    match single-GPU cugraph on the whole edge list (the reference's
+    python/cugraph/cugraph/tests/mg/test_mg_pagerank.py pattern):
+    * PageRank bit for bit (u64 fixed-point sums and their u64 allreduce: the
+      partition changes no sum; integer-valued weights keep the out-weight sums exact);
+    * BFS distances exactly;
+    * Louvain through one level -- MG and SG Louvain agree only through one level of
+      the outer loop, and only on the same numbering (cpp/tests/community/
+      mg_louvain_test.cpp:69-90,146-150): single-GPU Louvain with max_level 1 on the
+      graph renumbered by the MG number map (the gathered result's vertex order) must
+      give the same partition and the same modularity bits."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    _rank_setup(port, rank)
     import pandas as pd
     import torch
     import torch.distributed as dist
@@ -477,7 +592,7 @@ def _dask_worker(rank, world, port, C):
     from oracle import rmat
 
     s, d = rmat.rmat(10, 16 << 10, seed=9)
-    w = rmat.rmat_weights(s.size, seed=10).astype(np.float32)
+    w = (np.floor(rmat.rmat_weights(s.size, seed=10) * 8.0) + 1.0).astype(np.float32)
     df = pd.DataFrame({"src": s.astype(np.int64), "dst": d.astype(np.int64), "wt": w})
     Comms.initialize(pcols=C, backend="torch")
     assert Comms.get_2D_partition() == (world // C, C)
@@ -487,21 +602,33 @@ def _dask_worker(rank, world, port, C):
     pr = cugraph.dask.gather(cugraph.dask.pagerank(dg, tol=1e-6)).sort_values("vertex")
     root = int(s[0])
     bf = cugraph.dask.gather(cugraph.dask.bfs(dg, root)).sort_values("vertex")
-    lv, q = cugraph.dask.louvain(dg)
-    lv = cugraph.dask.gather(lv)
+    lv, q = cugraph.dask.louvain(dg, max_iter=1)
+    lv = cugraph.dask.gather(lv)  # rank order: the MG global id order
     if rank == 0:
         g = cugraph.Graph(directed=False)
         g.from_pandas_edgelist(df, source="src", destination="dst", edge_attr="wt")
         ref = cugraph.pagerank(g, tol=1e-6).sort_values("vertex")
         assert np.array_equal(pr["vertex"].to_numpy(), ref["vertex"].to_numpy())
-        rel = np.abs(pr["pagerank"].to_numpy() - ref["pagerank"].to_numpy()) / ref["pagerank"].to_numpy()
-        assert rel.max() < 1e-5, rel.max()
+        assert np.array_equal(pr["pagerank"].to_numpy(), ref["pagerank"].to_numpy())
         rb = cugraph.bfs(g, root).sort_values("vertex")
         assert np.array_equal(bf["distance"].to_numpy(), rb["distance"].to_numpy())
-        # Louvain: a partition of every vertex, modularity within the SG result's range
-        assert np.array_equal(np.sort(lv["vertex"].to_numpy()), ref["vertex"].to_numpy())
-        _, q_sg = cugraph.louvain(g)
-        assert q > 0.5 * q_sg
+        # Louvain: single-GPU Louvain, one level, on the MG-numbered graph
+        import pylibcugraph as plc
+        from oracle import graph as og
+        nmap = lv["vertex"].to_numpy().astype(np.int64)
+        assert np.array_equal(np.sort(nmap), ref["vertex"].to_numpy())
+        inv = np.zeros(int(nmap.max()) + 1, dtype=np.int64)
+        inv[nmap] = np.arange(nmap.size)
+        ss, sd, sw = og.symmetrize_dedup(s.astype(np.int64), d.astype(np.int64), w.astype(np.float64))
+        h1 = plc.ResourceHandle()
+        G1 = plc.SGGraph(h1, plc.GraphProperties(is_symmetric=True, is_multigraph=False),
+                         torch.as_tensor(inv[ss].astype(np.int32), device="cuda"),
+                         torch.as_tensor(inv[sd].astype(np.int32), device="cuda"),
+                         torch.as_tensor(sw.astype(np.float32), device="cuda"), store_transposed=False, renumber=False)
+        v1, c1, q1 = plc.louvain(h1, G1, 1, 1.0, False)
+        assert np.array_equal(v1.cpu().numpy(), np.arange(nmap.size))
+        assert _same_partition(c1.cpu().numpy(), lv["partition"].to_numpy())
+        assert q == q1, (q, q1)
     Comms.destroy()
     dist.destroy_process_group()
 

@@ -218,24 +218,6 @@ def test_packed_entries_bitwise_equal_plain(scale, renumber, monkeypatch):
     assert np.array_equal(r_packed, r_plain)
 
 
-@pytest.mark.parametrize("packed", ["0"])
-def test_source_partition_bitwise_equal(packed, monkeypatch):
-    """The opt-in source partition of the push schedule (CGX_PR_SRCPART=1,
-    pagerank.hip build_items_srcpart: units cut at the head / tail source ranges,
-    tail range k on XCD queue k) adds the same fixed-point terms in another order:
-    the same bits as the window schedule.  32-bit entries only (the packed format
-    keeps whole wave segments per window, which the cuts would break).  RMAT-20 has
-    enough sources (>= 2^19) for a partition."""
-    monkeypatch.setenv("CGX_PR_PACKED", packed)
-    s, d, _ = rmat_graph(20, False, True)
-    h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
-    r_win = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
-    monkeypatch.setenv("CGX_PR_SRCPART", "1")
-    h2, G2 = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
-    r_part = host(plc().pagerank(h2, G2, None, None, None, None, 0.85, 1e-6, 500, False)[1])
-    assert np.array_equal(r_win, r_part)
-
-
 def _star_plus_ring(n_leaves):
     """Vertex 0 points to n_leaves leaves and has no in-edges, so its x~ =
     pr / outdeg ~ 0.15 / V / V falls below 2^-39: enc_fixed's rounding branch.
@@ -309,51 +291,6 @@ def test_unit_weights_take_unweighted_push(scale, monkeypatch):
     got = by_ext(v3, r3)
     vv = host(v3)
     assert (np.abs(got[vv] - ref_ext[vv]) / ref_ext[vv]).max() < REL
-
-
-@pytest.mark.parametrize("scale,head,src", [(18, 16384, 16384), (20, 65536, 32768), (20, 65536, 1 << 20)])
-def test_source_slices_bitwise_equal(scale, head, src, monkeypatch):
-    """Source slices (pagerank.hip plan_slices: head / 8 mid slices queued per XCD /
-    tail, 9 groups of partial sums added by the apply) give the same fixed-point
-    sums -- so the same bits -- as the unsliced push (CGX_PR_SLICE=0).  Small head
-    and slice sizes force every slice kind (and, at the last size, no tail) at
-    test scale."""
-    s, d, _ = rmat_graph(scale, False, True)
-    monkeypatch.setenv("CGX_PR_SLICE", "0")
-    h0, G0 = make_graph(s, d, None, transposed=True, symmetric=True)
-    v0, r0 = plc().pagerank(h0, G0, None, None, None, None, 0.85, 1e-6, 500, False)
-    it0 = h0.last_iterations()
-    monkeypatch.setenv("CGX_PR_SLICE", "1")
-    monkeypatch.setenv("CGX_PR_SLICE_HEAD", str(head))
-    monkeypatch.setenv("CGX_PR_SLICE_SRC", str(src))
-    for packed in ("1", "0"):  # 16-bit and 32-bit entries
-        monkeypatch.setenv("CGX_PR_PACKED", packed)
-        h1, G1 = make_graph(s, d, None, transposed=True, symmetric=True)
-        v1, r1 = plc().pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
-        assert h1.last_iterations() == it0
-        assert np.array_equal(host(v0), host(v1)) and np.array_equal(host(r0), host(r1)), packed
-        # a second call reuses the schedule (stored and added partials are reset correctly)
-        _, r2 = plc().pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
-        assert np.array_equal(host(r0), host(r2))
-
-
-@pytest.mark.parametrize("graph", ["rmat20", "star"])
-def test_source_dedup_bitwise_equal(graph, monkeypatch):
-    """The dedup push (pagerank.hip push_body16 DD: only run heads gather x~, the
-    rest of a run takes the head's value by ds_bpermute) gives the same bits as the
-    plain packed push.  The star graph makes long runs that cross rows and units."""
-    if graph == "star":
-        s, d = _star_plus_ring(300_000)
-    else:
-        s, d, _ = rmat_graph(20, False, True)
-    out = []
-    for dd in ("0", "1"):
-        monkeypatch.setenv("CGX_PR_DEDUP", dd)
-        h, G = make_graph(s, d, None, transposed=True, symmetric=graph != "star")
-        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
-        out.append((host(v), host(r), h.last_iterations()))
-    assert out[0][2] == out[1][2]
-    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
 
 
 @pytest.mark.parametrize("scale", [12, 20])
@@ -469,3 +406,56 @@ def test_calibrated_queues_bitwise_equal(deal, monkeypatch):
         for o in out[1:]:
             assert o[2] == out[0][2]
             assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+
+
+def _outw_host(G, h):
+    """(number map, CSR offsets, CSR weights) in internal order, and the library's sums."""
+    v, _ = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-2, 500, False)
+    got = host(G.out_weight_sums(h))
+    off, _, w = G.adjacency(h, transposed=False)
+    return host(v), host(off).astype(np.int64), host(w).astype(np.float64), got
+
+
+@pytest.mark.parametrize("case", ["star_exact", "aligned_rows", "rmat20_uniform", "fp64_weights"])
+def test_out_weight_sums_tiled(case):
+    """compute_out_weight_sums (pagerank_impl.cuh:158-164) over edge tiles
+    (graph_build.hip k_row_sums_tiles / k_row_sums_spill): rows spanning many 2048-edge
+    tiles (a 300K-edge hub), rows ending exactly on tile boundaries, zero-degree rows
+    between and after the edges.  Weights that are multiples of 1/8 make every fp64
+    sum exact, so those must be bitwise the numpy sums; uniform weights within one
+    fp32 ulp."""
+    rng = np.random.default_rng(5)
+    wdtype = np.float32
+    if case == "star_exact":
+        n = 300_000
+        leaves = np.arange(1, n + 1)
+        s = np.concatenate([np.zeros(n, np.int64), leaves, leaves])
+        d = np.concatenate([leaves, np.roll(leaves, -1), np.zeros(n, np.int64)])
+        w = rng.integers(1, 64, s.size) / 8.0
+        renumber, sym = True, False
+    elif case == "aligned_rows":
+        # out-degrees 2048, 4096, 1, 0 (isolated ids 3..9 never appear as sources), 2047, 2049 ...
+        degs = [2048, 4096, 1, 0, 0, 0, 0, 0, 0, 0, 2047, 2049, 6144, 1, 2048]
+        s = np.concatenate([np.full(k, i, np.int64) for i, k in enumerate(degs)])
+        nv = 20000
+        d = np.concatenate([rng.choice(np.arange(20, nv), k, replace=False) for k in degs])
+        d[0] = nv - 1  # the id range reaches nv - 1: trailing ids without out-edges
+        w = rng.integers(1, 64, s.size) / 8.0
+        renumber, sym = False, False
+    else:
+        s, d, _ = rmat_graph(20, False, True)
+        w = rng.random(s.size)
+        renumber, sym = True, True
+        if case == "fp64_weights":
+            wdtype = np.float64
+            w = rng.integers(1, 1 << 20, s.size) / 1024.0
+    h, G = make_graph(s, d, w, transposed=False, renumber=renumber, symmetric=sym, wdtype=wdtype)
+    v, off, ww, got = _outw_host(G, h)
+    want = np.add.reduceat(np.concatenate([ww, [0.0]]), off[:-1]) * (off[1:] > off[:-1])
+    want = want.astype(wdtype)
+    assert got.dtype == wdtype and got.shape == want.shape
+    if case == "rmat20_uniform":
+        rel = np.abs(got.astype(np.float64) - want) / np.maximum(want, 1e-30)
+        assert rel.max() <= 1.2e-7 and (got == want).mean() > 0.9999
+    else:
+        assert np.array_equal(got, want)

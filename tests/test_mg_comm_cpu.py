@@ -93,3 +93,44 @@ def test_torch_comm_adapter_gloo(world, C):
         pytest.skip("libcugraph_c.so not built")
     tmp.spawn(_worker, args=(world, _free_port(), C), nprocs=world, join=True)
     del torch
+
+
+def _mismatch_worker(rank, world, port):
+    """Rank 0 calls an allreduce where rank 1 calls an allgather (the same call number):
+    both must fail with CollectiveMismatch naming the two calls, not hang or mix data."""
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pylibcugraph import comms as cm
+    _, w, _, _ = cm.torch_comms(world, memory="host")
+    send = np.ones(4, dtype=np.float64)
+    recv = np.zeros(4 * world, dtype=np.float64)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    # a matching call first: call numbers agree
+    assert w.allreduce(None, p(send), p(recv), 4, cm.CGX_COMM_F64, cm.CGX_COMM_SUM, None) == 0
+    try:
+        if rank == 0:
+            w._check("allreduce", 4, cm.CGX_COMM_F64, cm.CGX_COMM_SUM)
+        else:
+            w._check("allgather", 4, cm.CGX_COMM_F64)
+        raise AssertionError("mismatch not detected")
+    except cm.CollectiveMismatch as e:
+        msg = str(e)
+        assert "rank 0: call 2 allreduce" in msg and "rank 1: call 2 allgather" in msg, msg
+    # the C-facing entry point reports the failure as a nonzero return
+    if rank == 0:
+        rc = w.allreduce(None, p(send), p(recv), 4, cm.CGX_COMM_F64, cm.CGX_COMM_SUM, None)
+    else:
+        rc = w.allgather(None, p(send), p(recv), 4, cm.CGX_COMM_F64, None)
+    assert rc == 1
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_torch_comm_detects_mismatched_collectives():
+    pytest.importorskip("torch")
+    import torch.multiprocessing as tmp
+    tmp.spawn(_mismatch_worker, args=(2, _free_port()), nprocs=2, join=True)
