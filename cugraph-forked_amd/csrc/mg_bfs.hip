@@ -17,9 +17,16 @@
 //    1 x P grid the column has one rank: no candidate exchange at all;
 //  * bottom-up (symmetric graphs, direction_optimizing): every rank owns the
 //    out-adjacency of its own vertices (a 1D partition by source owner, built once
-//    from the 2D blocks and cached); the frontier bitmap of every rank is
-//    allgathered (V/8 bytes), each rank scans its unvisited vertices' sorted
-//    adjacency and stops at the first frontier neighbour.
+//    from the 2D blocks and cached).  Neighbours are stored as positions in the
+//    allgathered frontier bitmap -- rank q's vertices at q * W + (u - voff[q]), W =
+//    the largest rank's vertex count rounded up to 32 -- so a neighbour's frontier
+//    bit is one load, with no per-edge owner search (positions keep the global id
+//    order).  The rank's frontier bitmap segment (V/P/8 bytes) is allgathered, and
+//    the single-GPU two-pass scan runs over the owned vertices (bfs.hip k_bu_probe /
+//    k_bu_residual): a lane per vertex loads its first 8 neighbours and their
+//    frontier words back to back, the misses of longer lists go to 16 residual
+//    sub-queues scanned by 16-lane groups, and each wave writes its vertices' next-
+//    frontier bits as whole words.  Level counts go to 16 partial counters.
 //
 // Both pick the frontier neighbour with the smallest global id, so distances and
 // predecessors do not depend on the direction schedule.  The direction switch keeps
@@ -41,12 +48,25 @@ namespace {
 
 inline unsigned blocks(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 16384); }
 
+constexpr int64_t kPosPad = 16;  // entries past the end of bfs_rows_t::pos
+
 struct bfs_rows_t {
   int64_t n_own = 0, ne = 0;
   buffer off;  // int64[n_own + 1]
-  buffer idx;  // uint32 global ids, ascending per row
-  int64_t words = 0;  // 32-bit words of each rank's bitmap segment (max over ranks)
+  buffer pos;  // uint32 bitmap positions of the neighbours (q * W + local id), ascending per row
+               // (+ 16 entries of padding: the probe's vector loads)
+  int64_t words = 0;  // 32-bit words of each rank's bitmap segment (max over ranks); W = 32 * words
 };
+
+// global id -> position in the allgathered frontier bitmap
+__global__ void k_global_to_pos(uint32_t* ids, int64_t n, int64_t const* voff, int P, int64_t W)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const u = ids[i];
+    int const q     = mg_owner_of_global(u, voff, P);
+    ids[i]          = (uint32_t)(q * W + (u - voff[q]));
+  }
+}
 
 template <typename V>
 __global__ void k_owner_src(V const* src, int64_t n, int64_t const* voff, int P, int* dest)
@@ -124,8 +144,14 @@ bfs_rows_t& mg_rows(handle_t& h, graph_t& g)
   rows->ne    = m;
   dbuf<unsigned long long> k1(std::max<int64_t>(m, 1), s), k2(std::max<int64_t>(m, 1), s);
   dbuf<uint32_t> rr(std::max<int64_t>(m, 1), s);
-  rows->idx.set_stream(s);
-  rows->idx.resize(std::max<int64_t>(m, 1) * sizeof(uint32_t));
+  int64_t maxn = 0;
+  for (int q = 0; q < P; ++q) maxn = std::max(maxn, mg.voff[q + 1] - mg.voff[q]);
+  rows->words = std::max<int64_t>((maxn + 31) / 32, 1);
+  CGX_EXPECTS((uint64_t)P * (uint64_t)rows->words * 32ull < (1ull << 32), CUGRAPH_NOT_IMPLEMENTED,
+              "MG BFS: frontier bitmap positions exceed 32 bits");
+  rows->pos.set_stream(s);
+  rows->pos.resize((m + kPosPad) * sizeof(uint32_t));
+  HIP_CHECK(hipMemsetAsync(rows->pos.data<uint32_t>() + m, 0, kPosPad * sizeof(uint32_t), s));
   rows->off.set_stream(s);
   rows->off.resize((rows->n_own + 1) * sizeof(int64_t));
   if (m) {
@@ -134,15 +160,15 @@ bfs_rows_t& mg_rows(handle_t& h, graph_t& g)
     CGX_LAUNCH_CHECK();
     radix_sort_keys<unsigned long long>(k1.data(), k2.data(), m, 0, 64, s);
     hipLaunchKernelGGL(k_split_row_keys, dim3(blocks(m)), dim3(kBlock), 0, s, k2.data(), m, rr.data(),
-                       rows->idx.data<uint32_t>());
+                       rows->pos.data<uint32_t>());
+    CGX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_global_to_pos, dim3(blocks(m)), dim3(kBlock), 0, s, rows->pos.data<uint32_t>(), m,
+                       voff_d.data(), P, rows->words * 32);
     CGX_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(k_offsets_u32, dim3(blocks(rows->n_own + 1)), dim3(kBlock), 0, s, rr.data(), m, rows->n_own,
                      rows->off.data<int64_t>());
   CGX_LAUNCH_CHECK();
-  int64_t maxn = 0;
-  for (int q = 0; q < P; ++q) maxn = std::max(maxn, mg.voff[q + 1] - mg.voff[q]);
-  rows->words = std::max<int64_t>((maxn + 31) / 32, 1);
   HIP_CHECK(hipStreamSynchronize(s));
   mg.bfs_rows = rows;
   return *rows;
@@ -198,16 +224,32 @@ bfs_block_t& mg_block_csr(handle_t& h, graph_t& g)
 }
 
 // ---------------------------------------------------------------- level kernels
+constexpr int kParts = 16;  // partial counters 256 B apart (different L2 channels), as bfs.hip
 struct level_ctr {
-  unsigned long long next_n;  // own vertices discovered
+  unsigned long long next_n;  // own vertices discovered (top-down appends)
   unsigned long long next_m;  // sum of their degrees
-  unsigned long long ncand;   // candidates written
-  unsigned long long pad;
+  unsigned long long nconv;   // bitmap -> queue conversion appends
+  unsigned long long pad[29];
+  unsigned long long part[kParts][32];  // bottom-up: [p][0] vertices, [p][1] edges, [p][2] residual sub-queue p
 };
 
-// Level counters are single addresses: same-address atomics serialise at the memory
-// side (≈8 ns each, bfs.hip), so appends are reserved once per wave and sums are
-// added once per block, and the kernels that do so run on capped grids.
+// (vertices, edges) of a level: the top-down fields plus the bottom-up partials (host)
+inline std::pair<unsigned long long, unsigned long long> level_counts(level_ctr const& c)
+{
+  unsigned long long n = c.next_n, m = c.next_m;
+  for (int p = 0; p < kParts; ++p) {
+    n += c.part[p][0];
+    m += c.part[p][1];
+  }
+  return {n, m};
+}
+
+// residual sub-queue capacity: sub-queue p holds at most the 64 vertices of each of its chunks
+__host__ __device__ __forceinline__ int64_t mg_residual_cap(int64_t n) { return ((((n + 63) >> 6) + kParts - 1) / kParts) * 64; }
+
+// Same-address atomics serialise at the memory side (≈8 ns each, bfs.hip): top-down
+// appends are reserved once per wave and sums added once per block on capped grids;
+// the bottom-up kernels add per block to one of the kParts partial counters.
 inline unsigned capped(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 1024); }
 
 __device__ __forceinline__ long long wave_reserve(unsigned long long* tail, bool take)
@@ -368,34 +410,171 @@ __global__ void k_mark_bits(uint32_t const* q, int64_t n, uint32_t* bits)
     atomicOr(bits + (q[i] >> 5), 1u << (q[i] & 31u));
 }
 
-template <typename V>
-__global__ void k_bottom_up(int64_t n_own, int64_t const* off, uint32_t const* idx, V* dist, V* pred,
-                            uint32_t const* bitmap, int64_t const* voff, int P, int64_t words, V depth1, int* flag,
-                            uint32_t* next, level_ctr* ctr)
+// per-block (vertices, edges) to partial counter blockIdx % kParts; all threads call
+__device__ __forceinline__ void flush_parts(level_ctr* ctr, unsigned long long n, unsigned long long m)
 {
-  V const INF = std::numeric_limits<V>::max();
-  unsigned long long m = 0;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_own; v += (int64_t)gridDim.x * blockDim.x) {
-    bool take = false;
-    if (dist[v] == INF) {
-      for (int64_t e = off[v]; e < off[v + 1]; ++e) {
-        int64_t u = idx[e];
-        int q     = mg_owner_of_global(u, voff, P);
-        int64_t l = u - voff[q];
-        if ((bitmap[q * words + (l >> 5)] >> (l & 31)) & 1u) {
+  __shared__ unsigned long long sn[kBlock / 64], sm[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_xor(n, o, 64);
+    m += __shfl_xor(m, o, 64);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sn[threadIdx.x >> 6] = n;
+    sm[threadIdx.x >> 6] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tn = 0, tm = 0;
+    for (int w = 0; w < kBlock / 64; ++w) tn += sn[w], tm += sm[w];
+    int const p = blockIdx.x % kParts;
+    if (tn) atomicAdd(&ctr->part[p][0], tn);
+    if (tm) atomicAdd(&ctr->part[p][1], tm);
+  }
+}
+
+constexpr int kProbe = 8;  // first neighbours tested per vertex in the probe (bfs.hip: 8 measured best)
+
+// the global id of bitmap position x
+__device__ __forceinline__ int64_t pos_to_global(uint32_t x, int64_t const* voff, int64_t W)
+{
+  int64_t const q = (int64_t)x / W;
+  return voff[q] + ((int64_t)x - q * W);
+}
+
+// Bottom-up probe: one lane per owned vertex, 64 consecutive vertices per wave.  An
+// unvisited vertex loads its first kProbe neighbour positions and their frontier
+// words back to back and takes the lowest hit (the smallest-global-id frontier
+// neighbour: positions keep the id order).  The wave's next-frontier bits are two
+// whole words of seg_next that no other wave writes (no atomics, no memset); misses
+// of lists longer than kProbe go to residual sub-queue (chunk % kParts).
+template <typename V>
+__global__ __launch_bounds__(256) void k_mg_bu_probe(int64_t n_own, int64_t const* off, uint32_t const* pos, V* dist,
+                                                      V* pred, uint32_t const* bitmap, int64_t const* voff, int64_t W,
+                                                      V depth1, uint32_t* seg_next, uint32_t* res, level_ctr* ctr)
+{
+  V const INF    = std::numeric_limits<V>::max();
+  int const lane = threadIdx.x & 63;
+  unsigned long long my_n = 0, my_m = 0;
+  int64_t const nchunks = (n_own + 63) >> 6;
+  int64_t const stride  = (int64_t)gridDim.x * (kBlock / 64);
+  int64_t const rcap    = mg_residual_cap(n_own);
+  for (int64_t c = blockIdx.x * (int64_t)(kBlock / 64) + (threadIdx.x >> 6); c < nchunks; c += stride) {
+    int64_t const v = (c << 6) + lane;
+    bool const un   = v < n_own && dist[v] == INF;
+    int64_t beg = 0, end = 0;
+    if (un) {
+      beg = off[v];
+      end = off[v + 1];
+    }
+    int64_t const deg = end - beg;
+    bool hit = false, more = false;
+    uint32_t par = 0;
+    if (deg > 0) {
+      uint32_t u[kProbe];
+#pragma unroll
+      for (int t = 0; t < kProbe; ++t) u[t] = pos[beg + (t < deg ? t : 0)];
+      uint32_t fw[kProbe];  // every frontier word first: the loads issue back to back
+#pragma unroll
+      for (int t = 0; t < kProbe; ++t) fw[t] = bitmap[u[t] >> 5];
+      uint32_t hm = 0;
+#pragma unroll
+      for (int t = 0; t < kProbe; ++t) hm |= (t < deg ? (fw[t] >> (u[t] & 31u)) & 1u : 0u) << t;
+#pragma unroll
+      for (int t = kProbe - 1; t >= 0; --t)
+        if ((hm >> t) & 1u) par = u[t];
+      hit  = hm != 0;
+      more = !hit && deg > kProbe;
+    }
+    if (hit) {
+      dist[v] = depth1;
+      if (pred) pred[v] = (V)pos_to_global(par, voff, W);
+      my_n += 1;
+      my_m += (unsigned long long)deg;
+    }
+    unsigned long long const hb = __ballot(hit);
+    if ((lane & 31) == 0 && (c << 6) + lane < n_own) seg_next[((c << 6) + lane) >> 5] = (uint32_t)(hb >> lane);
+    unsigned long long const mm = __ballot(more);
+    if (mm) {
+      unsigned long long base = 0;
+      int const leader = __ffsll((long long)mm) - 1;
+      int const sq     = (int)(c % kParts);
+      if (lane == leader) base = atomicAdd(&ctr->part[sq][2], (unsigned long long)__popcll(mm));
+      base = __shfl(base, leader, 64);
+      if (more) res[sq * rcap + (int64_t)base + __popcll(mm & ((1ull << lane) - 1ull))] = (uint32_t)v;
+    }
+  }
+  flush_parts(ctr, my_n, my_m);
+}
+
+// Bottom-up residual: 16-lane groups scan the probe's misses from neighbour kProbe on
+template <typename V>
+__global__ __launch_bounds__(256) void k_mg_bu_residual(int64_t n_own, int64_t const* off, uint32_t const* pos,
+                                                         V* dist, V* pred, uint32_t const* bitmap, int64_t const* voff,
+                                                         int64_t W, V depth1, uint32_t* seg_next, uint32_t const* res,
+                                                         level_ctr* ctr)
+{
+  constexpr int w = 16;
+  int const tid   = threadIdx.x;
+  int const lane  = tid & (w - 1);
+  int const gbase = (tid & 63) & ~(w - 1);
+  __shared__ unsigned long long s_pre[kParts + 1];
+  if (tid == 0) {
+    s_pre[0] = 0ull;
+    for (int p = 0; p < kParts; ++p) s_pre[p + 1] = s_pre[p] + ctr->part[p][2];
+  }
+  __syncthreads();
+  int64_t const n    = (int64_t)s_pre[kParts];
+  int64_t const rcap = mg_residual_cap(n_own);
+  int64_t const ng   = (int64_t)gridDim.x * (kBlock / w);
+  unsigned long long my_n = 0, my_m = 0;
+  for (int64_t i = blockIdx.x * (int64_t)(kBlock / w) + tid / w; i < n; i += ng) {
+    int p = 0;
+    while ((unsigned long long)i >= s_pre[p + 1]) ++p;
+    int64_t const v   = res[p * rcap + (i - (int64_t)s_pre[p])];
+    int64_t const beg = off[v], end = off[v + 1];
+    for (int64_t base = beg + kProbe; base < end; base += w) {
+      int64_t const e = base + lane;
+      bool hit        = false;
+      uint32_t u      = 0;
+      if (e < end) {
+        u   = pos[e];
+        hit = (bitmap[u >> 5] >> (u & 31u)) & 1u;
+      }
+      unsigned long long const gm = (__ballot(hit) >> gbase) & 0xffffull;
+      if (gm) {
+        if (lane == __ffsll((long long)gm) - 1) {
           dist[v] = depth1;
-          if (pred) pred[v] = (V)u;
-          flag[v] = 1;
-          take    = true;
-          m += (unsigned long long)(off[v + 1] - off[v]);
-          break;
+          if (pred) pred[v] = (V)pos_to_global(u, voff, W);
+          atomicOr(seg_next + (v >> 5), 1u << (uint32_t(v) & 31u));
+          my_n += 1;
+          my_m += (unsigned long long)(end - beg);
         }
+        break;
       }
     }
-    long long const slot = wave_reserve(&ctr->next_n, take);
-    if (take) next[slot] = (uint32_t)v;
   }
-  block_add(&ctr->next_m, m);
+  flush_parts(ctr, my_n, my_m);
+}
+
+// the own frontier bitmap segment -> a list of local ids (bottom-up -> top-down)
+__global__ void k_seg_to_queue(uint32_t const* seg, int64_t nwords, uint32_t* q, unsigned long long* tail)
+{
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const wi = base + threadIdx.x;
+    uint32_t word    = wi < nwords ? seg[wi] : 0u;
+    for (int r = 0; r < 32; ++r) {
+      bool const take = word != 0;
+      if (!__any(take)) break;
+      uint32_t v = 0;
+      if (take) {
+        v = (uint32_t)(wi * 32 + (__ffs(word) - 1));
+        word &= word - 1;
+      }
+      long long const slot = wave_reserve(tail, take);
+      if (take) q[slot] = v;
+    }
+  }
 }
 
 template <typename V>
@@ -469,12 +648,17 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   hipLaunchKernelGGL(k_init_sources<V>, dim3(blocks(all_src.n)), dim3(kBlock), 0, s, all_src.data(), all_src.n, lo, hi,
                      dist, qa.data(), &ctr.data()->next_n, flag.data());
   CGX_LAUNCH_CHECK();
-  auto hc  = to_host(ctr.data(), 1, s)[0];
-  int64_t nf_own = (int64_t)hc.next_n;
+  int64_t nf_own = (int64_t)level_counts(to_host(ctr.data(), 1, s)[0]).first;
 
   dbuf<int64_t> voff_d(P + 1, s);
   HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  dbuf<uint32_t> seg(rows.words, s), bitmap(rows.words * P, s);
+  // own frontier bitmap segments (current / next: the probe writes every word of the
+  // next, so neither needs a memset per level once cleared here) and the allgathered bitmap
+  dbuf<uint32_t> seg(rows.words, s), seg_next(rows.words, s), bitmap(rows.words * P, s);
+  HIP_CHECK(hipMemsetAsync(seg_next.data(), 0, rows.words * 4, s));
+  dbuf<uint32_t> resq(dir_opt ? std::max<int64_t>(kParts * mg_residual_cap(n_own), 1) : 1, s);
+  int64_t const W  = rows.words * 32;
+  bool have_queue  = true;   // the own frontier is in qa (else in seg)
   dbuf<double> scratch(1024, s), dsum(1, s);
   // m_u: degrees of unvisited vertices (global)
   double deg_own = 0;
@@ -523,18 +707,34 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
     HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
     V const depth1 = depth + 1;
     if (bottom_up) {
-      HIP_CHECK(hipMemsetAsync(seg.data(), 0, rows.words * 4, s));
-      if (nf_own)
-        hipLaunchKernelGGL(k_mark_bits, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own, seg.data());
-      CGX_LAUNCH_CHECK();
+      if (have_queue) {  // queue -> own bitmap segment
+        HIP_CHECK(hipMemsetAsync(seg.data(), 0, rows.words * 4, s));
+        if (nf_own)
+          hipLaunchKernelGGL(k_mark_bits, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own, seg.data());
+        CGX_LAUNCH_CHECK();
+      }
       comm.allgather<uint32_t>(seg.data(), bitmap.data(), (size_t)rows.words, s);
-      if (n_own)
-        hipLaunchKernelGGL(k_bottom_up<V>, dim3(capped(n_own)), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
-                           rows.idx.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), P, rows.words, depth1,
-                           flag.data(), qb.data(), ctr.data());
-      CGX_LAUNCH_CHECK();
+      if (n_own) {
+        hipLaunchKernelGGL(k_mg_bu_probe<V>, dim3(grid_for((n_own + 63) / 64, kBlock / 64, 4096)), dim3(kBlock), 0, s,
+                           n_own, rows.off.data<int64_t>(), rows.pos.data<uint32_t>(), dist, pred, bitmap.data(),
+                           voff_d.data(), W, depth1, seg_next.data(), resq.data(), ctr.data());
+        CGX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_mg_bu_residual<V>, dim3(1024), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
+                           rows.pos.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), W, depth1,
+                           seg_next.data(), resq.data(), ctr.data());
+        CGX_LAUNCH_CHECK();
+      }
+      std::swap(seg, seg_next);
+      have_queue = false;
       ++bu_steps;
     } else {
+      if (!have_queue) {  // own bitmap segment -> queue (nf_own vertices)
+        if (nf_own)
+          hipLaunchKernelGGL(k_seg_to_queue, dim3(grid_for(rows.words, kBlock, 4096)), dim3(kBlock), 0, s, seg.data(),
+                             rows.words, qa.data(), &ctr.data()->nconv);
+        CGX_LAUNCH_CHECK();
+        have_queue = true;
+      }
       // 2D: the row's own frontiers to every rank of the row (row-local source ids)
       auto row_counts = rowc.host_allgather<int64_t>(nf_own, s);
       int64_t mx      = 0;
@@ -598,12 +798,12 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
         hipLaunchKernelGGL(k_td_finalize<V>, dim3(capped(hn.next_n)), dim3(kBlock), 0, s, qb.data(),
                            (int64_t)hn.next_n, depth1, dist, pred, best.data(), rows.off.data<int64_t>(), ctr.data());
       CGX_LAUNCH_CHECK();
+      std::swap(qa, qb);
     }
-    auto hn = to_host(ctr.data(), 1, s)[0];
-    nf_own  = (int64_t)hn.next_n;
-    std::swap(qa, qb);
+    auto const cnt = level_counts(to_host(ctr.data(), 1, s)[0]);
+    nf_own         = (int64_t)cnt.first;
     dbuf<double> red(2, s);
-    double loc[2] = {(double)hn.next_n, (double)hn.next_m};
+    double loc[2] = {(double)cnt.first, (double)cnt.second};
     HIP_CHECK(hipMemcpyAsync(red.data(), loc, sizeof(loc), hipMemcpyHostToDevice, s));
     comm.allreduce<double>(red.data(), red.data(), 2, CGX_COMM_SUM, s);
     auto gr = to_host(red.data(), 2, s);

@@ -520,7 +520,8 @@ struct push_args {
   int64_t nitems;
   unsigned int* tile_ctr;   // queue heads, kCtrStride apart, two sets (iteration parity)
   uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
-                            // its sums), 0 = stored whole; nullptr: clear every sum (MG)
+                            // its sums), 0 = stored whole; nullptr: clear every sum
+  int keep_acc;             // k_pr_apply leaves the sums (MG: a reduce-scatter overwrites them)
   int win_bits;
   int64_t nwin;
   // fused apply (single GPU): the block that completes a window applies it
@@ -712,7 +713,12 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
     unsigned long long const g =
         __hip_atomic_exchange(&sa.a.st->fdang, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + eg;
     __hip_atomic_store(&sa.a.st->wticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    update_state<V, E, R>(sa.a, (double)d * kSumScaleInv, (double)g * kSumScaleInv, true);
+    if (sa.a.mg_sums) {  // multi-GPU (one grid row): the rank's sums, allreduced before k_mg_finish
+      sa.a.mg_sums[0] = d;
+      sa.a.mg_sums[1] = g;
+    } else {
+      update_state<V, E, R>(sa.a, (double)d * kSumScaleInv, (double)g * kSumScaleInv, true);
+    }
   }
   if (tid < kQueues) sa.tile_ctr[((sa.parity ^ 1) * kQueues + tid) * kCtrStride] = 0u;
   __syncthreads();
@@ -1099,14 +1105,14 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 #pragma unroll
     for (int j = 0; j < kApplyBatch; ++j) {
       int64_t const vj = v + j * stride;
-      if (sa.acc[vj] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
+      if (!sa.keep_acc && sa.acc[vj] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
       vertex_update_from<V, E, R>(a, (V)vj, (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf, my_diff,
                                   my_dang);
     }
   }
   for (; v < a.nv; v += stride) {
     unsigned long long const f = sa.acc[v];
-    if (f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
+    if (!sa.keep_acc && f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
     vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
@@ -2038,7 +2044,17 @@ struct mg_pr_block {
   int64_t nmax_row = 0, nmax_col = 0;
   pr_push_t pp;
   buffer outw;  // weight_t[n_own]
+  dbuf<int64_t> multi_wins;  // windows summed by several items (their sums are added: cleared per iteration)
+  int64_t nmulti = 0;
 };
+
+// zero the sums of the listed windows (each 2^wb u64 words)
+__global__ void k_clear_windows(unsigned long long* acc, int64_t const* wins, int64_t n, int wb)
+{
+  int64_t const per = int64_t(1) << wb;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * per; i += (int64_t)gridDim.x * blockDim.x)
+    acc[(wins[i >> wb] << wb) + (i & (per - 1))] = 0ull;
+}
 
 template <typename V>
 __global__ void k_mg_block_coo(V const* src, V const* dst, int64_t ne, int64_t const* voff, int P, int C,
@@ -2135,6 +2151,16 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
     hipLaunchKernelGGL(k_to_weight<R>, dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s, own.data(), n_own,
                        blk->outw.data<R>());
   CGX_LAUNCH_CHECK();
+  {  // the windows whose sums are added (several items), cleared after each reduce-scatter
+    auto hm = blk->pp.win_multi.empty() ? std::vector<uint8_t>{}
+                                        : to_host(blk->pp.win_multi.data<uint8_t>(), (size_t)blk->pp.nwin, s);
+    std::vector<int64_t> wl;
+    for (int64_t w = 0; w < (int64_t)hm.size(); ++w)
+      if (hm[w]) wl.push_back(w);
+    blk->nmulti = (int64_t)wl.size();
+    blk->multi_wins.resize(std::max<size_t>(wl.size(), 1), s);
+    to_device(blk->multi_wins.data(), wl.data(), wl.size(), s);
+  }
   HIP_CHECK(hipStreamSynchronize(s));
   mg.pr_block = blk;
   return *blk;
@@ -2324,6 +2350,8 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   a.mg_sums   = sums.data();
   a.x_in      = x_row.data();
   a.x_out     = x_send.data();
+  // fp32 packed push: x~ travels (allgather) and is read as enc_fixed words, as on one GPU
+  a.enc       = blk.pp.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
   int const nblk_init = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 1024);
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
@@ -2335,15 +2363,27 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   push_args<V, E, R> sp{}, sap{};
   sp.a = a;
   set_queue_args(sp, blk.pp, s);
-  sap = sp;
-  // one grid row (R = 1): the block's sums are already the owner's; the apply reads
-  // and re-zeroes them in place, no column collective
+  sp.win_bits = blk.pp.win_bits;
+  // R > 1: the block's sums go through the column reduce-scatter into acc_own, which
+  // the apply reads and leaves (the next reduce-scatter overwrites it); afterwards only
+  // the windows summed by several items are cleared (stored windows are overwritten).
+  // R = 1 (one grid row): the block's sums are already the owner's; as on one GPU the
+  // apply reads them in place and clears the added windows -- or, with 16K windows, the
+  // push applies each window itself (fused_finish) and leaves its (diff, dangling) in
+  // mg_sums
   bool const col_reduce = R_ > 1;
-  sap.acc   = col_reduce ? acc_own.data() : sp.acc;
+  sap = sp;
+  sap.acc       = col_reduce ? acc_own.data() : sp.acc;
+  sap.keep_acc  = col_reduce ? 1 : 0;
+  sap.win_multi = col_reduce ? nullptr : blk.pp.win_multi.data<uint8_t>();
   int const nblk_push  = sp.nitems ? push_blocks(blk.pp.win_bits) : 0;
-  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted);
+  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted, a.enc != 0);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
-  size_t const block_acc_bytes = (size_t)R_ * blk.nmax_col * sizeof(unsigned long long);
+  bool const fused     = !col_reduce && nblk_push && fuse_apply(blk.pp);
+  if (fused) {
+    sp.fuse = 1;
+    sp.nhub = env_is("CGX_PR_HUB", "0") ? 0 : C * blk.nmax_row;  // hub x~ in LDS (row-local source ids)
+  }
 
   // measured-cost queues (calibrate_queues), per rank for its own block: no collective
   bool calibrating = nblk_push && blk.pp.nunits && calibration_wanted(blk.pp);
@@ -2371,15 +2411,21 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       int const chunk = next_chunk(hst, eps, a.max_iter);
       for (int i = 0; i < chunk; ++i) {
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
-        sp.item_ticks = calibrating && launched++ == 0 ? blk.pp.item_ticks.data<uint32_t>() : nullptr;
+        sp.item_ticks = calibrating && launched == 0 ? blk.pp.item_ticks.data<uint32_t>() : nullptr;
+        sp.parity     = (int)(launched & 1);
+        sap.parity    = sp.parity;
+        ++launched;
         if (nblk_push && blk.pp.nunits)
           hipLaunchKernelGGL(mg_pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
         CGX_LAUNCH_CHECK();
         if (col_reduce) {
           ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
-          if (block_acc_bytes) HIP_CHECK(hipMemsetAsync(sp.acc, 0, block_acc_bytes, s));
+          if (blk.nmulti)
+            hipLaunchKernelGGL(k_clear_windows, dim3(grid_for(blk.nmulti << blk.pp.win_bits, kBlock, 8192)),
+                               dim3(kBlock), 0, s, sp.acc, blk.multi_wins.data(), blk.nmulti, blk.pp.win_bits);
+          CGX_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
+        if (!fused) hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
         CGX_LAUNCH_CHECK();
         ctx.world->allreduce<unsigned long long>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
         hipLaunchKernelGGL((k_mg_finish_guarded<V, E, R>), dim3(1), dim3(64), 0, s, a, true);
