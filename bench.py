@@ -277,12 +277,15 @@ def pagerank_traffic(args):
 
 
 def bfs_traffic(args, traversals):
-    """HBM bytes per BFS traversal (all BFS kernels of the child's traversals)."""
-    per = {}
+    """HBM bytes per BFS traversal (all BFS kernels of the child's traversals), and the
+    per-kernel split (KiB per traversal) of each counter."""
+    per, by_kernel = {}, {}
     child = ["--traffic-child", "bfs", "--bfs-scale", str(args.bfs_scale), "--bfs-roots", str(args.bfs_roots)]
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         vals = pmc_pass(ctr, child, BFS_KERNELS)
         per[ctr] = sum(sum(v) for v in vals.values()) / traversals
+        by_kernel[ctr] = {k: round(sum(v) / traversals, 1) for k, v in vals.items() if v}
+    per["per_kernel_kib"] = by_kernel
     return (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0, per
 
 

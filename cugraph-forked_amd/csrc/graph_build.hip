@@ -157,7 +157,7 @@ __global__ void k_bin_starts(E const* offsets, V const* order, int64_t nv, int64
 // ---- per-row weight sums over a CSR (compute_out_weight_sums, pagerank_impl.cuh:158-164)
 // Edge tiles, not rows, are the unit of work, so a hub row (RMAT-24: 406K edges)
 // is spread over ~200 blocks instead of one thread's loop (68.8 ms per call as a
-// thread-per-row kernel).  Tile b = edges [bT, bT + T):
+// thread-per-row kernel).  Tile b = edges [bT, bT + T), T = 4096:
 //  * the rows whose first edge lies in the tile (rows [lbs[b], lbs[b + 1]), found by
 //    one binary search per tile beforehand) are summed from the tile's weights in
 //    LDS, one thread per row, in edge order;
@@ -166,7 +166,8 @@ __global__ void k_bin_starts(E const* offsets, V const* order, int64_t nv, int64
 //  * k_row_sums_spill then adds, for each such row, tail[first tile] + head[...]
 //    in tile order.
 // fp64 sums in a fixed order: deterministic, rounded once to weight_t.
-constexpr int kRsTile = 2048;  // edges per tile (8 per thread)
+constexpr int kRsTile    = 4096;  // edges per tile (16 per thread)
+constexpr int kRsThreads = 256;
 
 template <typename E>
 __global__ void k_row_sum_tile_rows(E const* off, int64_t nv, int64_t ntiles, int64_t* lbs)
@@ -187,42 +188,60 @@ __global__ void k_row_sum_tile_rows(E const* off, int64_t nv, int64_t ntiles, in
   }
 }
 
+// The tile's weights (as loaded, weight_t) and, when the tile owns at most kRsTile rows,
+// their offsets are staged in LDS together -- every global load of the block is issued
+// before the first barrier, so a block makes one round trip to memory
 template <typename E, typename W>
-__global__ __launch_bounds__(256) void k_row_sums_tiles(E const* off, W const* w, int64_t ne, int64_t const* lbs,
-                                                        W* out, double* head, double* tail)
+__global__ __launch_bounds__(kRsThreads) void k_row_sums_tiles(E const* off, W const* w, int64_t ne,
+                                                               int64_t const* lbs, W* out, double* head, double* tail)
 {
-  __shared__ double t_w[kRsTile];
+  __shared__ W t_w[kRsTile];
+  __shared__ int32_t t_off[kRsTile + 1];  // row starts relative to t0, clamped to n + 1 (a spill)
   __shared__ double sm[4];
   int64_t const b  = blockIdx.x;
   int64_t const t0 = b * kRsTile;
   int64_t const t1 = min(ne, t0 + kRsTile);
   int const n      = (int)(t1 - t0);
-#pragma unroll
-  for (int j = 0; j < kRsTile / 256; ++j) {
-    int const i = j * 256 + threadIdx.x;
-    t_w[i]      = i < n ? (double)w[t0 + i] : 0.0;
-  }
-  __syncthreads();
   int64_t const r0 = lbs[b], r1 = lbs[b + 1];
+  int64_t const nr = r1 - r0;
+  bool const staged = nr + 1 <= kRsTile;
+  W wv[kRsTile / kRsThreads];
+#pragma unroll
+  for (int j = 0; j < kRsTile / kRsThreads; ++j) {
+    int const i = j * kRsThreads + threadIdx.x;
+    wv[j]       = i < n ? w[t0 + i] : W(0);
+  }
+  if (staged)
+    for (int64_t i = threadIdx.x; i <= nr; i += kRsThreads) t_off[i] = (int32_t)min((int64_t)off[r0 + i] - t0, (int64_t)n + 1);
+#pragma unroll
+  for (int j = 0; j < kRsTile / kRsThreads; ++j) t_w[j * kRsThreads + threadIdx.x] = wv[j];
+  __syncthreads();
+  auto row_start = [&](int64_t r) { return staged ? t0 + (int64_t)t_off[r - r0] : min((int64_t)off[r], t1 + 1); };
   // head: the edges [t0, first owned row's start) belong to a row that began earlier
-  int64_t const h_end = r0 < r1 ? min((int64_t)off[r0], t1) : t1;
+  int64_t const h_end = nr > 0 ? min(row_start(r0), t1) : t1;
   double hs = 0.0;
-  for (int i = threadIdx.x; i < (int)(h_end - t0); i += 256) hs += t_w[i];
+  for (int i = threadIdx.x; i < (int)(h_end - t0); i += kRsThreads) hs += (double)t_w[i];
   hs = block_sum_256(hs, sm);
   if (threadIdx.x == 0) head[b] = hs;
-  // rows owned by the tile: complete ones summed here, the last may spill past t1
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
-    int64_t const a = (int64_t)off[r], e = (int64_t)off[r + 1];
+  // rows owned by the tile: complete ones summed here (two interleaved sums, in edge
+  // order), the last may spill past t1
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += kRsThreads) {
+    int64_t const a = row_start(r), e = row_start(r + 1);
     if (e > t1) continue;  // the spill row: block partial below
-    double s = 0.0;
-    for (int64_t k = a; k < e; ++k) s += t_w[k - t0];
-    out[r] = static_cast<W>(s);
+    double s0 = 0.0, s1 = 0.0;
+    int64_t k = a;
+    for (; k + 1 < e; k += 2) {
+      s0 += (double)t_w[k - t0];
+      s1 += (double)t_w[k + 1 - t0];
+    }
+    if (k < e) s0 += (double)t_w[k - t0];
+    out[r] = static_cast<W>(s0 + s1);
   }
   double ts = 0.0;
-  bool const spill = r0 < r1 && (int64_t)off[r1] > t1;
+  bool const spill = nr > 0 && row_start(r1) > t1;
   if (spill) {
-    int64_t const a = (int64_t)off[r1 - 1];
-    for (int i = (int)(a - t0) + threadIdx.x; i < n; i += 256) ts += t_w[i];
+    int64_t const a = row_start(r1 - 1);
+    for (int i = (int)(a - t0) + threadIdx.x; i < n; i += kRsThreads) ts += (double)t_w[i];
   }
   ts = block_sum_256(ts, sm);
   if (threadIdx.x == 0) tail[b] = spill ? ts : 0.0;
@@ -587,7 +606,7 @@ void outw_impl(handle_t& h, graph_t& g)
                            nv, ntiles, lbs.data());
         CGX_LAUNCH_CHECK();
         // rows of degree 0 past the last edge belong to no tile's edges: the last tile owns them
-        hipLaunchKernelGGL((k_row_sums_tiles<E, W>), dim3((unsigned)ntiles), dim3(256), 0, s, off,
+        hipLaunchKernelGGL((k_row_sums_tiles<E, W>), dim3((unsigned)ntiles), dim3(kRsThreads), 0, s, off,
                            g.out->weights.data<W>(), ne, lbs.data(), out, head.data(), tail.data());
         CGX_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_row_sums_spill<E, W>), dim3(grid_for(ntiles, kBlock, 8192)), dim3(kBlock), 0, s, off,

@@ -522,6 +522,7 @@ struct push_args {
   uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
                             // its sums), 0 = stored whole; nullptr: clear every sum
   int keep_acc;             // k_pr_apply leaves the sums (MG: a reduce-scatter overwrites them)
+  int maskj;                // packed push: jump entries gather nothing and add nothing (exec-masked)
   int win_bits;
   int64_t nwin;
   // fused apply (single GPU): the block that completes a window applies it
@@ -635,7 +636,9 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
   double const pf   = a.st->pers_factor;
   int64_t const v0  = w << WB;
   int const n       = (int)min((int64_t)1 << WB, a.nv - v0);
-  constexpr int kB = 4;  // (8, two passes for a 16K window: the same time, and the kernel spilled)
+  // vertices per thread and pass, loads first: 4 for 16K windows (8: the same time, and
+  // the kernel spilled); 1 in the 64-VGPR kernels of 4K / 8K windows
+  constexpr int kB = WB >= 14 ? 4 : 1;
   for (int i0 = threadIdx.x; i0 < n; i0 += kB * kPushThreads) {
     unsigned long long f[kB];
     R old[kB], ow[kB];
@@ -724,12 +727,14 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
   __syncthreads();
 }
 
-// the end of an item: fused finish, or the global sums for k_pr_apply
-// (16K windows only: the 64-VGPR kernels of smaller windows would spill around it)
-template <int WB, typename V, typename E, typename R>
+// the end of an item: fused finish, or the global sums for k_pr_apply.  FUSE: the
+// kernel has the fused finish (16K windows: always, decided at run time by sa.fuse;
+// 4K / 8K: a separate instantiation -- in the 64-VGPR kernels the apply's code costs
+// 140-156 B of scratch per lane, so the plain push stays free of it)
+template <int WB, typename V, typename E, typename R, bool FUSE>
 __device__ __forceinline__ void end_item(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
 {
-  if constexpr (WB >= 14) {
+  if constexpr (FUSE) {
     if (sa.fuse) {
       fused_finish<WB, V, E, R>(sa, acc, win_w);
       return;
@@ -819,7 +824,7 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
       n    = nn;
       base = bsn;
     }
-    end_item<WB, V, E, R>(sa, acc, win);
+    end_item<WB, V, E, R, (WB >= 14)>(sa, acc, win);
     // (the item id from LDS too: s_item holds it until thread 0 takes the next)
     if (sa.item_ticks && tid == 0) sa.item_ticks[s_item] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - s_t0);
   }
@@ -908,7 +913,7 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
 // the texture path -- the push's busiest unit (TA 71 %, TD 80 % busy).  Sources are
 // sorted within a window, so almost every segment is all-hub or hub-free; a segment
 // that straddles the boundary gathers from global memory.
-template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false>
+template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -932,6 +937,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   cunit_t* const units = (cunit_t*)sa.units;
   xw_t const* const x  = reinterpret_cast<xw_t const*>(sa.a.x_in);
   uint32_t const nh    = HUB ? (uint32_t)min((int64_t)kHub, sa.nhub) : 0u;
+  bool const maskj     = sa.maskj != 0;
   if constexpr (HUB)
     for (uint32_t i = tid; i < nh; i += kPushThreads) hub[i] = x[i];  // (the first item's barrier publishes it)
   int q                = (int)(blockIdx.x % kQueues);
@@ -968,12 +974,16 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     auto entry = [&](u32x4_t const& w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
     // decode a segment's sources (DPP scan of the deltas + the running base) and
     // issue its 8 gathers; jumps and padding read a valid source and are masked when summed
+    // (maskj: jump lanes issue no gather -- exec-masked, so the texture path skips them)
     auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows]) {
       uint32_t sc[kRows];
+      uint32_t jm = 0;
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const e = entry(w, j);
-        sc[j]            = (e >> WB) == kJump ? (e & kLow) : (e >> WB);
+        bool const jmp   = (e >> WB) == kJump;
+        sc[j]            = jmp ? (e & kLow) : (e >> WB);
+        jm |= (jmp && maskj ? 1u : 0u) << j;
       }
       wave_incl_scan_rows<kRows>(sc);
       uint32_t run = base;
@@ -989,7 +999,8 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
           for (int j = 0; j < kRows; ++j) xv[j] = hub[src[j]];
         } else {
 #pragma unroll
-          for (int j = 0; j < kRows; ++j) xv[j] = x[src[j]];
+          for (int j = 0; j < kRows; ++j)
+            if (!((jm >> j) & 1u)) xv[j] = x[src[j]];
         }
         return;
       }
@@ -997,7 +1008,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       for (int j = 0; j < kRows; ++j) {
         uint32_t const src = run + sc[j];
         run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-        xv[j] = x[src];
+        if (!((jm >> j) & 1u)) xv[j] = x[src];
       }
     };
     auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows]) {
@@ -1008,7 +1019,12 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         unsigned long long fix;
         if constexpr (ENC) fix = dec_fixed(v);
         else fix = fixed_of(v);
-        atomicAdd(&acc[e & kLow], (e >> WB) == kJump ? 0ull : fix);
+        bool const jmp = (e >> WB) == kJump;
+        if (maskj) {
+          if (!jmp) atomicAdd(&acc[e & kLow], fix);
+        } else {
+          atomicAdd(&acc[e & kLow], jmp ? 0ull : fix);
+        }
       }
     };
     // Software pipeline: the next unit's gathers are issued before this unit is
@@ -1041,7 +1057,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       nB = n2;
       bB = __builtin_amdgcn_readfirstlane(b2);
     }
-    end_item<WB, V, E, R>(sa, acc, win);
+    end_item<WB, V, E, R, FUSE>(sa, acc, win);
     // (the item id from LDS too: s_item holds it until thread 0 takes the next)
     if (sa.item_ticks && tid == 0) sa.item_ticks[s_item] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - s_t0);
     if (sa.tl && tid == 0) {
@@ -1059,17 +1075,17 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   }
 }
 
-template <int WB, typename V, typename E, typename R, bool ENC>
+template <int WB, typename V, typename E, typename R, bool ENC, bool FUSE = false>
 __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
 {
-  push_body16<WB, V, E, R, ENC>(sa);
+  push_body16<WB, V, E, R, ENC, false, FUSE>(sa);
 }
 
 // 16K-destination windows: 128 KB of LDS, one block (16 waves) per CU, no 8-waves bound
 template <typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
 {
-  push_body16<14, V, E, R, ENC, true>(sa);
+  push_body16<14, V, E, R, ENC, true, true>(sa);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -1767,24 +1783,29 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 
 }
 
-// fused apply (fused_finish) for a single-GPU schedule: 16K windows, one source group, items,
-// few windows without items (the last block applies those alone); CGX_PR_FUSE=0
-// keeps the separate k_pr_apply (A/B)
+// fused apply (fused_finish): items, few windows without items (the last block applies
+// those alone), packed entries or 16K windows; CGX_PR_FUSE=0 keeps the separate
+// k_pr_apply (A/B); CGX_PR_FUSE_SMALL=1 fuses 4K / 8K windows too (measurement)
 inline bool fuse_apply(pr_push_t const& pp)
 {
-  return pp.win_bits >= 14 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
-         !env_is("CGX_PR_FUSE", "0");
+  bool const small_ok = pp.packed && env_is("CGX_PR_FUSE_SMALL", "1");
+  return (pp.win_bits >= 14 || small_ok) && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 &&
+         !pp.win_items.empty() && !env_is("CGX_PR_FUSE", "0");
 }
 
 // the push kernel for the schedule's window bits and entry format
 template <typename V, typename E, typename R>
-auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
+auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false, bool fuse = false)
 {
   if (pp.win_bits == 14) {
     if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
     return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
   }
   if (pp.packed) {
+    if (fuse) {
+      if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true, true> : k_pr_push16<12, V, E, R, true, true>;
+      return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false, true> : k_pr_push16<12, V, E, R, false, true>;
+    }
     if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true> : k_pr_push16<12, V, E, R, true>;
     return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false> : k_pr_push16<12, V, E, R, false>;
   }
@@ -1924,14 +1945,16 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
 
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  auto pkernel = push_kernel<V, E, R>(adj.pr, push_w, a.enc != 0);
+  bool const fuse = push && fuse_apply(adj.pr);
+  auto pkernel    = push_kernel<V, E, R>(adj.pr, push_w, a.enc != 0, fuse);
   if (push) {
     set_queue_args(sa, adj.pr, s);
     sa.win_multi = adj.pr.win_multi.data<uint8_t>();  // single GPU: stored windows are not cleared
     sa.win_bits  = adj.pr.win_bits;
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
-    sa.fuse    = fuse_apply(adj.pr) ? 1 : 0;
+    sa.fuse    = fuse ? 1 : 0;
+    sa.maskj   = env_is("CGX_PR_MASKJ", "1") ? 1 : 0;  // (A/B)
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // measured-cost queues: the first launch on this schedule records item durations
@@ -2377,9 +2400,9 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   sap.keep_acc  = col_reduce ? 1 : 0;
   sap.win_multi = col_reduce ? nullptr : blk.pp.win_multi.data<uint8_t>();
   int const nblk_push  = sp.nitems ? push_blocks(blk.pp.win_bits) : 0;
-  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted, a.enc != 0);
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   bool const fused     = !col_reduce && nblk_push && fuse_apply(blk.pp);
+  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted, a.enc != 0, fused);
   if (fused) {
     sp.fuse = 1;
     sp.nhub = env_is("CGX_PR_HUB", "0") ? 0 : C * blk.nmax_row;  // hub x~ in LDS (row-local source ids)

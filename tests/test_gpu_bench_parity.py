@@ -96,8 +96,8 @@ def rmat24():
     b.close()
 
 
-@pytest.fixture(scope="module")
-def rmat26():
+@pytest.fixture(scope="function")
+def rmat26():  # (one test uses it: freed at once, before the RMAT-26 Louvain check)
     b = _Bench(26)
     yield b
     b.close()
@@ -263,6 +263,8 @@ def _louvain_q_recomputed(scale):
     del v
     off, idx, w = g.adjacency(h, transposed=False)
     g = None
+    p.trim_device_cache()  # Louvain's level graphs (RMAT-26: > 100 GB) go back to the device
+    torch.cuda.empty_cache()
     V = off.numel() - 1
     c = c.to(torch.int64)
     off64 = off.to(torch.int64)
@@ -280,9 +282,14 @@ def _louvain_q_recomputed(scale):
     # vertex weights k from a prefix sum of 2^32 fixed-point weights (exact integer
     # differences; an index_add_ of E fp64 atomics onto the hub rows took minutes and a
     # fp64 prefix sum loses the small rows' bits to cancellation)
-    wf = torch.round(w.to(torch.float64) * 2.0**32).to(torch.int64)
-    cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=idx.device), torch.cumsum(wf, 0)])
-    del wf
+    cs = torch.zeros(E + 1, dtype=torch.int64, device=idx.device)
+    carry = 0
+    for lo in range(0, E, chunk):
+        hi = min(E, lo + chunk)
+        part = torch.cumsum(torch.round(w[lo:hi].to(torch.float64) * 2.0**32).to(torch.int64), 0)
+        cs[lo + 1:hi + 1] = part + carry
+        carry = int(part[-1]) + carry
+        del part
     k = (cs[off64[1:]] - cs[off64[:-1]]).to(torch.float64) * 2.0**-32
     m = cs[-1].to(torch.float64) * 2.0**-32
     del cs
