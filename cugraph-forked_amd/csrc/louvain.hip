@@ -2350,6 +2350,17 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
   device_sum(plain_f{cur.w.data()}, (size_t)cur.ne, S.scal.data(), S.scratch.data(), s);
   comm.allreduce<double>(S.scal.data(), S.scal.data(), 1, CGX_COMM_SUM, s);
   S.m = to_host_scalar(S.scal.data(), s);
+  {  // the owners' fixed-point cluster weights (scale 2^(60 - e), every |k| and cluster
+     // weight below the total 2^e) assume w >= 0: negative (or NaN) weights are refused
+    dbuf<u64> st(2, s);
+    fill<u64>(st.data(), 2, 0ull, s);
+    if (cur.ne)
+      hipLaunchKernelGGL(k_level_stats, dim3(std::min<unsigned>(blocks(cur.ne), 2048)), dim3(kBlock), 0, s,
+                         cur.w.data(), cur.ne, (double const*)nullptr, (int64_t)0, st.data());
+    CGX_LAUNCH_CHECK();
+    int64_t const bad = comm.host_allreduce<int64_t>(to_host(st.data(), 1, s)[0] ? 1 : 0, CGX_COMM_SUM, s);
+    CGX_EXPECTS(bad == 0, CUGRAPH_NOT_IMPLEMENTED, "multi-GPU Louvain: negative edge weights are not supported");
+  }
 
   bool const trace = std::getenv("CGX_LOUVAIN_TRACE") != nullptr;  // measurement only
   // CGX_LOUVAIN_TRACE=2 (debugging only): every rank syncs and names each phase as it

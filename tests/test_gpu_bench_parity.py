@@ -290,14 +290,21 @@ def _louvain_q_recomputed(scale):
         cs[lo + 1:hi + 1] = part + carry
         carry = int(part[-1]) + carry
         del part
-    k = (cs[off64[1:]] - cs[off64[:-1]]).to(torch.float64) * 2.0**-32
+    kf = cs[off64[1:]] - cs[off64[:-1]]  # vertex weights, 2^32 fixed point
     m = cs[-1].to(torch.float64) * 2.0**-32
     del cs
-    a = torch.zeros(int(c.max()) + 1, dtype=torch.float64, device=idx.device).index_add_(0, c, k)
+    # cluster weights: sort by cluster and segment-sum the fixed-point k (an index_add_
+    # of every vertex onto the few large final clusters serialises on their addresses)
+    cv, order = torch.sort(c)
+    ck = torch.cumsum(kf[order], 0)
+    ends = torch.cat([torch.nonzero(cv[1:] != cv[:-1]).flatten(), torch.tensor([V - 1], device=cv.device)])
+    tot = ck[ends]
+    a = torch.cat([tot[:1], tot[1:] - tot[:-1]]).to(torch.float64) * 2.0**-32
+    del cv, order, ck, ends, tot, kf
     Q = float(internal / m - (a * a).sum() / (m * m))
     print(f"RMAT-{scale} Louvain: V={V} E={E} Q reported {q:.12f} recomputed {Q:.12f}, levels {levels}, "
           f"clusters {int(torch.unique(c).numel())}")
-    del off64, idx, w, c, k, a
+    del off64, idx, w, c, a
     torch.cuda.synchronize()
     p.trim_device_cache()
     torch.cuda.empty_cache()
