@@ -170,6 +170,11 @@ def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want
 def pagerank_leg(p, args, scale, steps, warmup, ctx=None, weighted=False):
     import torch
     h = p.ResourceHandle(ctx.ptr if ctx else None)
+    # module load (the code objects of every kernel on the path) off the clock: a
+    # PageRank on a tiny graph of the same kind, so first_call_ms is the graph's own cost
+    small, _, _ = build_rmat_graph(p, h, 10, weighted=weighted, mg=args.mg)
+    p.pagerank(h, small, None, None, None, None, args.alpha, args.epsilon, 500, False)
+    del small
     barrier(args)
     t0 = time.perf_counter()
     g, _, _ = build_rmat_graph(p, h, scale, weighted=weighted, mg=args.mg)
@@ -625,8 +630,9 @@ def main():
             "graph_build_s": round(r["build_s"], 3),
             "first_call_ms": round(r["first_ms"], 3),
             "first_call_note": ("one cugraph_pagerank on the freshly built graph (out-weight sums, push schedule "
-                                "build, calibration chunk, then the iterations to convergence); steady-state "
-                                f"calls take ms_per_step; first call ran {r['first_iters']} iterations"),
+                                "build, calibration chunk, then the iterations to convergence), after a "
+                                "PageRank on RMAT-10 has loaded the code objects; steady-state calls take "
+                                f"ms_per_step; first call ran {r['first_iters']} iterations"),
             "parallelism": "sg" if world == 1 else f"mg{world}: {grid_name(args, C)}",
         },
         "roofline": {

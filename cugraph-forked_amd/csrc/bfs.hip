@@ -627,100 +627,6 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
   flush_counts(a.ctr, my_n, my_m);
 }
 
-// The probe with two chunks per wave in flight (PAIR): a wave takes chunks c and
-// c + stride together, so the two dependent load chains (visited word + offsets ->
-// neighbour ids -> frontier words) overlap; the visited word and the offsets are loaded
-// together (offsets of visited vertices are read and ignored: one coalesced line).
-template <typename V, typename E, bool VEC>
-__global__ __launch_bounds__(256) void k_bu_probe2(bfs_args<V, E> a, V* res)
-{
-  constexpr int kP = 2;
-  V const nd     = (V)(a.depth + 1);
-  int const lane = threadIdx.x & 63;
-  unsigned long long my_n = 0, my_m = 0;
-  int64_t const nchunks = (a.nv + 63) >> 6;
-  int64_t const stride  = (int64_t)gridDim.x * (kBlock / 64);
-  int64_t const rcap    = residual_cap(a.nv);
-  for (int64_t c0 = blockIdx.x * (int64_t)(kBlock / 64) + (threadIdx.x >> 6); c0 < nchunks; c0 += kP * stride) {
-    int64_t v[kP];
-    bool in[kP], un[kP];
-    uint32_t vw[kP];
-    E beg[kP], end[kP];
-#pragma unroll
-    for (int k = 0; k < kP; ++k) {
-      v[k]  = ((c0 + k * stride) << 6) + lane;
-      in[k] = v[k] < a.nv;
-      vw[k] = in[k] ? a.vis[v[k] >> 5] : 0xffffffffu;
-      beg[k] = in[k] ? a.off[v[k]] : E(0);
-      end[k] = in[k] ? a.off[v[k] + 1] : E(0);
-    }
-    V u[kP][kProbe];
-    int64_t deg[kP];
-#pragma unroll
-    for (int k = 0; k < kP; ++k) {
-      un[k]  = in[k] && !((vw[k] >> (uint32_t(v[k]) & 31u)) & 1u);
-      deg[k] = un[k] ? (int64_t)(end[k] - beg[k]) : 0;
-      E const b0 = deg[k] > 0 ? beg[k] : E(0);  // (no list: read entry 0, never past the end)
-      if constexpr (VEC && sizeof(V) == 4 && kProbe == 8) {
-        E const a0     = b0 & ~E(3);
-        int const sh   = (int)(b0 - a0);
-        v4i_t const* p = reinterpret_cast<v4i_t const*>(a.idx + a0);
-        v4i_t const q0 = p[0], q1 = p[1], q2 = p[2];
-        int const wv[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-#pragma unroll
-        for (int t = 0; t < kProbe; ++t)
-          u[k][t] = (V)(sh == 0 ? wv[t] : sh == 1 ? wv[t + 1] : sh == 2 ? wv[t + 2] : wv[t + 3]);
-#pragma unroll
-        for (int t = 1; t < kProbe; ++t) u[k][t] = t < deg[k] ? u[k][t] : u[k][0];
-      } else {
-#pragma unroll
-        for (int t = 0; t < kProbe; ++t) u[k][t] = a.idx[b0 + (t < deg[k] ? t : 0)];
-      }
-    }
-    uint32_t fw[kP][kProbe];  // every frontier word of both chunks first
-#pragma unroll
-    for (int k = 0; k < kP; ++k)
-#pragma unroll
-      for (int t = 0; t < kProbe; ++t) fw[k][t] = a.fr[u[k][t] >> 5];
-#pragma unroll
-    for (int k = 0; k < kP; ++k) {
-      int64_t const c = c0 + k * stride;
-      if (c >= nchunks) break;  // wave-uniform
-      uint32_t hm = 0;
-#pragma unroll
-      for (int t = 0; t < kProbe; ++t) hm |= (t < deg[k] ? (fw[k][t] >> (uint32_t(u[k][t]) & 31u)) & 1u : 0u) << t;
-      V par = 0;
-#pragma unroll
-      for (int t = kProbe - 1; t >= 0; --t)
-        if ((hm >> t) & 1u) par = u[k][t];
-      bool const hit  = hm != 0;
-      bool const more = !hit && deg[k] > kProbe;
-      if (hit) {
-        a.dist[v[k]] = nd;
-        if (a.pred) a.pred[v[k]] = par;
-        my_n += 1;
-        my_m += (unsigned long long)deg[k];
-      }
-      unsigned long long const hb = __ballot(hit);
-      if ((lane & 31) == 0 && in[k]) {
-        uint32_t const b = (uint32_t)(hb >> lane);
-        if (b) a.vis[v[k] >> 5] = vw[k] | b;
-        a.nxt[v[k] >> 5] = b;
-      }
-      unsigned long long const mm = __ballot(more);
-      if (mm) {
-        unsigned long long base = 0;
-        int const leader = __ffsll((long long)mm) - 1;
-        int const sq     = (int)(c % kCtrParts);
-        if (lane == leader) base = atomicAdd(&a.ctr->part[sq][2], (unsigned long long)__popcll(mm));
-        base = __shfl(base, leader, 64);
-        if (more) res[sq * rcap + (int64_t)base + __popcll(mm & ((1ull << lane) - 1ull))] = (V)v[k];
-      }
-    }
-  }
-  flush_counts(a.ctr, my_n, my_m);
-}
-
 template <typename V, typename E>
 __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* res)
 {
@@ -1034,7 +940,6 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // k_bu_probe 133.6 -> 129.5 us average; CGX_BFS_PROBE_VEC=0: dword gathers, A/B)
     char const* pv       = std::getenv("CGX_BFS_PROBE_VEC");
     bool const probe_vec = adj.idx_padded && !(pv && std::string(pv) == "0");
-    bool const probe_pair = std::getenv("CGX_BFS_PROBE2") != nullptr;  // (A/B: two chunks per wave)
     // Grid sizes: every block ends with same-address atomics on the level counters,
     // which serialise at the memory side (≈8 ns each): RMAT-24 MTEPS with the probe
     // on 512 / 1024 / 2048 / 8192 / 32768 blocks: 166K / 173K / 168K / 148K / 101K
@@ -1076,14 +981,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         bool const probe_path = a.order == nullptr && !one_pass_bu;
         if (!probe_path) HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));  // the probe writes every word
         if (probe_path) {  // probe + residual (identity order)
+          // (measured and rejected: two chunks per wave in flight, 337K vs 370K MTEPS on
+          // RMAT-24 -- the probe is not bound by one wave's load chain)
           unsigned const pg = grid_for((nv + 63) / 64, kBlock / 64, probe_grid);
-          if (probe_pair) {
-            if (probe_vec) hipLaunchKernelGGL((k_bu_probe2<V, E, true>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
-            else hipLaunchKernelGGL((k_bu_probe2<V, E, false>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
-          } else {
-            if (probe_vec) hipLaunchKernelGGL((k_bu_probe<V, E, true>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
-            else hipLaunchKernelGGL((k_bu_probe<V, E, false>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
-          }
+          if (probe_vec) hipLaunchKernelGGL((k_bu_probe<V, E, true>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
+          else hipLaunchKernelGGL((k_bu_probe<V, E, false>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
           CGX_LAUNCH_CHECK();
           hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, a, qb[0].data());
         } else {

@@ -522,7 +522,6 @@ struct push_args {
   uint8_t const* win_multi; // per window: 1 = summed by several items (k_pr_apply clears
                             // its sums), 0 = stored whole; nullptr: clear every sum
   int keep_acc;             // k_pr_apply leaves the sums (MG: a reduce-scatter overwrites them)
-  int maskj;                // packed push: jump entries gather nothing and add nothing (exec-masked)
   int win_bits;
   int64_t nwin;
   // fused apply (single GPU): the block that completes a window applies it
@@ -728,9 +727,9 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
 }
 
 // the end of an item: fused finish, or the global sums for k_pr_apply.  FUSE: the
-// kernel has the fused finish (16K windows: always, decided at run time by sa.fuse;
-// 4K / 8K: a separate instantiation -- in the 64-VGPR kernels the apply's code costs
-// 140-156 B of scratch per lane, so the plain push stays free of it)
+// kernel has the fused finish (16K windows only, decided at run time by sa.fuse).  In
+// the 64-VGPR kernels of 4K / 8K windows its code costs 140-156 B of scratch per lane:
+// measured on RMAT-22, 0.274 against 0.176 ms/iteration unfused (same box)
 template <int WB, typename V, typename E, typename R, bool FUSE>
 __device__ __forceinline__ void end_item(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
 {
@@ -923,6 +922,9 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   constexpr uint32_t kLow   = (1u << WB) - 1;
   constexpr int kRows       = kSegEntries / 64;
   static_assert(kRows == kPerThread, "a wave segment is one unit row per thread");
+  // jump lanes skip the gather too where registers allow (16K windows; the 64-VGPR
+  // kernels of 4K / 8K windows spill with the mask live, so there they only skip the add)
+  constexpr bool kMaskGather = WB >= 14;
   __shared__ unsigned long long acc[kWin];
   constexpr int kHub = HUB ? kHubBytes / (int)sizeof(xw_t) : 1;
   __shared__ xw_t hub[kHub];
@@ -937,7 +939,6 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   cunit_t* const units = (cunit_t*)sa.units;
   xw_t const* const x  = reinterpret_cast<xw_t const*>(sa.a.x_in);
   uint32_t const nh    = HUB ? (uint32_t)min((int64_t)kHub, sa.nhub) : 0u;
-  bool const maskj     = sa.maskj != 0;
   if constexpr (HUB)
     for (uint32_t i = tid; i < nh; i += kPushThreads) hub[i] = x[i];  // (the first item's barrier publishes it)
   int q                = (int)(blockIdx.x % kQueues);
@@ -974,7 +975,9 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     auto entry = [&](u32x4_t const& w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
     // decode a segment's sources (DPP scan of the deltas + the running base) and
     // issue its 8 gathers; jumps and padding read a valid source and are masked when summed
-    // (maskj: jump lanes issue no gather -- exec-masked, so the texture path skips them)
+    // Jump and padding lanes issue no gather and no LDS add (exec-masked: the texture
+    // path and the LDS banks skip them): RMAT-22 / 24 / 26 2-4 / 2-5 / 1.6 % faster per
+    // iteration than gathering a valid source and adding 0 (same box)
     auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows]) {
       uint32_t sc[kRows];
       uint32_t jm = 0;
@@ -983,7 +986,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         uint32_t const e = entry(w, j);
         bool const jmp   = (e >> WB) == kJump;
         sc[j]            = jmp ? (e & kLow) : (e >> WB);
-        jm |= (jmp && maskj ? 1u : 0u) << j;
+        if constexpr (kMaskGather) jm |= (jmp ? 1u : 0u) << j;
       }
       wave_incl_scan_rows<kRows>(sc);
       uint32_t run = base;
@@ -1019,12 +1022,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         unsigned long long fix;
         if constexpr (ENC) fix = dec_fixed(v);
         else fix = fixed_of(v);
-        bool const jmp = (e >> WB) == kJump;
-        if (maskj) {
-          if (!jmp) atomicAdd(&acc[e & kLow], fix);
-        } else {
-          atomicAdd(&acc[e & kLow], jmp ? 0ull : fix);
-        }
+        if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
       }
     };
     // Software pipeline: the next unit's gathers are issued before this unit is
@@ -1075,10 +1073,10 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   }
 }
 
-template <int WB, typename V, typename E, typename R, bool ENC, bool FUSE = false>
+template <int WB, typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R> sa)
 {
-  push_body16<WB, V, E, R, ENC, false, FUSE>(sa);
+  push_body16<WB, V, E, R, ENC>(sa);
 }
 
 // 16K-destination windows: 128 KB of LDS, one block (16 waves) per CU, no 8-waves bound
@@ -1783,29 +1781,23 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 
 }
 
-// fused apply (fused_finish): items, few windows without items (the last block applies
-// those alone), packed entries or 16K windows; CGX_PR_FUSE=0 keeps the separate
-// k_pr_apply (A/B); CGX_PR_FUSE_SMALL=1 fuses 4K / 8K windows too (measurement)
+// fused apply (fused_finish): 16K windows, items, few windows without items (the last
+// block applies those alone); CGX_PR_FUSE=0 keeps the separate k_pr_apply (A/B)
 inline bool fuse_apply(pr_push_t const& pp)
 {
-  bool const small_ok = pp.packed && env_is("CGX_PR_FUSE_SMALL", "1");
-  return (pp.win_bits >= 14 || small_ok) && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 &&
-         !pp.win_items.empty() && !env_is("CGX_PR_FUSE", "0");
+  return pp.win_bits >= 14 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
+         !env_is("CGX_PR_FUSE", "0");
 }
 
 // the push kernel for the schedule's window bits and entry format
 template <typename V, typename E, typename R>
-auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false, bool fuse = false)
+auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
   if (pp.win_bits == 14) {
     if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
     return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
   }
   if (pp.packed) {
-    if (fuse) {
-      if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true, true> : k_pr_push16<12, V, E, R, true, true>;
-      return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false, true> : k_pr_push16<12, V, E, R, false, true>;
-    }
     if (enc) return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, true> : k_pr_push16<12, V, E, R, true>;
     return pp.win_bits == 13 ? k_pr_push16<13, V, E, R, false> : k_pr_push16<12, V, E, R, false>;
   }
@@ -1946,7 +1938,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
   bool const fuse = push && fuse_apply(adj.pr);
-  auto pkernel    = push_kernel<V, E, R>(adj.pr, push_w, a.enc != 0, fuse);
+  auto pkernel    = push_kernel<V, E, R>(adj.pr, push_w, a.enc != 0);
   if (push) {
     set_queue_args(sa, adj.pr, s);
     sa.win_multi = adj.pr.win_multi.data<uint8_t>();  // single GPU: stored windows are not cleared
@@ -1954,7 +1946,6 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
     sa.fuse    = fuse ? 1 : 0;
-    sa.maskj   = env_is("CGX_PR_MASKJ", "1") ? 1 : 0;  // (A/B)
     sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // measured-cost queues: the first launch on this schedule records item durations
@@ -2402,7 +2393,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   int const nblk_push  = sp.nitems ? push_blocks(blk.pp.win_bits) : 0;
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
   bool const fused     = !col_reduce && nblk_push && fuse_apply(blk.pp);
-  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted, a.enc != 0, fused);
+  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted, a.enc != 0);
   if (fused) {
     sp.fuse = 1;
     sp.nhub = env_is("CGX_PR_HUB", "0") ? 0 : C * blk.nmax_row;  // hub x~ in LDS (row-local source ids)

@@ -1,0 +1,73 @@
+"""One-rank RCCL MG PageRank against single-GPU PageRank on the same graph (measurement
+aid, not product).
+
+usage: python scripts/mg_one_rank.py [SCALE]
+One process, torch.distributed world of 1, the library's RCCL communicators
+(pylibcugraph.comms.init_rccl(1)): the MG path's every step -- x~ allgather, push,
+apply or fused apply, u64 allreduce, state kernel -- runs through RCCL with one rank.
+Prints ms per iteration (HIP events on the library stream, 16-iteration calls) for SG
+and MG, their ratio, and whether the ranks agree bit for bit.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cugraph-forked_amd"))
+sys.path.insert(0, ROOT)
+
+
+def timed(p, h, g, calls=5):
+    def run():
+        try:
+            p.pagerank(h, g, None, None, None, None, 0.85, 0.0, 16, False)
+        except RuntimeError as e:
+            if "converge" not in str(e):
+                raise
+    for _ in range(2):
+        run()
+    h.set_profiling(True)
+    ms, n = 0.0, 0
+    for _ in range(calls):
+        run()
+        ms += h.last_hot_kernel_ms()
+        n += h.last_hot_kernel_launches()
+    h.set_profiling(False)
+    return ms / max(n, 1)
+
+
+def main():
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import bench
+    import pylibcugraph as p
+    scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(bench.free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    torch.cuda.set_device(0)
+    h = p.ResourceHandle()
+    g, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
+    sg_ms = timed(p, h, g)
+    v, x = p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False)
+    sg = dict(zip(v.cpu().numpy().tolist(), x.cpu().numpy().view(np.int32).tolist()))
+    it_sg = h.last_iterations()
+    g = None
+    p.trim_device_cache()
+    ctx = p.comms.init_rccl(1)
+    hm = p.ResourceHandle(ctx.ptr)
+    gm, _, _ = bench.build_rmat_graph(p, hm, scale, transposed=True, mg=(0, 1))
+    mg_ms = timed(p, hm, gm)
+    vm, xm = p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False)
+    it_mg = hm.last_iterations()
+    same = all(sg[a] == b for a, b in zip(vm.cpu().numpy().tolist(), xm.cpu().numpy().view(np.int32).tolist()))
+    print(f"RMAT-{scale}: SG {sg_ms:.4f} ms/iteration, 1-rank RCCL MG {mg_ms:.4f} ms/iteration "
+          f"(ratio {mg_ms / sg_ms:.3f}); iterations SG {it_sg} MG {it_mg}; bitwise equal {same}", flush=True)
+    gm = None
+    hm = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

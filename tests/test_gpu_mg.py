@@ -297,6 +297,44 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     dist.destroy_process_group()
 
 
+def _louvain_negative_worker(rank, world, port, C):
+    """A negative edge weight: MG Louvain's owner-side fixed-point cluster weights assume
+    w >= 0, so every rank must refuse the graph with the same error (no rank may go on
+    into a collective the others skip)."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    _rank_setup(port, rank)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pylibcugraph as plc
+    s, d, w = _graph(8, True)
+    w = w.astype(np.float32)
+    w[5] = -0.5  # one entry only (the graph is no longer symmetric in w: irrelevant here)
+    E = s.size
+    lo, hi = _slice(rank, world, E)
+    ctx = plc.comms.init_torch(C)
+    h = plc.ResourceHandle(ctx.ptr)
+    dev = lambda a, t: torch.as_tensor(np.ascontiguousarray(a).astype(t), device="cuda")  # noqa: E731
+    G = plc.MGGraph(h, plc.GraphProperties(is_symmetric=True, is_multigraph=False), dev(s[lo:hi], np.int32),
+                    dev(d[lo:hi], np.int32), dev(w[lo:hi], np.float32), store_transposed=False, num_edges=E)
+    with pytest.raises(RuntimeError, match="negative"):
+        plc.louvain(h, G, 100, 1.0, False)
+    dist.barrier()
+    h = None
+    G = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+def test_mg_louvain_negative_weight_refused():
+    _spawn(_louvain_negative_worker, (2, _free_port(), 2), 2)
+
+
 @pytest.mark.parametrize("world,C,integer", [(2, 2, True), (3, 3, True), (4, 2, True), (2, 1, False)])
 def test_mg_louvain_levels_vs_oracle(world, C, integer):
     _spawn(_louvain_worker, (world, _free_port(), C, 10, integer), world)
