@@ -912,7 +912,7 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
 // the texture path -- the push's busiest unit (TA 71 %, TD 80 % busy).  Sources are
 // sorted within a window, so almost every segment is all-hub or hub-free; a segment
 // that straddles the boundary gathers from global memory.
-template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false>
+template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false, int MASK = 1>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -924,7 +924,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   static_assert(kRows == kPerThread, "a wave segment is one unit row per thread");
   // jump lanes skip the gather too where registers allow (16K windows; the 64-VGPR
   // kernels of 4K / 8K windows spill with the mask live, so there they only skip the add)
-  constexpr bool kMaskGather = WB >= 14;
+  constexpr bool kMaskGather = MASK >= 2;  // (MASK: 0 none, 1 the add, 2 the gather and the add; A/B)
   __shared__ unsigned long long acc[kWin];
   constexpr int kHub = HUB ? kHubBytes / (int)sizeof(xw_t) : 1;
   __shared__ xw_t hub[kHub];
@@ -1022,7 +1022,11 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         unsigned long long fix;
         if constexpr (ENC) fix = dec_fixed(v);
         else fix = fixed_of(v);
-        if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
+        if constexpr (MASK >= 1) {
+          if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
+        } else {
+          atomicAdd(&acc[e & kLow], (e >> WB) == kJump ? 0ull : fix);
+        }
       }
     };
     // Software pipeline: the next unit's gathers are issued before this unit is
@@ -1083,7 +1087,12 @@ __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R
 template <typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
 {
-  push_body16<14, V, E, R, ENC, true, true>(sa);
+  push_body16<14, V, E, R, ENC, true, true, 2>(sa);
+}
+template <typename V, typename E, typename R, bool ENC, int MASK>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14m(push_args<V, E, R> sa)
+{
+  push_body16<14, V, E, R, ENC, true, true, MASK>(sa);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -1794,7 +1803,13 @@ template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
   if (pp.win_bits == 14) {
-    if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
+    if (pp.packed) {
+      if (env_is("CGX_PR_MASK", "0"))  // (A/B)
+        return enc ? k_pr_push16_w14m<V, E, R, true, 0> : k_pr_push16_w14m<V, E, R, false, 0>;
+      if (env_is("CGX_PR_MASK", "1"))
+        return enc ? k_pr_push16_w14m<V, E, R, true, 1> : k_pr_push16_w14m<V, E, R, false, 1>;
+      return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
+    }
     return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
   }
   if (pp.packed) {
