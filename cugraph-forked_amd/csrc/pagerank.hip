@@ -912,7 +912,7 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
 // the texture path -- the push's busiest unit (TA 71 %, TD 80 % busy).  Sources are
 // sorted within a window, so almost every segment is all-hub or hub-free; a segment
 // that straddles the boundary gathers from global memory.
-template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false, int MASK = 1>
+template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -922,9 +922,6 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   constexpr uint32_t kLow   = (1u << WB) - 1;
   constexpr int kRows       = kSegEntries / 64;
   static_assert(kRows == kPerThread, "a wave segment is one unit row per thread");
-  // jump lanes skip the gather too where registers allow (16K windows; the 64-VGPR
-  // kernels of 4K / 8K windows spill with the mask live, so there they only skip the add)
-  constexpr bool kMaskGather = MASK >= 2;  // (MASK: 0 none, 1 the add, 2 the gather and the add; A/B)
   __shared__ unsigned long long acc[kWin];
   constexpr int kHub = HUB ? kHubBytes / (int)sizeof(xw_t) : 1;
   __shared__ xw_t hub[kHub];
@@ -974,19 +971,16 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
     auto seg_n = [&](int64_t u) { return (int)(units[u].k1 - units[u].k0) - wave * kSegEntries; };
     auto entry = [&](u32x4_t const& w, int j) { return (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
     // decode a segment's sources (DPP scan of the deltas + the running base) and
-    // issue its 8 gathers; jumps and padding read a valid source and are masked when summed
-    // Jump and padding lanes issue no gather and no LDS add (exec-masked: the texture
-    // path and the LDS banks skip them): RMAT-22 / 24 / 26 2-4 / 2-5 / 1.6 % faster per
-    // iteration than gathering a valid source and adding 0 (same box)
+    // issue its 8 gathers; jumps and padding read a valid source and add nothing to LDS
+    // (an exec-masked add instead of adding 0: RMAT-24 0.577-0.595 vs 0.596-0.599
+    // ms/iteration, same box).  Masking their gathers too was slower (RMAT-24 0.640,
+    // RMAT-26 3.09 vs 3.00 ms): the mask costs registers and exec switches in the loop
     auto gather = [&](u32x4_t const& w, uint32_t base, xw_t (&xv)[kRows]) {
       uint32_t sc[kRows];
-      uint32_t jm = 0;
 #pragma unroll
       for (int j = 0; j < kRows; ++j) {
         uint32_t const e = entry(w, j);
-        bool const jmp   = (e >> WB) == kJump;
-        sc[j]            = jmp ? (e & kLow) : (e >> WB);
-        if constexpr (kMaskGather) jm |= (jmp ? 1u : 0u) << j;
+        sc[j]            = (e >> WB) == kJump ? (e & kLow) : (e >> WB);
       }
       wave_incl_scan_rows<kRows>(sc);
       uint32_t run = base;
@@ -1002,8 +996,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
           for (int j = 0; j < kRows; ++j) xv[j] = hub[src[j]];
         } else {
 #pragma unroll
-          for (int j = 0; j < kRows; ++j)
-            if (!((jm >> j) & 1u)) xv[j] = x[src[j]];
+          for (int j = 0; j < kRows; ++j) xv[j] = x[src[j]];
         }
         return;
       }
@@ -1011,7 +1004,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       for (int j = 0; j < kRows; ++j) {
         uint32_t const src = run + sc[j];
         run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
-        if (!((jm >> j) & 1u)) xv[j] = x[src];
+        xv[j] = x[src];
       }
     };
     auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows]) {
@@ -1022,11 +1015,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         unsigned long long fix;
         if constexpr (ENC) fix = dec_fixed(v);
         else fix = fixed_of(v);
-        if constexpr (MASK >= 1) {
-          if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
-        } else {
-          atomicAdd(&acc[e & kLow], (e >> WB) == kJump ? 0ull : fix);
-        }
+        if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
       }
     };
     // Software pipeline: the next unit's gathers are issued before this unit is
@@ -1087,12 +1076,7 @@ __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R
 template <typename V, typename E, typename R, bool ENC>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
 {
-  push_body16<14, V, E, R, ENC, true, true, 2>(sa);
-}
-template <typename V, typename E, typename R, bool ENC, int MASK>
-__global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14m(push_args<V, E, R> sa)
-{
-  push_body16<14, V, E, R, ENC, true, true, MASK>(sa);
+  push_body16<14, V, E, R, ENC, true, true>(sa);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -1803,13 +1787,7 @@ template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
   if (pp.win_bits == 14) {
-    if (pp.packed) {
-      if (env_is("CGX_PR_MASK", "0"))  // (A/B)
-        return enc ? k_pr_push16_w14m<V, E, R, true, 0> : k_pr_push16_w14m<V, E, R, false, 0>;
-      if (env_is("CGX_PR_MASK", "1"))
-        return enc ? k_pr_push16_w14m<V, E, R, true, 1> : k_pr_push16_w14m<V, E, R, false, 1>;
-      return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
-    }
+    if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
     return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
   }
   if (pp.packed) {
