@@ -90,17 +90,6 @@ __device__ __forceinline__ void fold_parts(bfs_ctr* c, bool zero, unsigned long 
   m = pm + c->next_m;
 }
 
-// level counters -> the handle's pinned host block (A/B form of the poll)
-__global__ void k_publish_ctr(bfs_ctr* ctr, bfs_ctr_hdr* host)
-{
-  unsigned long long n, m;
-  fold_parts(ctr, false, n, m);
-  int const i = threadIdx.x;
-  unsigned long long v = i < 3 ? ctr->qlen[i] : (i == 3 ? n : m);
-  if (i < 5)
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(host) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // the level counters (then zeroed for the next level: no memset launch per level)
 // and the source check flag (pad[1]), then seq (the host's poll word, pad[0]) behind
 // a system fence.  ctr_b: a second level's counters (a speculative top-down level)
@@ -146,11 +135,12 @@ __device__ __forceinline__ bool cas_claim(V* dist, V v, V nd)
   }
 }
 
+// unsigned: predecessors start at -1 (all ones), the unreached value of the result
 template <typename V>
 __device__ __forceinline__ void atomic_min_v(V* p, V x)
 {
-  if constexpr (sizeof(V) == 4) atomicMin(reinterpret_cast<int*>(p), (int)x);
-  else atomicMin(reinterpret_cast<long long*>(p), (long long)x);
+  if constexpr (sizeof(V) == 4) atomicMin(reinterpret_cast<unsigned*>(p), (unsigned)x);
+  else atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)x);
 }
 
 // wave-aggregated append: every active lane with `take` gets a distinct slot
@@ -172,7 +162,8 @@ struct bfs_args {
   E const* off;
   V const* idx;
   V* dist;
-  V* pred;  // nullptr when predecessors are not requested
+  V* pred;  // nullptr when predecessors are not requested; -1 until set
+  V const* nmap;  // internal -> external ids (nullptr: not renumbered); predecessors are stored external
   uint32_t* vis;
   uint32_t* fr;   // bottom-up: current frontier bitmap
   uint32_t* nxt;  // bottom-up: next frontier bitmap
@@ -369,10 +360,15 @@ __global__ __launch_bounds__(256) void k_topdown(bfs_args<V, E> a)
 }
 
 // mark the next queues as visited (their distances were set by the claim);
-// cdev: read the queue lengths on the device (a level the host has not read yet)
+// cdev: read the queue lengths on the device (a level the host has not read yet).
+// pred + nmap: the queues are a finished top-down level's discoveries, whose
+// predecessors (smallest internal id, atomicMin) become external ids here -- every
+// such level's output passes through exactly one k_mark_queues (or the final one
+// after the loop), so the traversal needs no finishing pass over all vertices
 template <typename V>
 __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, unsigned long long n1, V const* q2,
-                              unsigned long long n2, uint32_t* vis, uint32_t* fr, bfs_ctr const* cdev = nullptr)
+                              unsigned long long n2, uint32_t* vis, uint32_t* fr, bfs_ctr const* cdev, V* pred,
+                              V const* nmap)
 {
   if (cdev) {
     n0 = cdev->qlen[0];
@@ -386,6 +382,10 @@ __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, u
     uint32_t bit = 1u << (uint32_t(v) & 31u);
     atomicOr(vis + (v >> 5), bit);
     if (fr) atomicOr(fr + (v >> 5), bit);
+    if (nmap) {  // (sources keep -1)
+      V const p = pred[v];
+      if (p != (V)-1) pred[v] = nmap[p];
+    }
   }
 }
 
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
           if (tid == h) {
             V u     = a.idx[e];
             a.dist[v] = nd;
-            if (a.pred) a.pred[v] = u;
+            if (a.pred) a.pred[v] = a.nmap ? a.nmap[u] : u;
             atomicOr(a.nxt + (v >> 5), bit);
             atomicOr(a.vis + (v >> 5), bit);
             my_n += 1;
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
           int first = __ffsll((long long)gm) - 1;
           if (lane == first) {
             a.dist[v] = nd;
-            if (a.pred) a.pred[v] = u;
+            if (a.pred) a.pred[v] = a.nmap ? a.nmap[u] : u;
             if (agg) {
               atomicOr(&s_bits[(int64_t(v) >> 5) - (p0 >> 5)], bit);
             } else {
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
     }
     if (hit) {
       a.dist[v] = nd;
-      if (a.pred) a.pred[v] = par;
+      if (a.pred) a.pred[v] = a.nmap ? a.nmap[par] : par;
       my_n += 1;
       my_m += (unsigned long long)deg;
     }
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
         if (lane == __ffsll((long long)gm) - 1) {
           uint32_t const bit = 1u << (uint32_t(v) & 31u);
           a.dist[v] = nd;
-          if (a.pred) a.pred[v] = u;
+          if (a.pred) a.pred[v] = a.nmap ? a.nmap[u] : u;
           atomicOr(a.nxt + (v >> 5), bit);
           atomicOr(a.vis + (v >> 5), bit);
           my_n += 1;
@@ -678,30 +678,8 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
   flush_counts(a.ctr, my_n, my_m);
 }
 
-// unreached -> -1, reached -> the external id of the predecessor (nmap: the
-// graph's number map, nullptr when not renumbered), one pass
-template <typename V>
-__global__ void k_finish_pred(V* pred, size_t n, V none, V const* nmap)
-{
-  constexpr int kB    = 4;  // elements per thread, loads (and number-map gathers) issued first
-  size_t const stride = (size_t)gridDim.x * blockDim.x;
-  size_t i            = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  for (; i + (kB - 1) * stride < n; i += kB * stride) {
-    V p[kB];
-#pragma unroll
-    for (int j = 0; j < kB; ++j) p[j] = pred[i + j * stride];
-#pragma unroll
-    for (int j = 0; j < kB; ++j) p[j] = p[j] == none ? (V)-1 : (nmap ? nmap[p[j]] : p[j]);
-#pragma unroll
-    for (int j = 0; j < kB; ++j) pred[i + j * stride] = p[j];
-  }
-  for (; i < n; i += stride) {
-    V const q = pred[i];
-    pred[i]   = q == none ? (V)-1 : (nmap ? nmap[q] : q);
-  }
-}
-
-// 4-byte ids: four predecessors per lane through 16-byte loads and stores, kQ quads
+// (A/B, CGX_BFS_PRED_FINISH=1: predecessors kept internal during the traversal and
+// translated by this pass afterwards.)  4-byte ids: four predecessors per lane through 16-byte loads and stores, kQ quads
 // per lane with every load (and then every number-map gather) issued before the
 // first use, so a lane makes one dependent round trip instead of kQ
 __global__ __launch_bounds__(256) void k_finish_pred4(int* pred, size_t n, int none, int const* nmap)
@@ -740,7 +718,7 @@ __global__ __launch_bounds__(256) void k_finish_pred4(int* pred, size_t n, int n
   }
 }
 
-// dist / pred = INF and the three bitmaps cleared in one launch (was 2 fills + 3 memsets)
+// dist = INF, pred = -1 and the three bitmaps cleared in one launch (was 2 fills + 3 memsets)
 template <typename V>
 __global__ void k_bfs_setup(V* dist, V* pred, int64_t nv, V inf, uint32_t* vis, uint32_t* fr, uint32_t* nxt,
                             int64_t nwords, int* bad)
@@ -749,7 +727,7 @@ __global__ void k_bfs_setup(V* dist, V* pred, int64_t nv, V inf, uint32_t* vis, 
   if (blockIdx.x == 0 && threadIdx.x == 0) *bad = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += stride) {
     dist[v] = inf;
-    if (pred) pred[v] = inf;
+    if (pred) pred[v] = (V)-1;
   }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords; i += stride) {
     vis[i] = 0u;
@@ -835,20 +813,17 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   a.ctr   = ctr.data();
   a.nv    = nv;
   a.order = (dir_opt && !adj.degree_sorted) ? adj.order.data<V>() : nullptr;
+  bool const finish_pass = std::getenv("CGX_BFS_PRED_FINISH") != nullptr && sizeof(V) == 4;  // A/B
+  a.nmap  = (pred && g.renumbered && !finish_pass) ? g.number_map.data<V>() : nullptr;
   a.items = dir_opt ? adj.items.data<work_item>() : nullptr;
 
-  // A/B (CGX_BFS_PUBLISH_KERNEL=1): counters published by k_publish_ctr instead of a
-  // D2H copy, both with a stream synchronize -- RMAT-24 1.168 vs 1.172 ms per
-  // traversal over 3 pairs, within noise
-  bool const ctr_memcpy = std::getenv("CGX_BFS_PUBLISH_KERNEL") != nullptr;
-  // Default: k_publish_seq into the handle's coherent block and a host spin on its
-  // sequence word -- no hipStreamSynchronize per level (CGX_BFS_SYNC=1: the
-  // memcpy + synchronize form, A/B)
-  bool const poll = std::getenv("CGX_BFS_SYNC") == nullptr && !ctr_memcpy;
-  bfs_ctr_hdr* pctr = poll ? h.polled_as<bfs_ctr_hdr>() : nullptr;  // [0]: a level, [1]: a speculative level
-  // ctr_b / src_m: see k_publish_seq (poll mode only)
+  // Level counters: k_publish_seq into the handle's coherent block and a host spin on
+  // its sequence word -- no hipStreamSynchronize per level (measured against a D2H
+  // copy + synchronize per level: that form was removed)
+  bfs_ctr_hdr* pctr = h.polled_as<bfs_ctr_hdr>();  // [0]: a level, [1]: a speculative level
+  // ctr_b / src_m: see k_publish_seq
   auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr* src_m = nullptr) {
-    if (poll) {
+    {
       unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
       hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m);
       CGX_LAUNCH_CHECK();
@@ -862,15 +837,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         }
       }
       std::memcpy(hctr, pctr, sizeof(bfs_ctr_hdr));
-      return;
     }
-    // (the partial counters need the fold: the copy form also goes through the kernel)
-    hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(64), 0, s, ctr.data(), hctr);
-    HIP_CHECK(hipStreamSynchronize(s));
-  };
-  auto zero_ctr = [&]() { HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(bfs_ctr), s)); };
-  auto rezero_ctr = [&]() {  // after a read: k_publish_seq already zeroed the counters
-    if (!poll) zero_ctr();
   };
 
   try {
@@ -878,10 +845,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     hipLaunchKernelGGL(k_bfs_sources<V>, dim3(grid_for(sources->size, kBlock, 1024)), dim3(kBlock), 0, s, dist,
                        sources->as<V>(), sources->size, nv, bad.data(), vis.data(), fr.data());
     CGX_LAUNCH_CHECK();
-    // poll mode: the source check comes back with the first counters (one host
-    // round trip fewer); invalid ids were skipped by k_bfs_sources
-    if (!poll)
-      CGX_INPUT(to_host_scalar(bad.data(), s) == 0, "Invalid input argument: sources have invalid vertex IDs.");
+    // the source check comes back with the first counters (one host round trip
+    // fewer); invalid ids were skipped by k_bfs_sources
     for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
     // Level 0 is certainly top-down when even every source at the maximum degree
     // stays below the switch rule: then the source counts are not read here -- level
@@ -889,9 +854,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // conversion) and the source check and the sources' edge count come back with
     // level 0's counters (one host round trip fewer)
     double const alpha_do = std::getenv("CGX_BFS_ALPHA") ? std::atof(std::getenv("CGX_BFS_ALPHA")) : 40.0;
-    bool const spec_ok    = poll && std::getenv("CGX_BFS_NO_SPEC") == nullptr;  // A/B: read every level
     bool quick_start      = false;
-    if (spec_ok && std::getenv("CGX_BFS_CONV_SYNC") == nullptr && adj.degree_sorted) {
+    if (adj.degree_sorted) {
       if (adj.max_degree < 0) {
         E o[2];
         HIP_CHECK(hipMemcpyAsync(o, adj.offsets.data<E>(), sizeof(o), hipMemcpyDeviceToHost, s));
@@ -921,7 +885,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
                          fr.data(), nwords);
       CGX_LAUNCH_CHECK();
       read_ctr(bad.data());
-      if (poll) CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
+      CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
       for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
       n_f = ncur[0] + ncur[1] + ncur[2];
       m_f = hctr->next_m;
@@ -935,7 +899,6 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
                                               (unsigned long long)std::numeric_limits<V>::max());
     size_t levels = 0, bu_steps = 0;
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
-    bool const one_pass_bu = std::getenv("CGX_BFS_ONE_PASS_BU") != nullptr;  // A/B: the one-pass bottom-up
     // probe neighbours by 16-byte loads (needs the padded adjacency, int32 ids; RMAT-24
     // k_bu_probe 133.6 -> 129.5 us average; CGX_BFS_PROBE_VEC=0: dword gathers, A/B)
     char const* pv       = std::getenv("CGX_BFS_PROBE_VEC");
@@ -959,26 +922,22 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // (40, 64) 226K; (80, 64) 223K; (80, 128) 225K; (150, 64) 209K.
     // Env overrides are measurement only.
     double const beta_do  = std::getenv("CGX_BFS_BETA") ? std::atof(std::getenv("CGX_BFS_BETA")) : 64.0;
-    // A/B: mark the visited bits after every top-down level, as before (CGX_BFS_MARK_ALL=1)
-    bool const mark_all = std::getenv("CGX_BFS_MARK_ALL") != nullptr;
-    // A/B: read the queue lengths of a bitmap -> queues conversion on the host (CGX_BFS_CONV_SYNC=1)
-    bool const conv_sync = std::getenv("CGX_BFS_CONV_SYNC") != nullptr;
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {
         if (!bottom_up && (double)m_f > (double)m_u / alpha_do) bottom_up = true;
         else if (bottom_up && (double)n_f < (double)nv / beta_do) bottom_up = false;
       }
-      a.depth = depth;
-      rezero_ctr();
+      a.depth = depth;  // (k_publish_seq zeroed the counters it read)
       if (bottom_up) {
         if (!have_bitmap) {  // queues -> frontier bitmap (fr is all zero here)
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
-                             ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), fr.data());
+                             ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), fr.data(), nullptr,
+                             pred, a.nmap);
           CGX_LAUNCH_CHECK();
           have_bitmap = true;
         }
-        bool const probe_path = a.order == nullptr && !one_pass_bu;
+        bool const probe_path = a.order == nullptr;  // (else the one-pass k_bottomup: no identity order)
         if (!probe_path) HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));  // the probe writes every word
         if (probe_path) {  // probe + residual (identity order)
           // (measured and rejected: two chunks per wave in flight, 337K vs 370K MTEPS on
@@ -1000,7 +959,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         m_f = hctr->next_m;
         ++bu_steps;
       } else {
-        if (!have_queue && poll && !conv_sync) {
+        if (!have_queue) {
           // frontier bitmap -> queues with no host round trip: the conversion counts
           // into ctr2, k_topdown reads the queue lengths from there and the grid is
           // sized for all n_f frontier vertices in every degree class
@@ -1013,15 +972,6 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           CGX_LAUNCH_CHECK();
           for (int c = 0; c < 3; ++c) ncur[c] = n_f;
           a.ncur_dev = reinterpret_cast<unsigned long long const*>(ctr2.data());  // bfs_ctr::qlen, offset 0
-          have_queue = true;
-        } else if (!have_queue) {  // frontier bitmap -> queues
-          for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
-          hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s,
-                             a, fr.data(), nwords);
-          CGX_LAUNCH_CHECK();
-          read_ctr();
-          for (int c = 0; c < 3; ++c) ncur[c] = hctr->qlen[c];
-          rezero_ctr();
           have_queue = true;
         }
         for (int c = 0; c < 3; ++c) {
@@ -1049,11 +999,12 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         // this level, every class at least one segment), and both levels come back
         // with one host round trip.  Results do not depend on the direction schedule
         // (smallest-id parent either way), so a wrong guess costs time only.
-        bool const spec = spec_ok && bu_steps > 0 && !pending_src && depth + 1 < limit;
+        bool const spec = bu_steps > 0 && !pending_src && depth + 1 < limit;
         if (spec) {
           // this level's new frontier is the next level's visited set
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
-                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data());
+                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data(), pred,
+                             a.nmap);
           CGX_LAUNCH_CHECK();
           bfs_args<V, E> b = a;
           b.depth          = (V)(depth + 1);
@@ -1090,10 +1041,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           unsigned long long const m_u_next = m_u > m_f ? m_u - m_f : 0;
           bool const next_bu = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
           bool const last    = n_f == 0 || depth + 1 >= limit;
-          if (mark_all ? n_f > 0 : (!last && !next_bu)) {
+          if (!last && !next_bu) {
             hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s,
                                qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(),
-                               nullptr);
+                               nullptr, nullptr, pred, a.nmap);
             CGX_LAUNCH_CHECK();
           }
           have_bitmap = false;
@@ -1121,9 +1072,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         unsigned long long const m_u_next = m_u > m_f ? m_u - m_f : 0;
         bool const next_bu   = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
         bool const last      = n_f == 0 || depth + 1 >= limit;
-        if (mark_all ? n_f > 0 : (!last && !next_bu)) {
+        if (!last && !next_bu) {
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
-                             ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], vis.data(), nullptr);
+                             ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], vis.data(), nullptr, nullptr,
+                             pred, a.nmap);
           CGX_LAUNCH_CHECK();
         }
         for (int c = 0; c < 3; ++c) std::swap(qa[c], qb[c]);
@@ -1141,26 +1093,23 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       read_ctr(bad.data());
       CGX_INPUT(pctr->pad[1] == 0, "Invalid input argument: sources have invalid vertex IDs.");
     }
+    // a depth limit ended the loop on a top-down level's discoveries: their
+    // predecessors to external ids (bottom-up levels wrote external ids already)
+    if (a.nmap && have_queue && n_f > 0 && levels > 0) {
+      hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
+                         ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), nullptr, nullptr, pred,
+                         a.nmap);
+      CGX_LAUNCH_CHECK();
+    }
+    if (finish_pass && pred && sizeof(V) == 4 && g.renumbered) {
+      hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 15) / 16, kBlock, 8192)), dim3(kBlock), 0, s,
+                         reinterpret_cast<int*>(pred), (size_t)nv, -1, g.number_map.data<int>());
+      CGX_LAUNCH_CHECK();
+    }
     h.last_bfs_levels    = levels;
     h.last_bfs_bottom_up = bu_steps;
   } catch (...) {
     throw;
-  }
-  if (pred) {
-    bool const vec4 = sizeof(V) == 4 && (reinterpret_cast<uintptr_t>(pred) & 15) == 0 &&
-                      std::getenv("CGX_BFS_PRED_SCALAR") == nullptr;  // A/B
-    if constexpr (sizeof(V) == 4) {
-      if (vec4) {
-        hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 15) / 16, kBlock, 8192)), dim3(kBlock), 0, s,
-                           reinterpret_cast<int*>(pred), (size_t)nv, (int)INF,
-                           g.renumbered ? g.number_map.data<int>() : (int const*)nullptr);
-        CGX_LAUNCH_CHECK();
-        return;
-      }
-    }
-    hipLaunchKernelGGL(k_finish_pred<V>, dim3(grid_for((nv + 3) / 4, kBlock, 8192)), dim3(kBlock), 0, s, pred, (size_t)nv, INF,
-                       g.renumbered ? g.number_map.data<V>() : (V const*)nullptr);
-    CGX_LAUNCH_CHECK();
   }
 }
 

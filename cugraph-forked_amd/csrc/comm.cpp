@@ -6,6 +6,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 
 namespace cgx {
@@ -168,11 +169,25 @@ class rccl_comm final : public comm_t {
   void alltoallv(void const* s, size_t const* sc, size_t const* sd, void* r, size_t const* rc, size_t const* rd,
                  int dt, hipStream_t st) override
   {
-    size_t es = comm_dtype_size(dt);
+    size_t const es = comm_dtype_size(dt);
+    // this rank's own share is a device copy, not a send to itself; a peer's share
+    // goes in pieces of at most kPiece bytes (both sides cut it alike: the sender's
+    // count is the receiver's).  A 1-rank MG build of RMAT-24 (2.08 GB of edge ids
+    // sent to itself in one ncclSend) came back with a different graph.
+    constexpr size_t kPiece = size_t(1) << 30;
+    size_t const pe         = kPiece / es;
+    if (sc[rank]) {
+      CGX_EXPECTS(sc[rank] == rc[rank], CUGRAPH_UNKNOWN_ERROR, "alltoallv: self counts differ");
+      HIP_CHECK(hipMemcpyAsync((char*)r + rd[rank] * es, (char const*)s + sd[rank] * es, sc[rank] * es,
+                               hipMemcpyDeviceToDevice, st));
+    }
     NCCL_CHECK(ncclGroupStart());
     for (int q = 0; q < size; ++q) {
-      if (sc[q]) NCCL_CHECK(ncclSend((char const*)s + sd[q] * es, sc[q], nccl_dt(dt), q, comm, st));
-      if (rc[q]) NCCL_CHECK(ncclRecv((char*)r + rd[q] * es, rc[q], nccl_dt(dt), q, comm, st));
+      if (q == rank) continue;
+      for (size_t o = 0; o < sc[q]; o += pe)
+        NCCL_CHECK(ncclSend((char const*)s + (sd[q] + o) * es, std::min(pe, sc[q] - o), nccl_dt(dt), q, comm, st));
+      for (size_t o = 0; o < rc[q]; o += pe)
+        NCCL_CHECK(ncclRecv((char*)r + (rd[q] + o) * es, std::min(pe, rc[q] - o), nccl_dt(dt), q, comm, st));
     }
     NCCL_CHECK(ncclGroupEnd());
   }

@@ -1584,6 +1584,9 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     CGX_LAUNCH_CHECK();
     exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nwin + 1, s);
     int64_t const total = total0 + (int64_t)to_host(pb.data() + nwin, 1, s)[0];
+    if (std::getenv("CGX_PR_DEBUG"))  // measurement only
+      std::fprintf(stderr, "[pr] schedule: %lld rows, %lld sources, %lld edges, %d-bit windows, %lld packed entries\n",
+                   (long long)n_rows, (long long)n_cols, (long long)ne, wb, (long long)total);
     if (total <= ne + ne / 2 && (uint64_t)total < (1ull << 32)) {
       uint16_t const pad_code = (uint16_t)(((1u << (16 - wb)) - 1) << wb);  // a jump of 0: no edge
       pp.packed = true;

@@ -62,11 +62,38 @@ def main():
     deg = np.zeros(n_ext, np.int64)
     deg[ext] = (off[1:] - off[:-1]).cpu().numpy()
     del off
+    root = int(ext[0])  # the largest-degree vertex
+    sg_dist = None
+    try:
+        dv, _, vv = p.bfs(h, g, np.asarray([root], np.int32), True, 0, True, False)
+        sg_dist = np.full(n_ext, -2, np.int64)
+        sg_dist[vv.cpu().numpy().astype(np.int64)] = dv.cpu().numpy()
+    except RuntimeError as e:
+        print(f"  SG BFS: {e}", flush=True)
+    if os.environ.get("SG_PACKED0"):  # the 32-bit-entry push on a second SG graph
+        os.environ["CGX_PR_PACKED"] = "0"
+        g2, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
+        v2, x2 = p.pagerank(h, g2, None, None, None, None, 0.85, 1e-6, 500, False)
+        del os.environ["CGX_PR_PACKED"]
+        r2 = sg_x[v2.cpu().numpy().astype(np.int64)]
+        print(f"  SG 32-bit entries: iterations {h.last_iterations()}, bitwise equal "
+              f"{bool(np.array_equal(x2.cpu().numpy().view(np.int32), r2.view(np.int32)))}", flush=True)
+        g2 = None
     g = None
     p.trim_device_cache()
     ctx = p.comms.init_rccl(1)
     hm = p.ResourceHandle(ctx.ptr)
     gm, _, _ = bench.build_rmat_graph(p, hm, scale, transposed=True, mg=(0, 1))
+    print(f"  graphs: SG V={len(ext)} E={int(deg.sum())}; MG V={gm.number_of_vertices()} E={gm.number_of_edges()}",
+          flush=True)
+    try:
+        dm, _, vm0 = p.bfs(hm, gm, np.asarray([root], np.int32), True, 0, True, False)
+        ids0 = vm0.cpu().numpy().astype(np.int64)
+        if sg_dist is not None:
+            print(f"  BFS from {root}: MG distances equal SG {bool(np.array_equal(dm.cpu().numpy(), sg_dist[ids0]))}",
+                  flush=True)
+    except RuntimeError as e:
+        print(f"  MG BFS: {e}", flush=True)
     mg_ms = timed(p, hm, gm)
     print(f"RMAT-{scale}: SG {sg_ms:.4f} ms/iteration, 1-rank RCCL MG {mg_ms:.4f} ms/iteration "
           f"(ratio {mg_ms / sg_ms:.3f}); SG iterations {it_sg}", flush=True)

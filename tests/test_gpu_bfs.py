@@ -192,9 +192,9 @@ def test_result_tensors_own_library_memory():
 @pytest.mark.parametrize("scale", [14, 18])
 def test_bitmap_to_queue_conversion_device_vs_host(scale, monkeypatch, capfd):
     """A bottom-up -> top-down switch converts the frontier bitmap to queues with the
-    queue lengths read on the device (default) or on the host (CGX_BFS_CONV_SYNC=1,
-    and the memcpy + synchronize form CGX_BFS_SYNC=1): same distances and
-    predecessors, and the runs do contain such a switch (CGX_BFS_DEBUG level log)."""
+    queue lengths read on the device: same distances and predecessors as the
+    top-down-only traversal (which converts nothing), and the runs do contain such a
+    switch (CGX_BFS_DEBUG level log)."""
     s, d = rmat_sym(scale)
     h, G = make_graph(s, d, None, renumber=True, symmetric=True)
     deg = np.bincount(s)
@@ -205,12 +205,9 @@ def test_bitmap_to_queue_conversion_device_vs_host(scale, monkeypatch, capfd):
     log = capfd.readouterr().err
     dirs = [ln.split()[3] for ln in log.splitlines() if ln.startswith("[bfs] level")]
     assert any(a == "bottom-up" and b == "top-down" for a, b in zip(dirs, dirs[1:])), log[-2000:]
-    for env in ("CGX_BFS_CONV_SYNC", "CGX_BFS_SYNC"):
-        monkeypatch.setenv(env, "1")
-        for x, (v0, d0, p0) in zip(srcs, base):
-            v, dist, pred = run(h, G, [x], True)
-            assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0), env
-        monkeypatch.delenv(env)
+    for x, (v0, d0, p0) in zip(srcs, base):
+        v, dist, pred = run(h, G, [x], False)
+        assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0)
     if scale == 14:
         for x, (v0, d0, p0) in zip(srcs, base):
             check_vs_oracle(s, d, v0, d0, p0, [x])
