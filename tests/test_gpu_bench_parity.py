@@ -248,6 +248,55 @@ def test_bfs_rmat24_all_bench_roots(rmat24):
     torch.cuda.synchronize()
 
 
+def test_mg_one_rank_rccl_rmat24_equals_sg(rmat24):
+    """The multi-GPU path at the headline size, through the library's RCCL
+    communicators with the one rank a box allows: the MG graph build (its
+    alltoallv moves 2.08 GB of edge ids: a single 2 GB ncclSend of a rank to
+    itself once came back with a different graph), MG PageRank bit for bit equal to
+    single-GPU PageRank (u64 fixed-point sums, u64 allreduce), MG BFS distances and
+    predecessors equal to single-GPU BFS, by external id."""
+    import os
+    import torch
+    import torch.distributed as dist
+    bench, p = _bench()
+    b = rmat24
+    v, x = p.pagerank(b.h, b.g, None, None, None, None, 0.85, 1e-6, 500, False)
+    it_sg = b.h.last_iterations()
+    ext = v.to(torch.int64)
+    n_ext = int(ext.max()) + 1
+    sg_x = torch.zeros(n_ext, dtype=torch.int32, device="cuda")
+    sg_x[ext] = x.view(torch.int32)
+    root = int(b.roots[0])
+    d, pr, vb = p.bfs(b.h, b.g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+    sg_d = torch.full((n_ext,), -2, dtype=torch.int64, device="cuda")
+    sg_p = torch.full((n_ext,), -2, dtype=torch.int64, device="cuda")
+    sg_d[vb.to(torch.int64)] = d.to(torch.int64)
+    sg_p[vb.to(torch.int64)] = pr.to(torch.int64)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(bench.free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    ctx = p.comms.init_rccl(1)
+    try:
+        hm = p.ResourceHandle(ctx.ptr)
+        gm, _, _ = bench.build_rmat_graph(p, hm, 24, transposed=True, mg=(0, 1))
+        assert gm.number_of_vertices() == b.g.number_of_vertices()
+        assert gm.number_of_edges() == b.g.number_of_edges()
+        vm, xm = p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert hm.last_iterations() == it_sg
+        assert torch.equal(xm.view(torch.int32), sg_x[vm.to(torch.int64)]), "MG PageRank differs from SG"
+        dm, pm, vmb = p.bfs(hm, gm, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+        ids = vmb.to(torch.int64)
+        assert torch.equal(dm.to(torch.int64), sg_d[ids]), "MG BFS distances differ from SG"
+        assert torch.equal(pm.to(torch.int64), sg_p[ids]), "MG BFS predecessors differ from SG"
+        gm = None
+        hm = None
+        torch.cuda.synchronize()
+        p.trim_device_cache()
+    finally:
+        ctx.free()
+        dist.destroy_process_group()
+
+
 def _louvain_q_recomputed(scale):
     """Louvain on a bench graph (symmetric R-MAT, fp32 [0,1) weights, bench.py
     louvain_leg): the reported Q is the modularity of the returned partition,

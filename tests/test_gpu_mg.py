@@ -45,8 +45,9 @@ def _rank_setup(port=None, rank=None):
     * HSA_ENABLE_SDMA=0: copies run as blit kernels, not on the DMA engines.  Up to 8
       rehearsal ranks share the one test GPU, and the world-8 Louvain rehearsal (the
       most copy-heavy: hundreds of small staged collectives per rank) stalled in 3 of
-      5 runs with every rank waiting on its stream's copies (tests/test_gpu_mg.py
-      history).  A node runs one rank per GPU over RCCL instead."""
+      5 round-3 runs: the stacks show every arrived rank inside the same collective and
+      the missing ones blocked draining their own stream's copies ("The
+      world-8 rehearsal hang").  A node runs one rank per GPU over RCCL instead."""
     import faulthandler
     import signal
     import sys
