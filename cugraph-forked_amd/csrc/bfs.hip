@@ -43,8 +43,9 @@ struct bfs_ctr_hdr {
   unsigned long long qlen[3];  // next queues: small / mid / large (first: bfs_args::ncur_dev points here)
   unsigned long long next_n;   // vertices discovered this level
   unsigned long long next_m;   // sum of their degrees
-  unsigned long long pad[3];
+  unsigned long long pad[3];  // [0]: publish sequence, [1]: source check, [2]: sources' edge count
 };
+static_assert(sizeof(bfs_ctr_hdr) == 64, "k_publish_seq writes host words 0..7 and 8..12 by index");
 
 // The device block.  Every kernel block adds its discovered-vertex and edge counts
 // at the end (flush_counts); same-address atomics serialise at the memory side
@@ -102,24 +103,33 @@ __global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr_hdr* host, unsigned long lon
   fold_parts(ctr, true, n, m);
   if (ctr_b) fold_parts(ctr_b, true, nb, mb);
   if (src_m) fold_parts(src_m, false, ns, ms);
-  if (threadIdx.x != 0) return;
+  // one host word per lane, all stores in flight at once (one thread storing the 12
+  // words one after another made this kernel 4.6 us)
+  int const i = threadIdx.x;
+  if (i >= 12) return;
   unsigned long long* c  = reinterpret_cast<unsigned long long*>(ctr);
+  unsigned long long* cb = reinterpret_cast<unsigned long long*>(ctr_b);
   unsigned long long* hp = reinterpret_cast<unsigned long long*>(host);
-  for (int i = 0; i < 5; ++i) {
-    __hip_atomic_store(hp + i, i < 3 ? c[i] : (i == 3 ? n : m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    c[i] = 0ull;
+  unsigned long long v = 0;
+  int slot             = i;
+  if (i < 5) {
+    v = i < 3 ? c[i] : (i == 3 ? n : m);
+  } else if (i < 10) {
+    int const k = i - 5;
+    slot        = 8 + k;  // host[1]
+    if (ctr_b) v = k < 3 ? cb[k] : (k == 3 ? nb : mb);
+  } else if (i == 10) {
+    slot = 7;  // pad[2]
+    v    = ms;
+  } else {
+    slot = 6;  // pad[1]
+    v    = bad ? (unsigned long long)*bad : 0ull;
   }
-  if (ctr_b) {
-    unsigned long long* cb = reinterpret_cast<unsigned long long*>(ctr_b);
-    unsigned long long* hb = reinterpret_cast<unsigned long long*>(host + 1);
-    for (int i = 0; i < 5; ++i) {
-      __hip_atomic_store(hb + i, i < 3 ? cb[i] : (i == 3 ? nb : mb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      cb[i] = 0ull;
-    }
-  }
-  __hip_atomic_store(&host->pad[2], ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&host->pad[1], bad ? (unsigned long long)*bad : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __threadfence_system();
+  if (i < 5 || i >= 10 || ctr_b) __hip_atomic_store(hp + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (i < 5) c[i] = 0ull;
+  else if (i < 10 && ctr_b) cb[i - 5] = 0ull;
+  __threadfence_system();  // (lanes 0..11 are one wave: the fence waits for all their stores)
+  if (i != 0) return;
   __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -177,6 +187,7 @@ struct bfs_args {
   V const* order;
   work_item const* items;
   long long blk_mid_start, blk_small_start;  // top-down grid segmentation
+  bool td_min_pred;  // top-down levels keep the smallest parent by atomicMin (else k_td_pred afterwards)
 };
 
 // Next-queue appends are staged per wave in LDS (kStage entries per class) and
@@ -247,7 +258,7 @@ __device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, wave_stage<V
   if (active) {
     uint32_t bit = 1u << (uint32_t(v) & 31u);
     if (!(a.vis[v >> 5] & bit)) {  // not visited before this level
-      if (a.pred) atomic_min_v<V>(a.pred + v, u);
+      if (a.pred && a.td_min_pred) atomic_min_v<V>(a.pred + v, u);
       take = cas_claim<V>(a.dist, v, (V)(a.depth + 1));
     }
   }
@@ -385,6 +396,91 @@ __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, u
     if (nmap) {  // (sources keep -1)
       V const p = pred[v];
       if (p != (V)-1) pred[v] = nmap[p];
+    }
+  }
+}
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+// Predecessors of a finished top-down level's discoveries without per-edge atomics
+// (A/B against the atomicMin in visit_edge): a vertex v found at depth d + 1 has
+// only neighbours at depths d .. d + 2, so before the level's own visited bits are
+// set, a visited neighbour is exactly a depth-d one, and the first visited entry of
+// v's sorted adjacency is the smallest-id parent the atomicMin keeps.  A lane per
+// vertex tests its first 8 neighbours (the loads back to back); the wave then
+// walks its misses' lists together, 64 entries a step.  Writes external ids.
+template <typename V, typename E, bool VEC>
+__global__ __launch_bounds__(256) void k_td_pred(bfs_args<V, E> a, V const* q0, unsigned long long n0, V const* q1,
+                                                 unsigned long long n1, V const* q2, unsigned long long n2,
+                                                 bfs_ctr const* cdev)
+{
+  if (cdev) {
+    n0 = cdev->qlen[0];
+    n1 = cdev->qlen[1];
+    n2 = cdev->qlen[2];
+  }
+  unsigned long long const tot = n0 + n1 + n2;
+  int const lane               = threadIdx.x & 63;
+  unsigned long long const nwv = (unsigned long long)gridDim.x * (kBlock / 64);
+  for (unsigned long long base = (blockIdx.x * (unsigned long long)(kBlock / 64) + (threadIdx.x >> 6)) * 64;
+       base < tot; base += nwv * 64) {
+    unsigned long long const i = base + lane;
+    bool const in              = i < tot;
+    V v                        = 0;
+    if (in) v = i < n0 ? q0[i] : (i < n0 + n1 ? q1[i - n0] : q2[i - n0 - n1]);
+    E beg = in ? a.off[v] : E(0), end = in ? a.off[v + 1] : E(0);
+    int64_t const deg = (int64_t)(end - beg);
+    bool hit = false;
+    V par    = 0;
+    if (deg > 0) {
+      V u[8];
+      if constexpr (VEC && sizeof(V) == 4) {
+        E const a0   = beg & ~E(3);
+        int const sh = (int)(beg - a0);
+        v4i_t const* p = reinterpret_cast<v4i_t const*>(a.idx + a0);
+        v4i_t const c0 = p[0], c1 = p[1], c2 = p[2];
+        int const wv[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) u[t] = (V)(sh == 0 ? wv[t] : sh == 1 ? wv[t + 1] : sh == 2 ? wv[t + 2] : wv[t + 3]);
+#pragma unroll
+        for (int t = 1; t < 8; ++t) u[t] = t < deg ? u[t] : u[0];
+      } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) u[t] = a.idx[beg + (t < deg ? t : 0)];
+      }
+      uint32_t w[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) w[t] = a.vis[u[t] >> 5];
+      uint32_t hm = 0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) hm |= (t < deg ? (w[t] >> (uint32_t(u[t]) & 31u)) & 1u : 0u) << t;
+#pragma unroll
+      for (int t = 7; t >= 0; --t)
+        if ((hm >> t) & 1u) par = u[t];
+      hit = hm != 0;
+    }
+    if (hit) a.pred[v] = a.nmap ? a.nmap[par] : par;
+    unsigned long long mm = __ballot(in && !hit && deg > 8);
+    while (mm) {  // (every such v has a visited neighbour further on: the walk ends on it)
+      int const j  = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      V const vj   = __shfl(v, j, 64);
+      E const bj   = __shfl(beg, j, 64) + 8;
+      E const ej   = __shfl(end, j, 64);
+      for (E e0 = bj; e0 < ej; e0 += 64) {
+        E const e   = e0 + lane;
+        V uu        = 0;
+        bool h      = false;
+        if (e < ej) {
+          uu = a.idx[e];
+          h  = (a.vis[uu >> 5] >> (uint32_t(uu) & 31u)) & 1u;
+        }
+        unsigned long long const hb = __ballot(h);
+        if (hb) {
+          if (lane == __ffsll((long long)hb) - 1) a.pred[vj] = a.nmap ? a.nmap[uu] : uu;
+          break;
+        }
+      }
     }
   }
 }
@@ -543,8 +639,6 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
 #endif
 constexpr int kProbe = CGX_BFS_PROBE;
 
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-
 // VEC: a lane's first 8 neighbours from three 16-byte loads of the aligned
 // 12-entry span around them (adjacency arrays are padded by 16 entries) instead of
 // 8 dword gathers: consecutive lanes' lists are adjacent, so each load instruction
@@ -558,7 +652,14 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
   int64_t const nchunks = (a.nv + 63) >> 6;
   int64_t const stride  = (int64_t)gridDim.x * (kBlock / 64);
   int64_t const rcap    = residual_cap(a.nv);
+  // A hit's predecessor is stored as an external id one chunk later: its number-map
+  // gather is issued ahead of the next chunk's loads, so it adds no step to the
+  // chain of dependent loads a chunk is (vis -> offsets -> neighbours -> frontier)
+  int64_t pend_v = -1;
+  V pend_par     = 0;
   for (int64_t c = blockIdx.x * (int64_t)(kBlock / 64) + (threadIdx.x >> 6); c < nchunks; c += stride) {
+    V pend_ext = pend_par;
+    if (a.nmap && pend_v >= 0) pend_ext = a.nmap[pend_par];
     int64_t const v  = (c << 6) + lane;
     bool const in    = v < a.nv;
     uint32_t const vw = in ? a.vis[v >> 5] : 0xffffffffu;
@@ -602,9 +703,12 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
       hit  = hm != 0;
       more = !hit && deg > kProbe;
     }
+    if (a.pred && pend_v >= 0) a.pred[pend_v] = pend_ext;
+    pend_v = -1;
     if (hit) {
       a.dist[v] = nd;
-      if (a.pred) a.pred[v] = a.nmap ? a.nmap[par] : par;
+      pend_v   = v;
+      pend_par = par;
       my_n += 1;
       my_m += (unsigned long long)deg;
     }
@@ -624,6 +728,7 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
       if (more) res[sq * rcap + (int64_t)base + __popcll(mm & ((1ull << lane) - 1ull))] = (V)v;
     }
   }
+  if (a.pred && pend_v >= 0) a.pred[pend_v] = a.nmap ? a.nmap[pend_par] : pend_par;
   flush_counts(a.ctr, my_n, my_m);
 }
 
@@ -815,6 +920,24 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   a.order = (dir_opt && !adj.degree_sorted) ? adj.order.data<V>() : nullptr;
   bool const finish_pass = std::getenv("CGX_BFS_PRED_FINISH") != nullptr && sizeof(V) == 4;  // A/B
   a.nmap  = (pred && g.renumbered && !finish_pass) ? g.number_map.data<V>() : nullptr;
+  // A/B (CGX_BFS_TD_PRED=pass): top-down levels claim without the atomicMin and
+  // k_td_pred finds each discovery's smallest parent before its visited bits are set
+  char const* tdp    = std::getenv("CGX_BFS_TD_PRED");
+  bool const td_pass = pred && tdp && std::string(tdp) == "pass";
+  a.td_min_pred      = !td_pass;
+  V* const mpred     = td_pass ? nullptr : pred;  // k_mark_queues translates only what atomicMin left internal
+  V const* mnmap     = td_pass ? nullptr : a.nmap;
+  bool const vec_idx = adj.idx_padded && sizeof(V) == 4;
+  auto td_preds = [&](V const* q0, unsigned long long n0, V const* q1, unsigned long long n1, V const* q2,
+                      unsigned long long n2, bfs_ctr const* cdev, unsigned long long grid_n) {
+    if (!td_pass) return;
+    dim3 const gr(grid_for((grid_n + 63) / 64, kBlock / 64, 4096));
+    if (vec_idx)
+      hipLaunchKernelGGL((k_td_pred<V, E, true>), gr, dim3(kBlock), 0, s, a, q0, n0, q1, n1, q2, n2, cdev);
+    else
+      hipLaunchKernelGGL((k_td_pred<V, E, false>), gr, dim3(kBlock), 0, s, a, q0, n0, q1, n1, q2, n2, cdev);
+    CGX_LAUNCH_CHECK();
+  };
   a.items = dir_opt ? adj.items.data<work_item>() : nullptr;
 
   // Level counters: k_publish_seq into the handle's coherent block and a host spin on
@@ -931,9 +1054,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       a.depth = depth;  // (k_publish_seq zeroed the counters it read)
       if (bottom_up) {
         if (!have_bitmap) {  // queues -> frontier bitmap (fr is all zero here)
+          td_preds(qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], nullptr, n_f);
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
                              ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), fr.data(), nullptr,
-                             pred, a.nmap);
+                             mpred, mnmap);
           CGX_LAUNCH_CHECK();
           have_bitmap = true;
         }
@@ -1002,9 +1126,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         bool const spec = bu_steps > 0 && !pending_src && depth + 1 < limit;
         if (spec) {
           // this level's new frontier is the next level's visited set
+          td_preds(qb[0].data(), 0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, ctr.data(), (unsigned long long)nv);
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
-                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data(), pred,
-                             a.nmap);
+                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data(), mpred,
+                             mnmap);
           CGX_LAUNCH_CHECK();
           bfs_args<V, E> b = a;
           b.depth          = (V)(depth + 1);
@@ -1042,9 +1167,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           bool const next_bu = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
           bool const last    = n_f == 0 || depth + 1 >= limit;
           if (!last && !next_bu) {
+            td_preds(qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], nullptr, n_f);
             hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s,
                                qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(),
-                               nullptr, nullptr, pred, a.nmap);
+                               nullptr, nullptr, mpred, mnmap);
             CGX_LAUNCH_CHECK();
           }
           have_bitmap = false;
@@ -1073,9 +1199,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         bool const next_bu   = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
         bool const last      = n_f == 0 || depth + 1 >= limit;
         if (!last && !next_bu) {
+          td_preds(qb[0].data(), ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], nullptr, n_f);
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
                              ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], vis.data(), nullptr, nullptr,
-                             pred, a.nmap);
+                             mpred, mnmap);
           CGX_LAUNCH_CHECK();
         }
         for (int c = 0; c < 3; ++c) std::swap(qa[c], qb[c]);
@@ -1095,11 +1222,14 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     }
     // a depth limit ended the loop on a top-down level's discoveries: their
     // predecessors to external ids (bottom-up levels wrote external ids already)
-    if (a.nmap && have_queue && n_f > 0 && levels > 0) {
-      hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
-                         ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), nullptr, nullptr, pred,
-                         a.nmap);
-      CGX_LAUNCH_CHECK();
+    if (have_queue && n_f > 0 && levels > 0) {
+      td_preds(qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], nullptr, n_f);
+      if (mnmap) {
+        hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
+                           ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), nullptr, nullptr, mpred,
+                           mnmap);
+        CGX_LAUNCH_CHECK();
+      }
     }
     if (finish_pass && pred && sizeof(V) == 4 && g.renumbered) {
       hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 15) / 16, kBlock, 8192)), dim3(kBlock), 0, s,

@@ -135,6 +135,31 @@ def test_initial_guess_and_precomputed_outw():
     assert np.allclose(a, b, rtol=1e-6, atol=0)
 
 
+def test_understated_precomputed_outw():
+    """Precomputed out-weight sums below the graph's own take the pull kernel with
+    fp64 sums: at 0.9 x the degrees the iteration still contracts (alpha / 0.9 < 1)
+    to a fixed point whose total mass is ~2.7 -- matched against the oracle at 1e-6;
+    at 0.5 x it diverges, and the call must fail to converge (as the oracle does)
+    instead of reporting convergence on a wrapped or saturated sum."""
+    s, d, _ = rmat_graph(10, False)
+    h, G = make_graph(s, d, None, transposed=True, renumber=False, symmetric=True)
+    V = int(max(s.max(), d.max())) + 1
+    deg = np.bincount(s, minlength=V).astype(np.float64)
+    verts = np.arange(V, dtype=np.int32)
+    outw = (0.9 * deg).astype(np.float32)
+    v, pr = plc().pagerank(h, G, verts, outw, None, None, 0.85, 1e-8, 500, False)
+    ref = opr.pagerank(V, s, d, alpha=0.85, epsilon=1e-8, out_weight_sums=outw.astype(np.float64))
+    got = by_ext(v, pr)
+    live = ref > 0
+    assert ref.sum() > 2.0
+    assert np.max(np.abs(got[live] - ref[live]) / ref[live]) < REL
+    with pytest.raises(opr.PageRankNotConverged):
+        opr.pagerank(V, s, d, alpha=0.85, epsilon=1e-6, max_iterations=200,
+                     out_weight_sums=(0.5 * deg))
+    with pytest.raises(RuntimeError, match="converge"):
+        plc().pagerank(h, G, verts, (0.5 * deg).astype(np.float32), None, None, 0.85, 1e-6, 200, False)
+
+
 def test_repeat_is_bitwise_deterministic():
     s, d, _ = rmat_graph(12, False)
     h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
