@@ -187,7 +187,6 @@ struct bfs_args {
   V const* order;
   work_item const* items;
   long long blk_mid_start, blk_small_start;  // top-down grid segmentation
-  bool td_min_pred;  // top-down levels keep the smallest parent by atomicMin (else k_td_pred afterwards)
 };
 
 // Next-queue appends are staged per wave in LDS (kStage entries per class) and
@@ -258,7 +257,7 @@ __device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, wave_stage<V
   if (active) {
     uint32_t bit = 1u << (uint32_t(v) & 31u);
     if (!(a.vis[v >> 5] & bit)) {  // not visited before this level
-      if (a.pred && a.td_min_pred) atomic_min_v<V>(a.pred + v, u);
+      if (a.pred) atomic_min_v<V>(a.pred + v, u);
       take = cas_claim<V>(a.dist, v, (V)(a.depth + 1));
     }
   }
@@ -401,89 +400,6 @@ __global__ void k_mark_queues(V const* q0, unsigned long long n0, V const* q1, u
 }
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
-
-// Predecessors of a finished top-down level's discoveries without per-edge atomics
-// (A/B against the atomicMin in visit_edge): a vertex v found at depth d + 1 has
-// only neighbours at depths d .. d + 2, so before the level's own visited bits are
-// set, a visited neighbour is exactly a depth-d one, and the first visited entry of
-// v's sorted adjacency is the smallest-id parent the atomicMin keeps.  A lane per
-// vertex tests its first 8 neighbours (the loads back to back); the wave then
-// walks its misses' lists together, 64 entries a step.  Writes external ids.
-template <typename V, typename E, bool VEC>
-__global__ __launch_bounds__(256) void k_td_pred(bfs_args<V, E> a, V const* q0, unsigned long long n0, V const* q1,
-                                                 unsigned long long n1, V const* q2, unsigned long long n2,
-                                                 bfs_ctr const* cdev)
-{
-  if (cdev) {
-    n0 = cdev->qlen[0];
-    n1 = cdev->qlen[1];
-    n2 = cdev->qlen[2];
-  }
-  unsigned long long const tot = n0 + n1 + n2;
-  int const lane               = threadIdx.x & 63;
-  unsigned long long const nwv = (unsigned long long)gridDim.x * (kBlock / 64);
-  for (unsigned long long base = (blockIdx.x * (unsigned long long)(kBlock / 64) + (threadIdx.x >> 6)) * 64;
-       base < tot; base += nwv * 64) {
-    unsigned long long const i = base + lane;
-    bool const in              = i < tot;
-    V v                        = 0;
-    if (in) v = i < n0 ? q0[i] : (i < n0 + n1 ? q1[i - n0] : q2[i - n0 - n1]);
-    E beg = in ? a.off[v] : E(0), end = in ? a.off[v + 1] : E(0);
-    int64_t const deg = (int64_t)(end - beg);
-    bool hit = false;
-    V par    = 0;
-    if (deg > 0) {
-      V u[8];
-      if constexpr (VEC && sizeof(V) == 4) {
-        E const a0   = beg & ~E(3);
-        int const sh = (int)(beg - a0);
-        v4i_t const* p = reinterpret_cast<v4i_t const*>(a.idx + a0);
-        v4i_t const c0 = p[0], c1 = p[1], c2 = p[2];
-        int const wv[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
-#pragma unroll
-        for (int t = 0; t < 8; ++t) u[t] = (V)(sh == 0 ? wv[t] : sh == 1 ? wv[t + 1] : sh == 2 ? wv[t + 2] : wv[t + 3]);
-#pragma unroll
-        for (int t = 1; t < 8; ++t) u[t] = t < deg ? u[t] : u[0];
-      } else {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) u[t] = a.idx[beg + (t < deg ? t : 0)];
-      }
-      uint32_t w[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) w[t] = a.vis[u[t] >> 5];
-      uint32_t hm = 0;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) hm |= (t < deg ? (w[t] >> (uint32_t(u[t]) & 31u)) & 1u : 0u) << t;
-#pragma unroll
-      for (int t = 7; t >= 0; --t)
-        if ((hm >> t) & 1u) par = u[t];
-      hit = hm != 0;
-    }
-    if (hit) a.pred[v] = a.nmap ? a.nmap[par] : par;
-    unsigned long long mm = __ballot(in && !hit && deg > 8);
-    while (mm) {  // (every such v has a visited neighbour further on: the walk ends on it)
-      int const j  = __ffsll((long long)mm) - 1;
-      mm &= mm - 1;
-      V const vj   = __shfl(v, j, 64);
-      E const bj   = __shfl(beg, j, 64) + 8;
-      E const ej   = __shfl(end, j, 64);
-      for (E e0 = bj; e0 < ej; e0 += 64) {
-        E const e   = e0 + lane;
-        V uu        = 0;
-        bool h      = false;
-        if (e < ej) {
-          uu = a.idx[e];
-          h  = (a.vis[uu >> 5] >> (uint32_t(uu) & 31u)) & 1u;
-        }
-        unsigned long long const hb = __ballot(h);
-        if (hb) {
-          if (lane == __ffsll((long long)hb) - 1) a.pred[vj] = a.nmap ? a.nmap[uu] : uu;
-          break;
-        }
-      }
-    }
-  }
-}
 
 // bitmap -> class queues (bottom-up to top-down switch).
 // The bitmap is cleared as it is read: while the frontier lives in queues the
@@ -783,46 +699,6 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
   flush_counts(a.ctr, my_n, my_m);
 }
 
-// (A/B, CGX_BFS_PRED_FINISH=1: predecessors kept internal during the traversal and
-// translated by this pass afterwards.)  4-byte ids: four predecessors per lane through 16-byte loads and stores, kQ quads
-// per lane with every load (and then every number-map gather) issued before the
-// first use, so a lane makes one dependent round trip instead of kQ
-__global__ __launch_bounds__(256) void k_finish_pred4(int* pred, size_t n, int none, int const* nmap)
-{
-  typedef int v4_t __attribute__((ext_vector_type(4)));
-  constexpr int kQ    = 4;
-  size_t const nq     = n / 4;
-  size_t const stride = (size_t)gridDim.x * blockDim.x;
-  v4_t* p4            = reinterpret_cast<v4_t*>(pred);
-  size_t i            = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  for (; i + (kQ - 1) * stride < nq; i += kQ * stride) {
-    v4_t p[kQ];
-#pragma unroll
-    for (int k = 0; k < kQ; ++k) p[k] = __builtin_nontemporal_load(p4 + i + k * stride);
-    int q[kQ][4];
-#pragma unroll
-    for (int k = 0; k < kQ; ++k) {
-      q[k][0] = p[k].x == none ? -1 : (nmap ? nmap[p[k].x] : p[k].x);
-      q[k][1] = p[k].y == none ? -1 : (nmap ? nmap[p[k].y] : p[k].y);
-      q[k][2] = p[k].z == none ? -1 : (nmap ? nmap[p[k].z] : p[k].z);
-      q[k][3] = p[k].w == none ? -1 : (nmap ? nmap[p[k].w] : p[k].w);
-    }
-#pragma unroll
-    for (int k = 0; k < kQ; ++k) __builtin_nontemporal_store(v4_t{q[k][0], q[k][1], q[k][2], q[k][3]}, p4 + i + k * stride);
-  }
-  for (; i < nq; i += stride) {
-    v4_t p = __builtin_nontemporal_load(p4 + i);
-    p      = v4_t{p.x == none ? -1 : (nmap ? nmap[p.x] : p.x), p.y == none ? -1 : (nmap ? nmap[p.y] : p.y),
-                  p.z == none ? -1 : (nmap ? nmap[p.z] : p.z), p.w == none ? -1 : (nmap ? nmap[p.w] : p.w)};
-    __builtin_nontemporal_store(p, p4 + i);
-  }
-  size_t const t = nq * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (t < n) {
-    int const q = pred[t];
-    pred[t]     = q == none ? -1 : (nmap ? nmap[q] : q);
-  }
-}
-
 // dist = INF, pred = -1 and the three bitmaps cleared in one launch (was 2 fills + 3 memsets)
 template <typename V>
 __global__ void k_bfs_setup(V* dist, V* pred, int64_t nv, V inf, uint32_t* vis, uint32_t* fr, uint32_t* nxt,
@@ -918,28 +794,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   a.ctr   = ctr.data();
   a.nv    = nv;
   a.order = (dir_opt && !adj.degree_sorted) ? adj.order.data<V>() : nullptr;
-  bool const finish_pass = std::getenv("CGX_BFS_PRED_FINISH") != nullptr && sizeof(V) == 4;  // A/B
-  a.nmap  = (pred && g.renumbered && !finish_pass) ? g.number_map.data<V>() : nullptr;
-  // A/B (CGX_BFS_TD_PRED=pass): top-down levels claim without the atomicMin and
-  // k_td_pred finds each discovery's smallest parent before its visited bits are set
-  char const* tdp    = std::getenv("CGX_BFS_TD_PRED");
-  bool const td_pass = pred && tdp && std::string(tdp) == "pass";
-  a.td_min_pred      = !td_pass;
-  V* const mpred     = td_pass ? nullptr : pred;  // k_mark_queues translates only what atomicMin left internal
-  V const* mnmap     = td_pass ? nullptr : a.nmap;
-  bool const vec_idx = adj.idx_padded && sizeof(V) == 4;
-  auto td_preds = [&](V const* q0, unsigned long long n0, V const* q1, unsigned long long n1, V const* q2,
-                      unsigned long long n2, bfs_ctr const* cdev, unsigned long long grid_n) {
-    if (!td_pass) return;
-    dim3 const gr(grid_for((grid_n + 63) / 64, kBlock / 64, 4096));
-    if (vec_idx)
-      hipLaunchKernelGGL((k_td_pred<V, E, true>), gr, dim3(kBlock), 0, s, a, q0, n0, q1, n1, q2, n2, cdev);
-    else
-      hipLaunchKernelGGL((k_td_pred<V, E, false>), gr, dim3(kBlock), 0, s, a, q0, n0, q1, n1, q2, n2, cdev);
-    CGX_LAUNCH_CHECK();
-  };
-  a.items = dir_opt ? adj.items.data<work_item>() : nullptr;
-
+  a.nmap  = (pred && g.renumbered) ? g.number_map.data<V>() : nullptr;
   // Level counters: k_publish_seq into the handle's coherent block and a host spin on
   // its sequence word -- no hipStreamSynchronize per level (measured against a D2H
   // copy + synchronize per level: that form was removed)
@@ -1054,10 +909,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       a.depth = depth;  // (k_publish_seq zeroed the counters it read)
       if (bottom_up) {
         if (!have_bitmap) {  // queues -> frontier bitmap (fr is all zero here)
-          td_preds(qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], nullptr, n_f);
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
                              ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), fr.data(), nullptr,
-                             mpred, mnmap);
+                             pred, a.nmap);
           CGX_LAUNCH_CHECK();
           have_bitmap = true;
         }
@@ -1126,10 +980,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         bool const spec = bu_steps > 0 && !pending_src && depth + 1 < limit;
         if (spec) {
           // this level's new frontier is the next level's visited set
-          td_preds(qb[0].data(), 0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, ctr.data(), (unsigned long long)nv);
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
-                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data(), mpred,
-                             mnmap);
+                             0ull, qb[1].data(), 0ull, qb[2].data(), 0ull, vis.data(), nullptr, ctr.data(), pred,
+                             a.nmap);
           CGX_LAUNCH_CHECK();
           bfs_args<V, E> b = a;
           b.depth          = (V)(depth + 1);
@@ -1167,10 +1020,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           bool const next_bu = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
           bool const last    = n_f == 0 || depth + 1 >= limit;
           if (!last && !next_bu) {
-            td_preds(qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], nullptr, n_f);
             hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s,
                                qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(),
-                               nullptr, nullptr, mpred, mnmap);
+                               nullptr, nullptr, pred, a.nmap);
             CGX_LAUNCH_CHECK();
           }
           have_bitmap = false;
@@ -1199,10 +1051,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         bool const next_bu   = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
         bool const last      = n_f == 0 || depth + 1 >= limit;
         if (!last && !next_bu) {
-          td_preds(qb[0].data(), ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], nullptr, n_f);
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),
                              ncur[0], qb[1].data(), ncur[1], qb[2].data(), ncur[2], vis.data(), nullptr, nullptr,
-                             mpred, mnmap);
+                             pred, a.nmap);
           CGX_LAUNCH_CHECK();
         }
         for (int c = 0; c < 3; ++c) std::swap(qa[c], qb[c]);
@@ -1222,18 +1073,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     }
     // a depth limit ended the loop on a top-down level's discoveries: their
     // predecessors to external ids (bottom-up levels wrote external ids already)
-    if (have_queue && n_f > 0 && levels > 0) {
-      td_preds(qa[0].data(), ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], nullptr, n_f);
-      if (mnmap) {
-        hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
-                           ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), nullptr, nullptr, mpred,
-                           mnmap);
-        CGX_LAUNCH_CHECK();
-      }
-    }
-    if (finish_pass && pred && sizeof(V) == 4 && g.renumbered) {
-      hipLaunchKernelGGL(k_finish_pred4, dim3(grid_for((nv + 15) / 16, kBlock, 8192)), dim3(kBlock), 0, s,
-                         reinterpret_cast<int*>(pred), (size_t)nv, -1, g.number_map.data<int>());
+    if (a.nmap && have_queue && n_f > 0 && levels > 0) {
+      hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qa[0].data(),
+                         ncur[0], qa[1].data(), ncur[1], qa[2].data(), ncur[2], vis.data(), nullptr, nullptr, pred,
+                         a.nmap);
       CGX_LAUNCH_CHECK();
     }
     h.last_bfs_levels    = levels;

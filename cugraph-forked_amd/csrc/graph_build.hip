@@ -198,6 +198,9 @@ __global__ __launch_bounds__(kRsThreads) void k_row_sums_tiles(E const* off, W c
   __shared__ W t_w[kRsTile];
   __shared__ int32_t t_off[kRsTile + 1];  // row starts relative to t0, clamped to n + 1 (a spill)
   __shared__ double sm[4];
+  __shared__ int32_t t_long[kRsTile / 48 + 1];  // rows longer than kRsShort (below): at most n / 49
+  __shared__ int n_long;
+  if (threadIdx.x == 0) n_long = 0;
   int64_t const b  = blockIdx.x;
   int64_t const t0 = b * kRsTile;
   int64_t const t1 = min(ne, t0 + kRsTile);
@@ -223,11 +226,19 @@ __global__ __launch_bounds__(kRsThreads) void k_row_sums_tiles(E const* off, W c
   for (int i = threadIdx.x; i < (int)(h_end - t0); i += kRsThreads) hs += (double)t_w[i];
   hs = block_sum_256(hs, sm);
   if (threadIdx.x == 0) head[b] = hs;
-  // rows owned by the tile: complete ones summed here (two interleaved sums, in edge
-  // order), the last may spill past t1
+  // rows owned by the tile: complete ones summed here, the last may spill past t1.
+  // Rows of up to kRsShort edges: one thread each, in edge order; longer rows: one
+  // wave each (lane-strided fp64 partials, then a fixed shuffle tree) -- a thread
+  // walking a 1000-edge row through LDS held its whole block back.  Both orders are
+  // fixed, so the sums are deterministic.
+  constexpr int kRsShort = 48;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += kRsThreads) {
     int64_t const a = row_start(r), e = row_start(r + 1);
     if (e > t1) continue;  // the spill row: block partial below
+    if (e - a > kRsShort) {
+      t_long[atomicAdd(&n_long, 1)] = (int32_t)(r - r0);
+      continue;
+    }
     double s0 = 0.0, s1 = 0.0;
     int64_t k = a;
     for (; k + 1 < e; k += 2) {
@@ -236,6 +247,17 @@ __global__ __launch_bounds__(kRsThreads) void k_row_sums_tiles(E const* off, W c
     }
     if (k < e) s0 += (double)t_w[k - t0];
     out[r] = static_cast<W>(s0 + s1);
+  }
+  __syncthreads();
+  int const lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = wave; j < n_long; j += kRsThreads / 64) {
+    int64_t const r = r0 + t_long[j];
+    int64_t const a = row_start(r), e = row_start(r + 1);
+    double x = 0.0;
+    for (int64_t k = a + lane; k < e; k += 64) x += (double)t_w[k - t0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    if (lane == 0) out[r] = static_cast<W>(x);
   }
   double ts = 0.0;
   bool const spill = nr > 0 && row_start(r1) > t1;

@@ -168,26 +168,23 @@ def test_probe_vector_loads_same_result(scale, monkeypatch):
             check_vs_oracle(s, d, v, dist, pred, [x])
 
 
-@pytest.mark.parametrize("mode", [{"CGX_BFS_TD_PRED": "pass"}, {"CGX_BFS_PRED_FINISH": "1"}])
 @pytest.mark.parametrize("scale", [14, 18])
-def test_predecessor_forms_same_result(scale, mode, monkeypatch):
-    """The three ways to the smallest-id external predecessor give the same arrays:
-    atomicMin in the top-down claim with the ids translated as each level's queue
-    is marked (default), the top-down levels' parents found afterwards by k_td_pred
-    (CGX_BFS_TD_PRED=pass), and internal ids translated by one pass at the end
-    (CGX_BFS_PRED_FINISH=1) -- direction-optimising and top-down only, with and
-    without a depth limit, several sources."""
+def test_predecessors_every_level_kind(scale):
+    """External-id predecessors are written during the traversal: bottom-up levels
+    store them directly, a top-down level's (smallest parent by atomicMin on internal
+    ids) are translated when its queue is marked -- or after the loop when a depth
+    limit ends it.  Direction-optimising and top-down-only traversals (which take
+    different paths through that) must give the same arrays, with and without a
+    depth limit, from one and several sources; checked against the oracle at 14."""
     s, d = rmat_sym(scale)
     h, G = make_graph(s, d, None, renumber=True, symmetric=True)
     deg = np.bincount(s)
-    cases = [([int(np.argmax(deg))], True, 0), ([int(s[len(s) // 3])], True, 0), ([int(d[-1])], False, 0),
-             ([int(s[7]), int(d[11])], True, 2), ([int(s[5])], False, 3)]
-    base = [run(h, G, x, do, depth) for x, do, depth in cases]
-    for k, val in mode.items():
-        monkeypatch.setenv(k, val)
-    for (x, do, depth), (v0, d0, p0) in zip(cases, base):
-        v, dist, pred = run(h, G, x, do, depth)
-        assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0), (x, do, depth)
+    cases = [([int(np.argmax(deg))], 0), ([int(s[len(s) // 3])], 0), ([int(d[-1])], 0),
+             ([int(s[7]), int(d[11])], 2), ([int(s[5])], 3), ([int(s[9])], 1)]
+    for x, depth in cases:
+        v0, d0, p0 = run(h, G, x, False, depth)
+        v, dist, pred = run(h, G, x, True, depth)
+        assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0), (x, depth)
         if scale == 14:
             check_vs_oracle(s, d, v, dist, pred, x, depth_limit=depth or None)
 
