@@ -145,12 +145,13 @@ __device__ __forceinline__ bool cas_claim(V* dist, V v, V nd)
   }
 }
 
-// unsigned: predecessors start at -1 (all ones), the unreached value of the result
+// unsigned: predecessors start at -1 (all ones), the unreached value of the result.
+// Returns whether this was the vertex's first parent (the old value was -1).
 template <typename V>
-__device__ __forceinline__ void atomic_min_v(V* p, V x)
+__device__ __forceinline__ bool atomic_min_first(V* p, V x)
 {
-  if constexpr (sizeof(V) == 4) atomicMin(reinterpret_cast<unsigned*>(p), (unsigned)x);
-  else atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)x);
+  if constexpr (sizeof(V) == 4) return atomicMin(reinterpret_cast<unsigned*>(p), (unsigned)x) == ~0u;
+  else return atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)x) == ~0ull;
 }
 
 // wave-aggregated append: every active lane with `take` gets a distinct slot
@@ -257,8 +258,15 @@ __device__ __forceinline__ void visit_edge(bfs_args<V, E> const& a, wave_stage<V
   if (active) {
     uint32_t bit = 1u << (uint32_t(v) & 31u);
     if (!(a.vis[v >> 5] & bit)) {  // not visited before this level
-      if (a.pred) atomic_min_v<V>(a.pred + v, u);
-      take = cas_claim<V>(a.dist, v, (V)(a.depth + 1));
+      if (a.pred) {
+        // one atomic per edge: the smallest-parent atomicMin is also the claim (its
+        // first caller sees -1), and the claimer stores the distance -- was atomicMin
+        // + a CAS on the distance
+        take = atomic_min_first<V>(a.pred + v, u);
+        if (take) a.dist[v] = (V)(a.depth + 1);
+      } else {
+        take = cas_claim<V>(a.dist, v, (V)(a.depth + 1));
+      }
     }
   }
   push_next<V, E>(a, st, v, take, my_m);
