@@ -802,6 +802,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   a.ctr   = ctr.data();
   a.nv    = nv;
   a.order = (dir_opt && !adj.degree_sorted) ? adj.order.data<V>() : nullptr;
+  a.items = dir_opt ? adj.items.data<work_item>() : nullptr;
   a.nmap  = (pred && g.renumbered) ? g.number_map.data<V>() : nullptr;
   // Level counters: k_publish_seq into the handle's coherent block and a host spin on
   // its sequence word -- no hipStreamSynchronize per level (measured against a D2H

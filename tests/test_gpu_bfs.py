@@ -114,6 +114,27 @@ def test_isolated_source_and_unrenumbered_gaps():
     assert dist[v == 5][0] == 0 and np.all(dist[v != 5] == INT32_MAX)
 
 
+@pytest.mark.parametrize("scale", [12, 16])
+def test_unrenumbered_direction_optimising(scale):
+    """renumber=False with ids that do not descend by degree: the bottom-up levels run
+    the one-pass k_bottomup over the degree-binned work items (not the probe, which
+    needs the identity order), predecessors stay internal = external ids.  Same
+    arrays as the top-down-only traversal, and the oracle at 12."""
+    s, d = rmat_sym(scale)
+    n = int(max(s.max(), d.max())) + 1
+    perm = np.random.default_rng(3).permutation(n)
+    ps, pd_ = perm[s], perm[d]
+    h, G = make_graph(ps, pd_, None, renumber=False, symmetric=True)
+    deg = np.bincount(ps, minlength=n)
+    for x in (int(np.argmax(deg)), int(ps[len(ps) // 2])):
+        v0, d0, p0 = run(h, G, [x], False)
+        v, dist, pred = run(h, G, [x], True)
+        assert h.last_bfs_bottom_up_steps() > 0
+        assert np.array_equal(v, v0) and np.array_equal(dist, d0) and np.array_equal(pred, p0)
+        if scale == 12:
+            check_vs_oracle(ps, pd_, v, dist, pred, [x])
+
+
 @pytest.mark.parametrize("transposed", [False, True])
 def test_extract_paths_c_golden(golden, transposed):
     g = golden["extract_paths_c"]
