@@ -885,6 +885,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     V limit = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
                                               (unsigned long long)std::numeric_limits<V>::max());
     size_t levels = 0, bu_steps = 0;
+    int bu_phase = 0;  // bottom-up levels since the last top-down one
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
     // probe neighbours by 16-byte loads (needs the padded adjacency, int32 ids; RMAT-24
     // k_bu_probe 133.6 -> 129.5 us average; CGX_BFS_PROBE_VEC=0: dword gathers, A/B)
@@ -925,27 +926,63 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           have_bitmap = true;
         }
         bool const probe_path = a.order == nullptr;  // (else the one-pass k_bottomup: no identity order)
-        if (!probe_path) HIP_CHECK(hipMemsetAsync(nxt.data(), 0, nwords * 4, s));  // the probe writes every word
-        if (probe_path) {  // probe + residual (identity order)
-          // (measured and rejected: two chunks per wave in flight, 337K vs 370K MTEPS on
-          // RMAT-24 -- the probe is not bound by one wave's load chain)
-          unsigned const pg = grid_for((nv + 63) / 64, kBlock / 64, probe_grid);
-          if (probe_vec) hipLaunchKernelGGL((k_bu_probe<V, E, true>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
-          else hipLaunchKernelGGL((k_bu_probe<V, E, false>), dim3(pg), dim3(kBlock), 0, s, a, qb[0].data());
+        auto bu_level = [&](bfs_args<V, E> const& x) {
+          if (probe_path) {  // probe + residual (identity order)
+            // (measured and rejected: two chunks per wave in flight, 337K vs 370K MTEPS on
+            // RMAT-24 -- the probe is not bound by one wave's load chain)
+            unsigned const pg = grid_for((nv + 63) / 64, kBlock / 64, probe_grid);
+            if (probe_vec) hipLaunchKernelGGL((k_bu_probe<V, E, true>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            else hipLaunchKernelGGL((k_bu_probe<V, E, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            CGX_LAUNCH_CHECK();
+            hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, x, qb[0].data());
+          } else {
+            HIP_CHECK(hipMemsetAsync(x.nxt, 0, nwords * 4, s));  // (the probe writes every word itself)
+            hipLaunchKernelGGL((k_bottomup<V, E>), dim3(adj.num_items), dim3(kBlock), 0, s, x);
+          }
           CGX_LAUNCH_CHECK();
-          hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, a, qb[0].data());
+        };
+        bu_level(a);
+        // A bottom-up phase's first level is followed by another bottom-up level (its
+        // frontier is the phase's largest): that level is launched at once, on the
+        // bitmap this one writes and with its own counters, and both come back with
+        // one host round trip.  The direction changes no result, so the guess costs
+        // time only when it is wrong.
+        bool const spec_bu = dir_opt && bu_phase == 0 && depth + 1 < limit;
+        if (spec_bu) {
+          bfs_args<V, E> b = a;
+          b.depth          = (V)(depth + 1);
+          b.ctr            = ctr3.data();
+          b.fr             = a.nxt;  // this level's discoveries
+          b.nxt            = a.fr;   // (rewritten whole by the next level)
+          bu_level(b);
+          read_ctr(nullptr, ctr3.data());
+          bfs_ctr_hdr const l2 = pctr[1];
+          n_f = hctr->next_n;
+          m_f = hctr->next_m;
+          if (dbg)
+            std::fprintf(stderr, "[bfs] level %d bottom-up n_f=%llu m_f=%llu m_u=%llu (speculated next)\n", (int)depth,
+                         n_f, m_f, m_u);
+          m_u = m_u > m_f ? m_u - m_f : 0;
+          ++depth;
+          ++levels;
+          ++bu_steps;
+          have_queue = false;
+          if (n_f == 0) break;  // (the next level ran on an empty frontier)
+          n_f = l2.next_n;  // the next level's; its frontier is in fr again (two swaps)
+          m_f = l2.next_m;
+          bu_phase += 2;
         } else {
-          hipLaunchKernelGGL((k_bottomup<V, E>), dim3(adj.num_items), dim3(kBlock), 0, s, a);
+          read_ctr();
+          std::swap(a.fr, a.nxt);
+          std::swap(fr, nxt);
+          have_queue = false;
+          n_f = hctr->next_n;
+          m_f = hctr->next_m;
+          ++bu_phase;
         }
-        CGX_LAUNCH_CHECK();
-        read_ctr();
-        std::swap(a.fr, a.nxt);
-        std::swap(fr, nxt);
-        have_queue = false;
-        n_f = hctr->next_n;
-        m_f = hctr->next_m;
         ++bu_steps;
       } else {
+        bu_phase = 0;
         if (!have_queue) {
           // frontier bitmap -> queues with no host round trip: the conversion counts
           // into ctr2, k_topdown reads the queue lengths from there and the grid is
