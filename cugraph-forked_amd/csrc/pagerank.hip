@@ -2050,13 +2050,57 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
 //   destinations -> column reduce-scatter (u64 sums: exact) -> apply on the owned
 //   vertices -> world allreduce of (diff, dangling) -> state update.
 // Everything is stream-ordered; the host reads the convergence flag once per chunk.
-struct mg_pr_block {
-  int64_t nmax_row = 0, nmax_col = 0;
-  pr_push_t pp;
-  buffer outw;  // weight_t[n_own]
+//
+// Row chunks (R > 1): the block's destination rows are cut into K chunks of cs
+// owner-local rows, chunk k holding rows [k cs, (k + 1) cs) of every owner in the
+// column, laid out [owner][row] -- so chunk k's sums are one contiguous R x cs array
+// and its reduce-scatter hands each owner its cs rows of the chunk.  Each chunk has
+// its own push schedule; the iteration pushes the chunks one after another and
+// reduce-scatters chunk k on a second stream while the push works on chunk k + 1.
+struct mg_chunk {
+  pr_push_t pp;              // rows: owner * cs + (owner-local row - k cs)
   dbuf<int64_t> multi_wins;  // windows summed by several items (their sums are added: cleared per iteration)
   int64_t nmulti = 0;
 };
+
+struct mg_pr_block {
+  int64_t nmax_row = 0, nmax_col = 0;
+  int K = 1;                       // row chunks (1 when R = 1: no reduce-scatter to overlap)
+  int64_t cs = 0;                  // owner-local rows per chunk
+  std::vector<mg_chunk> ch;
+  buffer outw;  // weight_t[n_own]
+  hipStream_t comm_stream = nullptr;  // the chunks' reduce-scatters (R > 1)
+  std::vector<hipEvent_t> ev;         // K push-done events + 1 reduce-scatters-done
+  ~mg_pr_block()
+  {
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
+  }
+};
+
+// first position of each key 0..K in a sorted array (K + 1 binary searches)
+__global__ void k_sorted_starts(uint32_t const* sorted, int64_t n, int K, int64_t* st)
+{
+  for (int k = threadIdx.x; k <= K; k += blockDim.x) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      int64_t const mid = (lo + hi) >> 1;
+      if ((int)sorted[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    st[k] = lo;
+  }
+}
+
+// chunk of each edge's destination row, and the row within the chunk's [owner][row] array
+__global__ void k_mg_row_chunks(uint32_t* rows, int64_t ne, int64_t nmax_col, int64_t cs, uint32_t* chunk)
+{
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const q = rows[e] / nmax_col, l = rows[e] % nmax_col, k = l / cs;
+    chunk[e] = (uint32_t)k;
+    rows[e]  = (uint32_t)(q * cs + (l - k * cs));
+  }
+}
 
 // zero the sums of the listed windows (each 2^wb u64 words)
 __global__ void k_clear_windows(unsigned long long* acc, int64_t const* wins, int64_t n, int wb)
@@ -2126,9 +2170,46 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
                        mg.dst.data<V>(), ne, voff_d.data(), P, C, blk->nmax_row, blk->nmax_col, rows.data(),
                        cols.data());
   CGX_LAUNCH_CHECK();
-  build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), g.weighted ? mg.w.data<R>() : nullptr, ne, n_rows,
-                                   n_cols, blk->pp);
-  int64_t bad = ctx.world->host_allreduce<int64_t>(blk->pp.ok ? 0 : 1, CGX_COMM_SUM, s);
+  // row chunks: K = 4 from 64K rows per owner when the column has several ranks
+  // (CGX_MG_CHUNKS: any K, for the tests), else one chunk = the whole block
+  int K = 1;
+  if (R_ > 1) {
+    char const* ek = std::getenv("CGX_MG_CHUNKS");
+    K = ek ? std::max(1, std::atoi(ek)) : (blk->nmax_col >= 4 * 16384 ? 4 : 1);
+    K = (int)std::min<int64_t>(K, std::max<int64_t>(blk->nmax_col, 1));
+  }
+  blk->K  = K;
+  blk->cs = std::max<int64_t>((blk->nmax_col + K - 1) / K, 1);
+  blk->ch.resize(K);
+  int64_t const n_rows_k = R_ * blk->cs;
+  R const* const w_in    = g.weighted ? mg.w.data<R>() : nullptr;
+  (void)n_rows;
+  if (K == 1) {  // (cs = nmax_col: the rows are already owner * cs + owner-local row)
+    build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), w_in, ne, n_rows_k, n_cols, blk->ch[0].pp);
+  } else {
+    dbuf<uint32_t> chunk(ne, s), chunk_s(ne, s), iv(ne, s), perm(ne, s), rows_s(ne, s), cols_s(ne, s);
+    dbuf<R> w_s(w_in ? ne : 1, s);
+    hipLaunchKernelGGL(k_mg_row_chunks, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, rows.data(), ne,
+                       blk->nmax_col, blk->cs, chunk.data());
+    CGX_LAUNCH_CHECK();
+    iota<uint32_t>(iv.data(), ne, 0u, s);
+    radix_sort_pairs<uint32_t, uint32_t>(chunk.data(), chunk_s.data(), iv.data(), perm.data(), ne, 0,
+                                         bits_for((unsigned long long)K), s);
+    gather<uint32_t, uint32_t>(rows_s.data(), rows.data(), perm.data(), ne, s);
+    gather<uint32_t, uint32_t>(cols_s.data(), cols.data(), perm.data(), ne, s);
+    if (w_in) gather<R, uint32_t>(w_s.data(), w_in, perm.data(), ne, s);
+    dbuf<int64_t> st_d(K + 1, s);
+    hipLaunchKernelGGL(k_sorted_starts, dim3(1), dim3(64), 0, s, chunk_s.data(), ne, K, st_d.data());
+    CGX_LAUNCH_CHECK();
+    auto const st = to_host(st_d.data(), K + 1, s);
+    for (int k = 0; k < K; ++k)
+      build_push_from_coo<uint32_t, R>(s, rows_s.data() + st[k], cols_s.data() + st[k],
+                                       w_in ? w_s.data() + st[k] : nullptr, st[k + 1] - st[k], n_rows_k, n_cols,
+                                       blk->ch[k].pp);
+  }
+  bool ok = true;
+  for (auto const& c_ : blk->ch) ok = ok && c_.pp.ok;
+  int64_t bad = ctx.world->host_allreduce<int64_t>(ok ? 0 : 1, CGX_COMM_SUM, s);
   CGX_EXPECTS(bad == 0, CUGRAPH_NOT_IMPLEMENTED, "MG PageRank: a 2D block exceeds the 32-bit push packing");
   // out-weight sums: per-block partials (sorted, deterministic) -> row reduce-scatter
   dbuf<double> part(std::max<int64_t>(n_cols, 1), s), own(std::max<int64_t>(blk->nmax_row, 1), s);
@@ -2161,15 +2242,20 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
     hipLaunchKernelGGL(k_to_weight<R>, dim3(grid_for(n_own, kBlock, 4096)), dim3(kBlock), 0, s, own.data(), n_own,
                        blk->outw.data<R>());
   CGX_LAUNCH_CHECK();
-  {  // the windows whose sums are added (several items), cleared after each reduce-scatter
-    auto hm = blk->pp.win_multi.empty() ? std::vector<uint8_t>{}
-                                        : to_host(blk->pp.win_multi.data<uint8_t>(), (size_t)blk->pp.nwin, s);
+  for (auto& c_ : blk->ch) {  // the windows whose sums are added (several items), cleared after each reduce-scatter
+    auto hm = c_.pp.win_multi.empty() ? std::vector<uint8_t>{}
+                                      : to_host(c_.pp.win_multi.data<uint8_t>(), (size_t)c_.pp.nwin, s);
     std::vector<int64_t> wl;
     for (int64_t w = 0; w < (int64_t)hm.size(); ++w)
       if (hm[w]) wl.push_back(w);
-    blk->nmulti = (int64_t)wl.size();
-    blk->multi_wins.resize(std::max<size_t>(wl.size(), 1), s);
-    to_device(blk->multi_wins.data(), wl.data(), wl.size(), s);
+    c_.nmulti = (int64_t)wl.size();
+    c_.multi_wins.resize(std::max<size_t>(wl.size(), 1), s);
+    to_device(c_.multi_wins.data(), wl.data(), wl.size(), s);
+  }
+  if (R_ > 1) {
+    HIP_CHECK(hipStreamCreateWithFlags(&blk->comm_stream, hipStreamNonBlocking));
+    blk->ev.resize(K + 1);
+    for (auto& e : blk->ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   HIP_CHECK(hipStreamSynchronize(s));
   mg.pr_block = blk;
@@ -2339,8 +2425,10 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   }
   dbuf<R> x_send(std::max<int64_t>(blk.nmax_row, 1), s), x_row(std::max<int64_t>(C * blk.nmax_row, 1), s);
   fill<R>(x_send.data(), std::max<int64_t>(blk.nmax_row, 1), R(0), s);
-  dbuf<unsigned long long> acc_own(std::max<int64_t>(blk.nmax_col, 1), s);
-  fill<unsigned long long>(acc_own.data(), std::max<int64_t>(blk.nmax_col, 1), 0ull, s);
+  int const K         = blk.K;
+  int64_t const n_accown = std::max<int64_t>(K * blk.cs, 1);  // chunk k's reduce-scatter lands at k cs
+  dbuf<unsigned long long> acc_own(n_accown, s);
+  fill<unsigned long long>(acc_own.data(), n_accown, 0ull, s);
   dbuf<double> partials(2 * 4096, s);
   dbuf<unsigned long long> sums(2, s);
   dbuf<pr_state> st(1, s);
@@ -2360,8 +2448,11 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   a.mg_sums   = sums.data();
   a.x_in      = x_row.data();
   a.x_out     = x_send.data();
-  // fp32 packed push: x~ travels (allgather) and is read as enc_fixed words, as on one GPU
-  a.enc       = blk.pp.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
+  // fp32 packed push: x~ travels (allgather) and is read as enc_fixed words, as on one
+  // GPU -- when every chunk with edges has the packed format (the words are shared)
+  bool all_packed = true;
+  for (auto const& c_ : blk.ch) all_packed = all_packed && (c_.pp.packed || c_.pp.nunits == 0);
+  a.enc = all_packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
   int const nblk_init = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 1024);
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
@@ -2370,41 +2461,53 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   CGX_LAUNCH_CHECK();
   if (max_iter == 0) fail(CUGRAPH_UNKNOWN_ERROR, "PageRank failed to converge.");
 
-  push_args<V, E, R> sp{}, sap{};
-  sp.a = a;
-  set_queue_args(sp, blk.pp, s);
-  sp.win_bits = blk.pp.win_bits;
   // R > 1: the block's sums go through the column reduce-scatter into acc_own, which
   // the apply reads and leaves (the next reduce-scatter overwrites it); afterwards only
   // the windows summed by several items are cleared (stored windows are overwritten).
+  // With K > 1 row chunks the chunks are pushed one after another and chunk k's
+  // reduce-scatter (with its clears and queue-head reset) runs on the block's comm
+  // stream, after an event, while the push works on chunk k + 1; the apply waits for
+  // the last one.
   // R = 1 (one grid row): the block's sums are already the owner's; as on one GPU the
   // apply reads them in place and clears the added windows -- or, with 16K windows, the
   // push applies each window itself (fused_finish) and leaves its (diff, dangling) in
   // mg_sums
   bool const col_reduce = R_ > 1;
-  sap = sp;
-  sap.acc       = col_reduce ? acc_own.data() : sp.acc;
+  hipStream_t const cst = K > 1 ? blk.comm_stream : s;
+  std::vector<push_args<V, E, R>> spk(K);
+  std::vector<int> nblk_push(K);
+  std::vector<decltype(push_kernel<V, E, R>(blk.ch[0].pp, false, false))> pker(K);
+  std::vector<char> calibrating(K, 0);
+  for (int k = 0; k < K; ++k) {
+    pr_push_t& pp = blk.ch[k].pp;
+    spk[k].a      = a;
+    set_queue_args(spk[k], pp, s);
+    spk[k].win_bits = pp.win_bits;
+    nblk_push[k]    = spk[k].nitems && pp.nunits ? push_blocks(pp.win_bits) : 0;
+    pker[k]         = push_kernel<V, E, R>(pp, g.weighted, a.enc != 0);
+    // measured-cost queues (calibrate_queues), per rank and chunk: no collective
+    calibrating[k] = nblk_push[k] && calibration_wanted(pp);
+    if (calibrating[k]) {
+      pp.item_ticks.set_stream(s);
+      pp.item_ticks.resize(pp.nitems * sizeof(uint32_t));
+      HIP_CHECK(hipMemsetAsync(pp.item_ticks.data(), 0, pp.nitems * sizeof(uint32_t), s));
+      pp.calib = 1;
+    } else if (pp.calib == 0) {
+      pp.calib = 2;
+    }
+  }
+  push_args<V, E, R> sap = spk[0];
+  sap.acc       = col_reduce ? acc_own.data() : spk[0].acc;
   sap.keep_acc  = col_reduce ? 1 : 0;
-  sap.win_multi = col_reduce ? nullptr : blk.pp.win_multi.data<uint8_t>();
-  int const nblk_push  = sp.nitems ? push_blocks(blk.pp.win_bits) : 0;
+  sap.win_multi = col_reduce ? nullptr : blk.ch[0].pp.win_multi.data<uint8_t>();
+  if (K > 1) sap.tile_ctr = nullptr;  // (every chunk's heads are reset on the comm stream)
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
-  bool const fused     = !col_reduce && nblk_push && fuse_apply(blk.pp);
-  auto const mg_pkernel = push_kernel<V, E, R>(blk.pp, g.weighted, a.enc != 0);
+  bool const fused     = !col_reduce && K == 1 && nblk_push[0] && fuse_apply(blk.ch[0].pp);
   if (fused) {
-    sp.fuse = 1;
-    sp.nhub = env_is("CGX_PR_HUB", "0") ? 0 : C * blk.nmax_row;  // hub x~ in LDS (row-local source ids)
+    spk[0].fuse = 1;
+    spk[0].nhub = env_is("CGX_PR_HUB", "0") ? 0 : C * blk.nmax_row;  // hub x~ in LDS (row-local source ids)
   }
 
-  // measured-cost queues (calibrate_queues), per rank for its own block: no collective
-  bool calibrating = nblk_push && blk.pp.nunits && calibration_wanted(blk.pp);
-  if (calibrating) {
-    blk.pp.item_ticks.set_stream(s);
-    blk.pp.item_ticks.resize(blk.pp.nitems * sizeof(uint32_t));
-    HIP_CHECK(hipMemsetAsync(blk.pp.item_ticks.data(), 0, blk.pp.nitems * sizeof(uint32_t), s));
-    blk.pp.calib = 1;
-  } else if (blk.pp.calib == 0) {
-    blk.pp.calib = 2;
-  }
   size_t launched = 0;
   std::vector<hipEvent_t> ev;
   pr_state hst{};
@@ -2421,20 +2524,35 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       int const chunk = next_chunk(hst, eps, a.max_iter);
       for (int i = 0; i < chunk; ++i) {
         ctx.row->allgather<R>(x_send.data(), x_row.data(), (size_t)blk.nmax_row, s);
-        sp.item_ticks = calibrating && launched == 0 ? blk.pp.item_ticks.data<uint32_t>() : nullptr;
-        sp.parity     = (int)(launched & 1);
-        sap.parity    = sp.parity;
-        ++launched;
-        if (nblk_push && blk.pp.nunits)
-          hipLaunchKernelGGL(mg_pkernel, dim3(nblk_push), dim3(kPushThreads), 0, s, sp);
-        CGX_LAUNCH_CHECK();
-        if (col_reduce) {
-          ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data(), (size_t)blk.nmax_col, CGX_COMM_SUM, s);
-          if (blk.nmulti)
-            hipLaunchKernelGGL(k_clear_windows, dim3(grid_for(blk.nmulti << blk.pp.win_bits, kBlock, 8192)),
-                               dim3(kBlock), 0, s, sp.acc, blk.multi_wins.data(), blk.nmulti, blk.pp.win_bits);
+        int const parity = (int)(launched & 1);
+        for (int k = 0; k < K; ++k) {
+          mg_chunk& ck     = blk.ch[k];
+          auto& sp         = spk[k];
+          sp.item_ticks    = calibrating[k] && launched == 0 ? ck.pp.item_ticks.data<uint32_t>() : nullptr;
+          sp.parity        = parity;
+          if (nblk_push[k]) hipLaunchKernelGGL(pker[k], dim3(nblk_push[k]), dim3(kPushThreads), 0, s, sp);
           CGX_LAUNCH_CHECK();
+          if (!col_reduce) continue;
+          if (K > 1) {
+            HIP_CHECK(hipEventRecord(blk.ev[k], s));
+            HIP_CHECK(hipStreamWaitEvent(cst, blk.ev[k], 0));
+          }
+          ctx.col->reduce_scatter<unsigned long long>(sp.acc, acc_own.data() + k * blk.cs, (size_t)blk.cs,
+                                                      CGX_COMM_SUM, cst);
+          if (ck.nmulti)
+            hipLaunchKernelGGL(k_clear_windows, dim3(grid_for(ck.nmulti << ck.pp.win_bits, kBlock, 8192)),
+                               dim3(kBlock), 0, cst, sp.acc, ck.multi_wins.data(), ck.nmulti, ck.pp.win_bits);
+          CGX_LAUNCH_CHECK();
+          if (K > 1 && sp.tile_ctr)  // this parity's heads, for the iteration after next
+            HIP_CHECK(hipMemsetAsync(sp.tile_ctr + parity * kQueues * kCtrStride, 0,
+                                     kQueues * kCtrStride * sizeof(unsigned int), cst));
         }
+        if (col_reduce && K > 1) {
+          HIP_CHECK(hipEventRecord(blk.ev[K], cst));
+          HIP_CHECK(hipStreamWaitEvent(s, blk.ev[K], 0));
+        }
+        ++launched;
+        sap.parity = parity;
         if (!fused) hipLaunchKernelGGL((k_pr_apply<V, E, R>), dim3(nblk_apply), dim3(kBlock), 0, s, sap);
         CGX_LAUNCH_CHECK();
         ctx.world->allreduce<unsigned long long>(sums.data(), sums.data(), 2, CGX_COMM_SUM, s);
@@ -2445,10 +2563,11 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       HIP_CHECK(hipMemcpyAsync(hpin, st.data(), sizeof(pr_state), hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
       hst = *hpin;
-      if (calibrating) {
-        calibrate_queues(s, blk.pp);
-        for (int q = 0; q <= kQueues; ++q) sp.qoff[q] = blk.pp.qoff[q];
-        calibrating = false;
+      for (int k = 0; k < K; ++k) {
+        if (!calibrating[k]) continue;
+        calibrate_queues(s, blk.ch[k].pp);
+        for (int q = 0; q <= kQueues; ++q) spk[k].qoff[q] = blk.ch[k].pp.qoff[q];
+        calibrating[k] = 0;
       }
       if (hst.done) break;
     }

@@ -507,7 +507,7 @@ def test_mg_world8_reference_grid(algo, C):
         _spawn(_worker, (8, port, C, 11, False, algo), 8)
 
 
-def _mg_sg_worker(rank, world, port, C, scale):
+def _mg_sg_worker(rank, world, port, C, scale, chunks=None):
     """MG against the single-GPU library on the same graph (the reference's MG tests:
     cpp/tests/link_analysis/mg_pagerank_test.cpp:258-270,333-347 compares MG with SG
     on RMAT(20, 32); cpp/tests/traversal/mg_bfs_test.cpp:160-225):
@@ -525,6 +525,8 @@ def _mg_sg_worker(rank, world, port, C, scale):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if chunks:
+        os.environ["CGX_MG_CHUNKS"] = str(chunks)
     _rank_setup(port, rank)
     import torch
     import torch.distributed as dist
@@ -594,11 +596,15 @@ def _mg_sg_worker(rank, world, port, C, scale):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,C,scale", [(8, 2, 18), (8, 8, 16), (2, 1, 16)])
-def test_mg_equals_sg(world, C, scale):
+@pytest.mark.parametrize("world,C,scale,chunks", [(8, 2, 18, None), (8, 8, 16, None), (2, 1, 16, None),
+                                                  (8, 2, 16, 3), (4, 1, 14, 5)])
+def test_mg_equals_sg(world, C, scale, chunks):
     """The reference's 8-GPU grid (4 x 2) at RMAT-18 and the flat 1 x 8 grid, rehearsed
-    with 8 ranks on the one test GPU (torch.distributed/gloo callbacks)."""
-    _spawn(_mg_sg_worker, (world, _free_port(), C, scale), world, deadline=300.0)
+    with 8 ranks on the one test GPU (torch.distributed/gloo callbacks).  chunks: the
+    PageRank block's rows in that many chunks, pushed one after another with each
+    chunk's column reduce-scatter on the comm stream (CGX_MG_CHUNKS; the default cuts
+    4 chunks only from 64K rows per owner) -- still bitwise SG."""
+    _spawn(_mg_sg_worker, (world, _free_port(), C, scale, chunks), world, deadline=300.0)
 
 
 def _dask_worker(rank, world, port, C):
