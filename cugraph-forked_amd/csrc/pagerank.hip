@@ -489,7 +489,9 @@ inline bool env_is(char const* name, char const* value)
 }
 
 // items per push block on average: a window larger than 1.5 x E / (blocks x this) is
-// cut into shares
+// cut into shares.  RMAT-24 ms/iteration with 2 / 4 / 8 / 16: 0.593 / 0.589-0.599 /
+// 0.620-0.630 / 0.687 (RMAT-26 4: 2.98, 8: 3.06, 16: 3.23; same box): more shares
+// mean more added (not stored) windows, and the balance gained does not pay for them
 constexpr int64_t kShareDiv = 4;
 
 inline bool packed_enabled()
