@@ -97,7 +97,7 @@ __device__ __forceinline__ void fold_parts(bfs_ctr* c, bool zero, unsigned long 
 // -> host[1], also zeroed; src_m: the sources' edge count of a conversion the host
 // did not read (bfs_ctr::next_m of that block) -> pad[2]
 __global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr_hdr* host, unsigned long long seq, int const* bad, bfs_ctr* ctr_b,
-                              bfs_ctr* src_m, int wb_l2)
+                              bfs_ctr* src_m)
 {
   unsigned long long n, m, nb = 0, mb = 0, ns = 0, ms = 0;
   fold_parts(ctr, true, n, m);
@@ -128,16 +128,12 @@ __global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr_hdr* host, unsigned long lon
   if (i < 5 || i >= 10 || ctr_b) __hip_atomic_store(hp + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (i < 5) c[i] = 0ull;
   else if (i < 10 && ctr_b) cb[i - 5] = 0ull;
-  if (wb_l2) {  // (A/B) the system-scope release: also writes the L2's dirty lines back
-    __threadfence_system();  // (lanes 0..11 are one wave: the fence waits for all their stores)
-    if (i != 0) return;
-    __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
   // The host block is fine-grained (coherent, uncached) memory: the words reach it
   // in order once this wave's stores are acknowledged, so a wait for them orders the
   // sequence word behind the data without writing the L2 back (nothing the host
-  // reads is in it; the next kernels are stream-ordered behind this one anyway)
+  // reads is in it; the next kernels are stream-ordered behind this one anyway).  A
+  // system-scope release there (its L2 write-back) measured 0.674-0.675 against
+  // 0.667-0.669 ms per RMAT-24 traversal, same box.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (i != 0) return;
   __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -818,13 +814,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // its sequence word -- no hipStreamSynchronize per level (measured against a D2H
   // copy + synchronize per level: that form was removed)
   bfs_ctr_hdr* pctr = h.polled_as<bfs_ctr_hdr>();  // [0]: a level, [1]: a speculative level
-  bool const pub_wb_l2 = std::getenv("CGX_BFS_PUB_FENCE") != nullptr;  // A/B
   // ctr_b / src_m: see k_publish_seq
   auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr* src_m = nullptr) {
     {
       unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
-      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m,
-                         pub_wb_l2 ? 1 : 0);
+      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m);
       CGX_LAUNCH_CHECK();
       for (unsigned long long n = 1; __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) != seq; ++n) {
         __builtin_ia32_pause();
