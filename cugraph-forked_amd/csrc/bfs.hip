@@ -97,39 +97,56 @@ __device__ __forceinline__ void fold_parts(bfs_ctr* c, bool zero, unsigned long 
 // -> host[1], also zeroed; src_m: the sources' edge count of a conversion the host
 // did not read (bfs_ctr::next_m of that block) -> pad[2]
 __global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr_hdr* host, unsigned long long seq, int const* bad, bfs_ctr* ctr_b,
-                              bfs_ctr* src_m)
+                              bfs_ctr* src_m, bfs_ctr* ctr_c)
 {
-  unsigned long long n, m, nb = 0, mb = 0, ns = 0, ms = 0;
+  unsigned long long n, m, nb = 0, mb = 0, ns = 0, ms = 0, nc = 0, mc = 0;
   fold_parts(ctr, true, n, m);
   if (ctr_b) fold_parts(ctr_b, true, nb, mb);
   if (src_m) fold_parts(src_m, false, ns, ms);
-  // one host word per lane, all stores in flight at once (one thread storing the 12
-  // words one after another made this kernel 4.6 us)
-  int const i = threadIdx.x;
-  if (i >= 12) return;
-  unsigned long long* c  = reinterpret_cast<unsigned long long*>(ctr);
-  unsigned long long* cb = reinterpret_cast<unsigned long long*>(ctr_b);
-  unsigned long long* hp = reinterpret_cast<unsigned long long*>(host);
-  unsigned long long v = 0;
-  int slot             = i;
+  if (ctr_c) fold_parts(ctr_c, true, nc, mc);
+  // One host word per lane, all stores in flight at once (one thread storing the
+  // words one after another made this kernel 4.6 us): lanes 0..4 this level (host
+  // words 0..4), 5..9 ctr_b (host[1]), 10..11 pad[2] / pad[1], 12..16 ctr_c (host[2]).
+  // No lane leaves early: every store is issued before the wave reconverges and
+  // waits for them, and only then is the sequence word stored -- a lane group that
+  // returned early could run its branch after the sequence store.
+  int const i                = threadIdx.x;
+  unsigned long long* const c  = reinterpret_cast<unsigned long long*>(ctr);
+  unsigned long long* const cb = reinterpret_cast<unsigned long long*>(ctr_b);
+  unsigned long long* const cc = reinterpret_cast<unsigned long long*>(ctr_c);
+  unsigned long long* const hp = reinterpret_cast<unsigned long long*>(host);
+  unsigned long long v  = 0;
+  int slot              = -1;  // host word
+  unsigned long long* z = nullptr;  // device counter word to clear
   if (i < 5) {
-    v = i < 3 ? c[i] : (i == 3 ? n : m);
+    v    = i < 3 ? c[i] : (i == 3 ? n : m);
+    slot = i;
+    z    = c + i;
   } else if (i < 10) {
     int const k = i - 5;
-    slot        = 8 + k;  // host[1]
-    if (ctr_b) v = k < 3 ? cb[k] : (k == 3 ? nb : mb);
+    if (ctr_b) {
+      v    = k < 3 ? cb[k] : (k == 3 ? nb : mb);
+      slot = 8 + k;
+      z    = cb + k;
+    }
   } else if (i == 10) {
-    slot = 7;  // pad[2]
     v    = ms;
-  } else {
-    slot = 6;  // pad[1]
+    slot = 7;  // pad[2]
+  } else if (i == 11) {
     v    = bad ? (unsigned long long)*bad : 0ull;
+    slot = 6;  // pad[1]
+  } else if (i < 17) {
+    int const k = i - 12;
+    if (ctr_c) {
+      v    = k < 3 ? cc[k] : (k == 3 ? nc : mc);
+      slot = 16 + k;
+      z    = cc + k;
+    }
   }
-  if (i < 5 || i >= 10 || ctr_b) __hip_atomic_store(hp + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (i < 5) c[i] = 0ull;
-  else if (i < 10 && ctr_b) cb[i - 5] = 0ull;
+  if (slot >= 0) __hip_atomic_store(hp + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (z) *z = 0ull;
   // The host block is fine-grained (coherent, uncached) memory: the words reach it
-  // in order once this wave's stores are acknowledged, so a wait for them orders the
+  // in order once the wave's stores are acknowledged, so waiting for them orders the
   // sequence word behind the data without writing the L2 back (nothing the host
   // reads is in it; the next kernels are stream-ordered behind this one anyway).  A
   // system-scope release there (its L2 write-back) measured 0.674-0.675 against
@@ -788,13 +805,13 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // ctr2: queue lengths of a bitmap -> queues conversion; ctr3: a speculative level's counters
   // one allocation and one memset for the three counter blocks; k_publish_seq
   // zeroes ctr and ctr3 after every read, so they stay clean without more memsets
-  dbuf<bfs_ctr> ctrs(3, s);
-  HIP_CHECK(hipMemsetAsync(ctrs.data(), 0, 3 * sizeof(bfs_ctr), s));
+  dbuf<bfs_ctr> ctrs(4, s);  // (+ ctr4: a second speculative bottom-up level's counters)
+  HIP_CHECK(hipMemsetAsync(ctrs.data(), 0, 4 * sizeof(bfs_ctr), s));
   struct ctr_ref {
     bfs_ctr* p;
     bfs_ctr* data() const { return p; }
   };
-  ctr_ref const ctr{ctrs.data()}, ctr2{ctrs.data() + 1}, ctr3{ctrs.data() + 2};
+  ctr_ref const ctr{ctrs.data()}, ctr2{ctrs.data() + 1}, ctr3{ctrs.data() + 2}, ctr4{ctrs.data() + 3};
   bfs_ctr_hdr* hctr = h.pinned_as<bfs_ctr_hdr>();
 
   bfs_args<V, E> a{};
@@ -815,10 +832,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // copy + synchronize per level: that form was removed)
   bfs_ctr_hdr* pctr = h.polled_as<bfs_ctr_hdr>();  // [0]: a level, [1]: a speculative level
   // ctr_b / src_m: see k_publish_seq
-  auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr* src_m = nullptr) {
+  auto read_ctr = [&](int const* bad_flag = nullptr, bfs_ctr* ctr_b = nullptr, bfs_ctr* src_m = nullptr,
+                      bfs_ctr* ctr_c = nullptr) {
     {
       unsigned long long const seq = __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) + 1;
-      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m);
+      hipLaunchKernelGGL(k_publish_seq, dim3(1), dim3(64), 0, s, ctr.data(), pctr, seq, bad_flag, ctr_b, src_m, ctr_c);
       CGX_LAUNCH_CHECK();
       for (unsigned long long n = 1; __atomic_load_n(&pctr->pad[0], __ATOMIC_ACQUIRE) != seq; ++n) {
         __builtin_ia32_pause();
@@ -948,35 +966,49 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           CGX_LAUNCH_CHECK();
         };
         bu_level(a);
-        // A bottom-up phase's first level is followed by another bottom-up level (its
-        // frontier is the phase's largest): that level is launched at once, on the
-        // bitmap this one writes and with its own counters, and both come back with
-        // one host round trip.  The direction changes no result, so the guess costs
-        // time only when it is wrong.
-        bool const spec_bu = dir_opt && bu_phase == 0 && depth + 1 < limit;
-        if (spec_bu) {
-          bfs_args<V, E> b = a;
-          b.depth          = (V)(depth + 1);
-          b.ctr            = ctr3.data();
-          b.fr             = a.nxt;  // this level's discoveries
-          b.nxt            = a.fr;   // (rewritten whole by the next level)
-          bu_level(b);
-          read_ctr(nullptr, ctr3.data());
-          bfs_ctr_hdr const l2 = pctr[1];
-          n_f = hctr->next_n;
-          m_f = hctr->next_m;
-          if (dbg)
-            std::fprintf(stderr, "[bfs] level %d bottom-up n_f=%llu m_f=%llu m_u=%llu (speculated next)\n", (int)depth,
-                         n_f, m_f, m_u);
-          m_u = m_u > m_f ? m_u - m_f : 0;
-          ++depth;
-          ++levels;
-          ++bu_steps;
+        // A bottom-up phase's first level is followed by two more bottom-up levels (the
+        // first two levels leave frontiers far above nv / beta on every bench root):
+        // those are launched at once, each on the bitmap the level before writes and
+        // with its own counters, and all three come back with one host round trip.
+        // The direction changes no result, so a wrong guess costs time only.  RMAT-24:
+        // 0.669-0.672 ms per traversal against 0.682 with one speculated level (same box).
+        int const nspec = dir_opt && bu_phase == 0 ? (int)std::min<long long>(2, (long long)limit - depth - 1) : 0;
+        if (nspec > 0) {
+          bfs_ctr* const sctr[2] = {ctr3.data(), ctr4.data()};
+          bfs_args<V, E> x       = a;
+          for (int j = 0; j < nspec; ++j) {
+            x.depth = (V)(depth + 1 + j);
+            x.ctr   = sctr[j];
+            std::swap(x.fr, x.nxt);  // reads the level before's discoveries, rewrites the older bitmap whole
+            bu_level(x);
+          }
+          read_ctr(nullptr, ctr3.data(), nullptr, nspec > 1 ? ctr4.data() : nullptr);
+          bfs_ctr_hdr const lv[3] = {*hctr, pctr[1], pctr[2]};
+          bool over = false;
+          for (int j = 0; j < nspec; ++j) {
+            n_f = lv[j].next_n;
+            m_f = lv[j].next_m;
+            if (dbg)
+              std::fprintf(stderr, "[bfs] level %d bottom-up n_f=%llu m_f=%llu m_u=%llu (speculated next)\n",
+                           (int)depth, n_f, m_f, m_u);
+            m_u = m_u > m_f ? m_u - m_f : 0;
+            ++depth;
+            ++levels;
+            ++bu_steps;
+            if (n_f == 0) {  // (the later levels ran on an empty frontier)
+              over = true;
+              break;
+            }
+          }
+          if (over) break;
+          n_f = lv[nspec].next_n;  // the last level's
+          m_f = lv[nspec].next_m;
+          if (nspec % 2 == 0) {  // an odd number of levels: the frontier is in nxt
+            std::swap(a.fr, a.nxt);
+            std::swap(fr, nxt);
+          }
           have_queue = false;
-          if (n_f == 0) break;  // (the next level ran on an empty frontier)
-          n_f = l2.next_n;  // the next level's; its frontier is in fr again (two swaps)
-          m_f = l2.next_m;
-          bu_phase += 2;
+          bu_phase += nspec + 1;
         } else {
           read_ctr();
           std::swap(a.fr, a.nxt);
