@@ -35,6 +35,8 @@ struct handle_t {
   size_t last_bfs_bottom_up  = 0;
   size_t last_louvain_levels = 0;
   double last_louvain_sweep_bytes = 0;  // MG: average bytes sent per sweep by this rank
+  int64_t last_louvain_local_edges = 0;  // MG: this rank's level-0 edges (rows it owns)
+  int64_t last_louvain_ghosts      = 0;  // MG: its level-0 ghosts (distinct remote destinations)
   // Host-pinned scratch for the per-level / per-chunk device state reads and a pool
   // of profiling events, both kept for the handle's lifetime: hipHostMalloc +
   // hipHostFree per call measured ~250 us of host stall per BFS traversal.

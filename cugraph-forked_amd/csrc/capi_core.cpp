@@ -531,5 +531,11 @@ extern "C" double cugraph_amd_last_louvain_sweep_bytes(const cugraph_resource_ha
 {
   return H(handle)->last_louvain_sweep_bytes;
 }
+extern "C" void cugraph_amd_last_louvain_partition(const cugraph_resource_handle_t* handle, int64_t* local_edges,
+                                                   int64_t* ghosts)
+{
+  *local_edges = H(handle)->last_louvain_local_edges;
+  *ghosts      = H(handle)->last_louvain_ghosts;
+}
 extern "C" size_t cugraph_amd_trim_device_cache(void) { return cgx::device_cache_trim(); }
 extern "C" const char* cugraph_amd_version(void) { return "cugraph-forked_amd libcugraph_c gfx950 " __DATE__; }

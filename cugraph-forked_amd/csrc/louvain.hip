@@ -2340,6 +2340,8 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
   res.clusters = std::make_unique<device_array_t>((size_t)n_own, g.vertex_type, s);
   h.last_louvain_levels      = 0;
   h.last_louvain_sweep_bytes = 0;
+  h.last_louvain_local_edges = 0;
+  h.last_louvain_ghosts      = 0;
   res.modularity             = 0;
   if (nv0 == 0) return;
 
@@ -2397,6 +2399,10 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     if (nr) vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
     S.bytes = 0;
     mg_setup_level(S, cur, L, has_edges.data(), k.data());
+    if (dendrogram.empty()) {  // the 1D partition's shape at level 0 (handle statistics)
+      h.last_louvain_local_edges = cur.ne;
+      h.last_louvain_ghosts      = L.ng;
+    }
     phase("setup", dendrogram.size());
     size_t const setup_bytes = S.bytes;
     dendrogram.emplace_back(r1, s);

@@ -79,6 +79,12 @@ class ResourceHandle:
         """Multi-GPU Louvain: average bytes this rank sent per local-move sweep."""
         return _lib.lib.cugraph_amd_last_louvain_sweep_bytes(self.c_resource_handle_ptr)
 
+    def last_louvain_partition(self):
+        """Multi-GPU Louvain: (level-0 edges, level-0 ghosts) of this rank's 1D share."""
+        e, g = ctypes.c_int64(), ctypes.c_int64()
+        _lib.lib.cugraph_amd_last_louvain_partition(self.c_resource_handle_ptr, ctypes.byref(e), ctypes.byref(g))
+        return e.value, g.value
+
     def measure_copy_bandwidth(self, nbytes=4 << 30, reps=10):
         """HBM ceiling: 16-B-per-lane copy kernel on this handle's stream, GB/s (read + write)."""
         r = _lib.lib.cugraph_amd_measure_copy_bandwidth(self.c_resource_handle_ptr, int(nbytes), int(reps))

@@ -117,6 +117,11 @@ size_t cugraph_amd_last_louvain_levels(const cugraph_resource_handle_t* handle);
 /* Multi-GPU Louvain: average bytes this rank sent per local-move sweep (cluster
  * lookups, weight deltas, ghost updates) in the last call; 0 on one GPU */
 double cugraph_amd_last_louvain_sweep_bytes(const cugraph_resource_handle_t* handle);
+/* Multi-GPU Louvain: this rank's level-0 share of the 1D partition in the last call --
+ * its edges (the rows it owns) and its ghosts (distinct destinations owned elsewhere,
+ * whose clusters it mirrors); 0 and 0 on one GPU */
+void cugraph_amd_last_louvain_partition(const cugraph_resource_handle_t* handle, int64_t* local_edges,
+                                        int64_t* ghosts);
 /* Louvain dendrogram (the reference C++ API returns Dendrogram<vertex_t>,
  * louvain_impl.cuh:280-301; the C ABI only exposes the flattened clustering).
  * Level i holds the cluster of every level-i vertex this rank owns, in global-id

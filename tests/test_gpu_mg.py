@@ -241,7 +241,8 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
     v, c, q, levels = plc.louvain_dendrogram(h, G, 100, 1.0)
     # owner-sharded state: per-sweep exchange volume (sends to other ranks only)
     sb = h.last_louvain_sweep_bytes()
-    mine = (v.cpu().numpy(), c.cpu().numpy(), q, [x.cpu().numpy() for x in levels], sb)
+    part = h.last_louvain_partition()  # (level-0 edges, ghosts) of this rank's 1D share
+    mine = (v.cpu().numpy(), c.cpu().numpy(), q, [x.cpu().numpy() for x in levels], sb, part)
     allr = [None] * world
     dist.all_gather_object(allr, mine)
     if rank == 0:  # (every check after the gather: a rank that failed alone would hang the others)
@@ -249,6 +250,11 @@ def _louvain_worker(rank, world, port, C, scale, integer, comm="torch"):
             assert (a[4] > 0) if world > 1 else (a[4] == 0), a[4]
             assert a[4] < 64 * E / world + 4096, a[4]  # O(moved + referenced) per sweep, not O(V)
         assert all(a[2] == q for a in allr)  # every rank returns the same modularity
+        # the 1D partition: every edge at the owner of its source; report the shape
+        assert sum(a[5][0] for a in allr) == E, [a[5] for a in allr]
+        if world > 1:
+            print(f"RMAT-{scale} MG Louvain {world} ranks: level-0 edges per rank {[a[5][0] for a in allr]} "
+                  f"(E={E}), ghosts per rank {[a[5][1] for a in allr]} (V={int(np.unique(np.concatenate([s, d])).size)})")
         nmap = np.concatenate([a[0] for a in allr]).astype(np.int64)  # global id -> external id
         assert np.array_equal(np.sort(nmap), np.unique(np.concatenate([s, d])))
         inv = np.zeros(int(nmap.max()) + 1, dtype=np.int64)
