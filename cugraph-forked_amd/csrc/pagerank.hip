@@ -452,6 +452,7 @@ constexpr int kTileUnits   = 8;    // units per tile below 2^22 rows (RMAT-22: 8
 constexpr int kGroupItems  = 128;  // items per group dealt to a queue
 constexpr int kCtrStride   = 32;   // queue heads 128 B apart
 constexpr int kPushBlocks  = 512;  // persistent grid: two 1024-thread blocks per CU, 256 CUs
+constexpr int kCommCUs     = 16;   // multi-GPU, overlapped reduce-scatters: CUs the push leaves to RCCL (modelled)
 // LDS left beside a 16K-window push block's 128 KB of sums (163,840 B per workgroup on
 // gfx950, less the block's other shared words) for the hub x~ (push_body16 HUB)
 constexpr int kHubBytes = 32768 - 512;
@@ -2486,6 +2487,11 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
     set_queue_args(spk[k], pp, s);
     spk[k].win_bits = pp.win_bits;
     nblk_push[k]    = spk[k].nitems && pp.nunits ? push_blocks(pp.win_bits) : 0;
+    // the push's persistent blocks fill every CU (LDS or registers), so an RCCL
+    // kernel launched beside it would wait for the push to end: with overlapped
+    // reduce-scatters the push leaves kCommCUs CUs free for them
+    if (col_reduce && K > 1 && nblk_push[k])
+      nblk_push[k] -= kCommCUs * (pp.win_bits >= 14 ? 1 : 2);  // (blocks per CU)
     pker[k]         = push_kernel<V, E, R>(pp, g.weighted, a.enc != 0);
     // measured-cost queues (calibrate_queues), per rank and chunk: no collective
     calibrating[k] = nblk_push[k] && calibration_wanted(pp);
