@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 #pragma unroll
     for (int j = 0; j < kApplyBatch; ++j) {
       int64_t const vj = v + j * stride;
-      if (!sa.keep_acc && sa.acc[vj] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
+      if (!sa.keep_acc && f[j] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
       vertex_update_from<V, E, R>(a, (V)vj, (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf, my_diff,
                                   my_dang);
     }
