@@ -764,6 +764,32 @@ __global__ void k_bfs_sources(V* dist, V const* src, size_t ns, int64_t nv, int*
   }
 }
 
+// Quick start (level 0 certainly top-down): the sources straight into the degree-class
+// queues, their lengths and the sources' edge count in c (as k_bitmap_to_queues
+// leaves them) -- one small launch instead of the bitmap pass over all V / 32 words
+// (k_bfs_sources + k_bitmap_to_queues); the frontier bitmap is never set.  A
+// repeated source is dropped by the visited bit it finds already set.
+template <typename V, typename E>
+__global__ void k_bfs_sources_q(V* dist, V const* src, size_t ns, int64_t nv, int* bad, uint32_t* vis, E const* off,
+                                V* q0, V* q1, V* q2, bfs_ctr* c)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < ns; i += (size_t)gridDim.x * blockDim.x) {
+    V const x = src[i];
+    if (x < 0 || (int64_t)x >= nv) {
+      atomicAdd(bad, 1);
+      continue;
+    }
+    uint32_t const bit = 1u << (uint32_t(x) & 31u);
+    if (atomicOr(vis + (x >> 5), bit) & bit) continue;
+    dist[x]       = 0;
+    E const deg   = off[x + 1] - off[x];
+    int const cls = deg <= kSmallDeg ? 0 : (deg <= kMidDeg ? 1 : 2);
+    unsigned long long const pos = atomicAdd(&c->qlen[cls], 1ull);
+    (cls == 0 ? q0 : cls == 1 ? q1 : q2)[pos] = x;
+    atomicAdd(&c->next_m, (unsigned long long)deg);
+  }
+}
+
 template <typename V, typename E, typename W>
 void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size_t depth_limit, bool want_pred,
               bool expensive, paths_result_t& res)
@@ -852,12 +878,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   };
 
   try {
-    // sources -> distance 0, visited, frontier bitmap; then bitmap -> queues
-    hipLaunchKernelGGL(k_bfs_sources<V>, dim3(grid_for(sources->size, kBlock, 1024)), dim3(kBlock), 0, s, dist,
-                       sources->as<V>(), sources->size, nv, bad.data(), vis.data(), fr.data());
-    CGX_LAUNCH_CHECK();
     // the source check comes back with the first counters (one host round trip
-    // fewer); invalid ids were skipped by k_bfs_sources
+    // fewer); invalid ids are skipped by the source kernels
     for (int c = 0; c < 3; ++c) a.qnext[c] = qa[c].data();
     // Level 0 is certainly top-down when even every source at the maximum degree
     // stays below the switch rule: then the source counts are not read here -- level
@@ -880,10 +902,9 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     unsigned long long n_f, m_f, m_u;
     bool pending_src = false;  // level 0's read also returns the source check and the sources' edge count
     if (quick_start) {  // (ctr2 is still zero from the allocation memset)
-      bfs_args<V, E> ac = a;
-      ac.ctr            = ctr2.data();
-      hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, ac,
-                         fr.data(), nwords);
+      hipLaunchKernelGGL((k_bfs_sources_q<V, E>), dim3(grid_for(sources->size, kBlock, 1024)), dim3(kBlock), 0, s,
+                         dist, sources->as<V>(), sources->size, nv, bad.data(), vis.data(), a.off, qa[0].data(),
+                         qa[1].data(), qa[2].data(), ctr2.data());
       CGX_LAUNCH_CHECK();
       for (int c = 0; c < 3; ++c) ncur[c] = sources->size;  // bounds: the grid covers every class
       a.ncur_dev = reinterpret_cast<unsigned long long const*>(ctr2.data());
@@ -892,6 +913,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
       m_u        = (unsigned long long)g.num_edges;
       pending_src = true;
     } else {
+      // sources -> distance 0, visited, frontier bitmap; then bitmap -> queues
+      hipLaunchKernelGGL(k_bfs_sources<V>, dim3(grid_for(sources->size, kBlock, 1024)), dim3(kBlock), 0, s, dist,
+                         sources->as<V>(), sources->size, nv, bad.data(), vis.data(), fr.data());
+      CGX_LAUNCH_CHECK();
       hipLaunchKernelGGL((k_bitmap_to_queues<V, E>), dim3(grid_for(nwords, kBlock, 4096)), dim3(kBlock), 0, s, a,
                          fr.data(), nwords);
       CGX_LAUNCH_CHECK();
