@@ -211,6 +211,7 @@ struct bfs_args {
   V const* order;
   work_item const* items;
   long long blk_mid_start, blk_small_start;  // top-down grid segmentation
+  int const* head;  // nullptr, or kHeadN + 1 words per vertex: its first kHeadN neighbours + degree (k_bfs_head)
 };
 
 // Next-queue appends are staged per wave in LDS (kStage entries per class) and
@@ -586,13 +587,44 @@ __global__ __launch_bounds__(256) void k_bottomup(bfs_args<V, E> a)
 #endif
 constexpr int kProbe = CGX_BFS_PROBE;
 
+// The probe's head table (int32 ids): per vertex 16 bytes, its first kHeadN = 3
+// neighbours (slots past the list repeat the first) and its degree (clamped to
+// 32 bits), so the probe reads 16 contiguous bytes per vertex -- a wave 1 KB in
+// one run -- instead of offsets + a 48-byte span at an unaligned place in the
+// adjacency, and the chain of dependent loads loses its offsets step.  Fewer
+// neighbours per vertex than the adjacency probe's 8 send more vertices to the
+// residual scan, and still win: the probe pass reads every unvisited vertex, the
+// residual only the misses.
+#ifndef CGX_BFS_HEADN
+#define CGX_BFS_HEADN 3
+#endif
+constexpr int kHeadN = CGX_BFS_HEADN;  // 3, 7 or 15 (RMAT-24 ms/traversal: 0.58 / 0.61-0.64 / 0.73)
+constexpr int kHeadQ = (kHeadN + 1) / 4;  // 16-byte words per vertex
+template <typename E>
+__global__ void k_bfs_head(E const* off, int const* idx, int64_t nv, v4i_t* head)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    E const beg = off[v];
+    E const deg = off[v + 1] - beg;
+    int w[kHeadN + 1];
+#pragma unroll
+    for (int t = 0; t < kHeadN; ++t) w[t] = deg > 0 ? idx[beg + (t < deg ? t : 0)] : 0;
+    unsigned long long const d = (unsigned long long)deg;
+    w[kHeadN] = (int)(uint32_t)(d > 0xffffffffull ? 0xffffffffull : d);
+#pragma unroll
+    for (int q = 0; q < kHeadQ; ++q) head[kHeadQ * v + q] = v4i_t{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+  }
+}
+
 // VEC: a lane's first 8 neighbours from three 16-byte loads of the aligned
 // 12-entry span around them (adjacency arrays are padded by 16 entries) instead of
 // 8 dword gathers: consecutive lanes' lists are adjacent, so each load instruction
 // touches about as many cache lines as one dword gather did.
-template <typename V, typename E, bool VEC>
+// HEAD: the first kHeadN neighbours and the degree from the head table (a.head).
+template <typename V, typename E, bool VEC, bool HEAD>
 __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
 {
+  constexpr int NP = HEAD ? kHeadN : kProbe;
   V const nd    = (V)(a.depth + 1);
   int const lane = threadIdx.x & 63;
   unsigned long long my_n = 0, my_m = 0;
@@ -612,16 +644,32 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
     uint32_t const vw = in ? a.vis[v >> 5] : 0xffffffffu;
     bool const un    = in && !((vw >> (uint32_t(v) & 31u)) & 1u);
     E beg = 0, end = 0;
+    int hv[kHeadN + 1] = {};
     if (un) {
-      beg = a.off[v];
-      end = a.off[v + 1];
+      if constexpr (HEAD) {
+        v4i_t const* hp = reinterpret_cast<v4i_t const*>(a.head) + kHeadQ * v;
+#pragma unroll
+        for (int q = 0; q < kHeadQ; ++q) {
+          v4i_t const x = hp[q];
+          hv[4 * q]     = x.x;
+          hv[4 * q + 1] = x.y;
+          hv[4 * q + 2] = x.z;
+          hv[4 * q + 3] = x.w;
+        }
+      } else {
+        beg = a.off[v];
+        end = a.off[v + 1];
+      }
     }
-    int64_t const deg = (int64_t)(end - beg);
+    int64_t const deg = HEAD ? (int64_t)(uint32_t)hv[kHeadN] : (int64_t)(end - beg);
     bool hit = false, more = false;
     V par    = 0;
     if (deg > 0) {
-      V u[kProbe];
-      if constexpr (VEC && sizeof(V) == 4 && kProbe == 8) {
+      V u[NP];
+      if constexpr (HEAD) {
+#pragma unroll
+        for (int t = 0; t < NP; ++t) u[t] = (V)hv[t];
+      } else if constexpr (VEC && sizeof(V) == 4 && kProbe == 8) {
         E const a0   = beg & ~E(3);
         int const sh = (int)(beg - a0);
         v4i_t const* p = reinterpret_cast<v4i_t const*>(a.idx + a0);
@@ -638,17 +686,17 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
 #pragma unroll
         for (int t = 0; t < kProbe; ++t) u[t] = a.idx[beg + (t < deg ? t : 0)];
       }
-      uint32_t fw[kProbe];  // all frontier words first: the loads issue back to back
+      uint32_t fw[NP];  // all frontier words first: the loads issue back to back
 #pragma unroll
-      for (int t = 0; t < kProbe; ++t) fw[t] = a.fr[u[t] >> 5];
+      for (int t = 0; t < NP; ++t) fw[t] = a.fr[u[t] >> 5];
       uint32_t hm = 0;
 #pragma unroll
-      for (int t = 0; t < kProbe; ++t) hm |= (t < deg ? (fw[t] >> (uint32_t(u[t]) & 31u)) & 1u : 0u) << t;
+      for (int t = 0; t < NP; ++t) hm |= (t < deg ? (fw[t] >> (uint32_t(u[t]) & 31u)) & 1u : 0u) << t;
 #pragma unroll
-      for (int t = kProbe - 1; t >= 0; --t)  // the lowest hit wins: the smallest-id frontier neighbour
+      for (int t = NP - 1; t >= 0; --t)  // the lowest hit wins: the smallest-id frontier neighbour
         if ((hm >> t) & 1u) par = u[t];
       hit  = hm != 0;
-      more = !hit && deg > kProbe;
+      more = !hit && deg > NP;
     }
     if (a.pred && pend_v >= 0) a.pred[pend_v] = pend_ext;
     pend_v = -1;
@@ -704,7 +752,7 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
     V const v     = res[p * rcap + (i - (int64_t)s_pre[p])];
     E const beg0  = a.off[v];
     E const end   = a.off[v + 1];
-    for (E base = beg0 + kProbe; base < end; base += w) {
+    for (E base = beg0 + (a.head ? kHeadN : kProbe); base < end; base += w) {
       E const e = base + lane;
       bool hit  = false;
       V u       = 0;
@@ -940,6 +988,19 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // k_bu_probe 133.6 -> 129.5 us average; CGX_BFS_PROBE_VEC=0: dword gathers, A/B)
     char const* pv       = std::getenv("CGX_BFS_PROBE_VEC");
     bool const probe_vec = adj.idx_padded && !(pv && std::string(pv) == "0");
+    // the probe's head table (CGX_BFS_HEAD=0: the adjacency probe, A/B; RMAT-24 0.579 vs 0.666 ms)
+    char const* hd = std::getenv("CGX_BFS_HEAD");
+    if constexpr (sizeof(V) == 4) {
+      if (dir_opt && a.order == nullptr && !(hd && hd[0] == '0')) {
+        if (adj.bfs_head.empty()) {
+          adj.bfs_head = buffer((size_t)nv * 16 * kHeadQ, s);
+          hipLaunchKernelGGL(k_bfs_head<E>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, a.off,
+                             reinterpret_cast<int const*>(a.idx), nv, adj.bfs_head.data<v4i_t>());
+          CGX_LAUNCH_CHECK();
+        }
+        a.head = adj.bfs_head.data<int>();
+      }
+    }
     // Grid sizes: every block ends with same-address atomics on the level counters,
     // which serialise at the memory side (≈8 ns each): RMAT-24 MTEPS with the probe
     // on 512 / 1024 / 2048 / 8192 / 32768 blocks: 166K / 173K / 168K / 148K / 101K
@@ -980,8 +1041,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
             // (measured and rejected: two chunks per wave in flight, 337K vs 370K MTEPS on
             // RMAT-24 -- the probe is not bound by one wave's load chain)
             unsigned const pg = grid_for((nv + 63) / 64, kBlock / 64, probe_grid);
-            if (probe_vec) hipLaunchKernelGGL((k_bu_probe<V, E, true>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
-            else hipLaunchKernelGGL((k_bu_probe<V, E, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            if (x.head) hipLaunchKernelGGL((k_bu_probe<V, E, false, true>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            else if (probe_vec)
+              hipLaunchKernelGGL((k_bu_probe<V, E, true, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            else hipLaunchKernelGGL((k_bu_probe<V, E, false, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
             CGX_LAUNCH_CHECK();
             hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, x, qb[0].data());
           } else {

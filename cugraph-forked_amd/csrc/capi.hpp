@@ -161,6 +161,7 @@ struct adjacency_t {
   std::vector<int64_t> bin_begin;       // positions (in processing order) where each bin starts
   buffer items;                         // work items for the SpMV-like kernels
   int64_t num_items = 0;
+  buffer bfs_head;  // BFS bottom-up probe: 32 B per vertex (bfs.hip k_bfs_head), built on first use
   pr_push_t pr;  // PageRank windowed-push schedule (pagerank.hip), built on first use
 };
 
