@@ -211,6 +211,7 @@ struct bfs_args {
   V const* order;
   work_item const* items;
   long long blk_mid_start, blk_small_start;  // top-down grid segmentation
+  bool head2;       // with head: misses probe the next kProbe neighbours in the adjacency too
   int const* head;  // nullptr, or kHeadN + 1 words per vertex: its first kHeadN neighbours + degree (k_bfs_head)
 };
 
@@ -621,7 +622,7 @@ __global__ void k_bfs_head(E const* off, int const* idx, int64_t nv, v4i_t* head
 // 8 dword gathers: consecutive lanes' lists are adjacent, so each load instruction
 // touches about as many cache lines as one dword gather did.
 // HEAD: the first kHeadN neighbours and the degree from the head table (a.head).
-template <typename V, typename E, bool VEC, bool HEAD>
+template <typename V, typename E, bool VEC, bool HEAD, bool STAGE2>
 __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
 {
   constexpr int NP = HEAD ? kHeadN : kProbe;
@@ -697,6 +698,36 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
         if ((hm >> t) & 1u) par = u[t];
       hit  = hm != 0;
       more = !hit && deg > NP;
+      if constexpr (HEAD && STAGE2 && sizeof(V) == 4) {
+        // the head missed: the next kProbe neighbours from the adjacency (three 16-byte
+        // loads, as the VEC probe) before the vertex goes to the residual scan
+        if (more) {
+          E const b2    = a.off[v] + kHeadN;
+          E const a0    = b2 & ~E(3);
+          int const sh  = (int)(b2 - a0);
+          int64_t const rem = deg - kHeadN;
+          v4i_t const* p = reinterpret_cast<v4i_t const*>(a.idx + a0);
+          v4i_t const c0 = p[0], c1 = p[1], c2 = p[2];
+          int const wv[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+          V w2[kProbe];
+#pragma unroll
+          for (int t = 0; t < kProbe; ++t)
+            w2[t] = (V)(sh == 0 ? wv[t] : sh == 1 ? wv[t + 1] : sh == 2 ? wv[t + 2] : wv[t + 3]);
+#pragma unroll
+          for (int t = 1; t < kProbe; ++t) w2[t] = t < rem ? w2[t] : w2[0];
+          uint32_t f2[kProbe];
+#pragma unroll
+          for (int t = 0; t < kProbe; ++t) f2[t] = a.fr[w2[t] >> 5];
+          uint32_t h2 = 0;
+#pragma unroll
+          for (int t = 0; t < kProbe; ++t) h2 |= (t < rem ? (f2[t] >> (uint32_t(w2[t]) & 31u)) & 1u : 0u) << t;
+#pragma unroll
+          for (int t = kProbe - 1; t >= 0; --t)
+            if ((h2 >> t) & 1u) par = w2[t];
+          hit  = h2 != 0;
+          more = !hit && rem > kProbe;
+        }
+      }
     }
     if (a.pred && pend_v >= 0) a.pred[pend_v] = pend_ext;
     pend_v = -1;
@@ -752,7 +783,7 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
     V const v     = res[p * rcap + (i - (int64_t)s_pre[p])];
     E const beg0  = a.off[v];
     E const end   = a.off[v + 1];
-    for (E base = beg0 + (a.head ? kHeadN : kProbe); base < end; base += w) {
+    for (E base = beg0 + (a.head ? (a.head2 ? kHeadN + kProbe : kHeadN) : kProbe); base < end; base += w) {
       E const e = base + lane;
       bool hit  = false;
       V u       = 0;
@@ -999,6 +1030,10 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
           CGX_LAUNCH_CHECK();
         }
         a.head = adj.bfs_head.data<int>();
+        // head misses then probe neighbours 3..10 in the adjacency (RMAT-24 0.537-0.545 vs
+        // 0.591-0.595 ms without: root 7's first bottom-up level, a frontier few vertices
+        // find among their first 3 neighbours, 0.90 -> 0.66 ms)
+        a.head2 = probe_vec;
       }
     }
     // Grid sizes: every block ends with same-address atomics on the level counters,
@@ -1041,10 +1076,14 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
             // (measured and rejected: two chunks per wave in flight, 337K vs 370K MTEPS on
             // RMAT-24 -- the probe is not bound by one wave's load chain)
             unsigned const pg = grid_for((nv + 63) / 64, kBlock / 64, probe_grid);
-            if (x.head) hipLaunchKernelGGL((k_bu_probe<V, E, false, true>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            if (x.head && x.head2)
+              hipLaunchKernelGGL((k_bu_probe<V, E, false, true, true>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            else if (x.head)
+              hipLaunchKernelGGL((k_bu_probe<V, E, false, true, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
             else if (probe_vec)
-              hipLaunchKernelGGL((k_bu_probe<V, E, true, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
-            else hipLaunchKernelGGL((k_bu_probe<V, E, false, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+              hipLaunchKernelGGL((k_bu_probe<V, E, true, false, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
+            else
+              hipLaunchKernelGGL((k_bu_probe<V, E, false, false, false>), dim3(pg), dim3(kBlock), 0, s, x, qb[0].data());
             CGX_LAUNCH_CHECK();
             hipLaunchKernelGGL((k_bu_residual<V, E>), dim3(residual_grid), dim3(kBlock), 0, s, x, qb[0].data());
           } else {
