@@ -791,7 +791,10 @@ __global__ __launch_bounds__(256) void k_bu_probe(bfs_args<V, E> a, V* res)
 template <typename V, typename E>
 __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* res)
 {
-  constexpr int w = 16;
+#ifndef CGX_BFS_RES_W
+#define CGX_BFS_RES_W 16
+#endif
+  constexpr int w = CGX_BFS_RES_W;
   V const nd       = (V)(a.depth + 1);
   int const tid    = threadIdx.x;
   int const lane   = tid & (w - 1);
@@ -821,7 +824,7 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
         u   = a.idx[e];
         hit = (a.fr[u >> 5] >> (uint32_t(u) & 31u)) & 1u;
       }
-      unsigned long long const gm = (__ballot(hit) >> gbase) & 0xffffull;
+      unsigned long long const gm = (__ballot(hit) >> gbase) & ((1ull << w) - 1ull);
       if (gm) {
         if (lane == __ffsll((long long)gm) - 1) {
           uint32_t const bit = 1u << (uint32_t(v) & 31u);
