@@ -167,9 +167,11 @@ def build_rmat_graph(p, h, scale, seed=42, weighted=False, transposed=True, want
 
 
 # ----------------------------------------------------------------------------- PageRank
-def pagerank_leg(p, args, scale, steps, warmup, ctx=None, weighted=False):
+def pagerank_leg(p, args, scale, steps, warmup, ctx=None, weighted=False, options=None):
     import torch
     h = p.ResourceHandle(ctx.ptr if ctx else None)
+    for k, v in (options or {}).items():  # measurement / A-B switches (include/cugraph_amd/ext.h)
+        h.set_option(k, v)
     # module load (the code objects of every kernel on the path) off the clock: a
     # PageRank on a tiny graph of the same kind, so first_call_ms is the graph's own cost
     small, _, _ = build_rmat_graph(p, h, 10, weighted=weighted, mg=args.mg)
@@ -210,8 +212,8 @@ def pagerank_leg(p, args, scale, steps, warmup, ctx=None, weighted=False):
     value = E * sum(iters) / t
     # algorithmic bytes of one rank's share: (4E + 16V) / N, +4E when the
     # push reads edge weights -- not for all-ones weights, which run the unweighted push
-    # unless CGX_PR_UNIT_W=0 forces the entry-weight push
-    reads_w = bool(weighted) and (weighted != "ones" or os.environ.get("CGX_PR_UNIT_W") == "0")
+    # unless the option pr_unit_w = 0 forces the entry-weight push
+    reads_w = bool(weighted) and (weighted != "ones" or (options or {}).get("pr_unit_w", 1) == 0)
     bytes_per_iter = ((8 if reads_w else 4) * E + 16 * V) / args.world
     avg_ms = kms / max(klaunch, 1)
     achieved = bytes_per_iter / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
@@ -687,18 +689,15 @@ def main():
                 release_caches(p)
                 # the reference Python path's graph: all-ones fp32 weights (simpleGraph.py:840-843),
                 # detected at the first call and run on the unweighted push; then the same graph
-                # on the entry-weight push (CGX_PR_UNIT_W=0: 32-bit entries + 4 B weights)
-                for key, env in (("pagerank_rmat24_weighted", None), ("pagerank_rmat24_weighted_entry_push", "0")):
-                    if env is not None:
-                        os.environ["CGX_PR_UNIT_W"] = env
-                    try:
-                        r2 = pagerank_leg(p, args, args.scale, max(1, args.steps // 2), 1, weighted="ones")
-                    finally:
-                        os.environ.pop("CGX_PR_UNIT_W", None)
+                # on the entry-weight push (option pr_unit_w = 0: 32-bit entries + 4 B weights)
+                for key, opts in (("pagerank_rmat24_weighted", None),
+                                  ("pagerank_rmat24_weighted_entry_push", {"pr_unit_w": 0})):
+                    r2 = pagerank_leg(p, args, args.scale, max(1, args.steps // 2), 1, weighted="ones",
+                                      options=opts)
                     out[key] = pagerank_summary(r2, args, "sg")
                     out[key]["weights"] = "all-ones fp32 (cugraph.Graph unweighted edge list)"
-                    out[key]["push"] = ("unweighted 16-bit entries (unit weights detected)" if env is None else
-                                        "32-bit entries + fp32 entry weights (CGX_PR_UNIT_W=0)")
+                    out[key]["push"] = ("unweighted 16-bit entries (unit weights detected)" if opts is None else
+                                        "32-bit entries + fp32 entry weights (option pr_unit_w = 0)")
                     del r2
                     release_caches(p)
             else:

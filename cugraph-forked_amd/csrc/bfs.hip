@@ -998,7 +998,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // 0 takes its queue lengths on the device (as after a bitmap -> queues
     // conversion) and the source check and the sources' edge count come back with
     // level 0's counters (one host round trip fewer)
-    double const alpha_do = std::getenv("CGX_BFS_ALPHA") ? std::atof(std::getenv("CGX_BFS_ALPHA")) : 40.0;
+    tuning_t const& tu    = h.tune;
+    double const alpha_do = tu.bfs_alpha;
     bool quick_start      = false;
     if (adj.degree_sorted) {
       if (adj.max_degree < 0) {
@@ -1049,13 +1050,11 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     int bu_phase = 0;  // bottom-up levels since the last top-down one
     bool const dbg = std::getenv("CGX_BFS_DEBUG") != nullptr;  // measurement only
     // probe neighbours by 16-byte loads (needs the padded adjacency, int32 ids; RMAT-24
-    // k_bu_probe 133.6 -> 129.5 us average; CGX_BFS_PROBE_VEC=0: dword gathers, A/B)
-    char const* pv       = std::getenv("CGX_BFS_PROBE_VEC");
-    bool const probe_vec = adj.idx_padded && !(pv && std::string(pv) == "0");
-    // the probe's head table (CGX_BFS_HEAD=0: the adjacency probe, A/B; RMAT-24 0.579 vs 0.666 ms)
-    char const* hd = std::getenv("CGX_BFS_HEAD");
+    // k_bu_probe 133.6 -> 129.5 us average; bfs_probe_vec = 0: dword gathers, A/B)
+    bool const probe_vec = adj.idx_padded && tu.bfs_probe_vec;
+    // the probe's head table (bfs_head = 0: the adjacency probe, A/B; RMAT-24 0.579 vs 0.666 ms)
     if constexpr (sizeof(V) == 4) {
-      if (dir_opt && a.order == nullptr && !(hd && hd[0] == '0')) {
+      if (dir_opt && a.order == nullptr && tu.bfs_head) {
         if (adj.bfs_head.empty()) {
           adj.bfs_head = buffer((size_t)nv * 16 * kHeadQ, s);
           hipLaunchKernelGGL(k_bfs_head<E>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, a.off,
@@ -1072,22 +1071,20 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // Grid sizes: every block ends with same-address atomics on the level counters,
     // which serialise at the memory side (≈8 ns each): RMAT-24 MTEPS with the probe
     // on 512 / 1024 / 2048 / 8192 / 32768 blocks: 166K / 173K / 168K / 148K / 101K
-    unsigned const residual_grid = std::getenv("CGX_BFS_RES_GRID") ? (unsigned)std::atoi(std::getenv("CGX_BFS_RES_GRID"))
-                                                                   : 1024u;
+    unsigned const residual_grid = (unsigned)std::max(1, tu.bfs_res_grid);
     // (top-down segments capped at 1024 blocks each: 176.5K vs 148K MTEPS uncapped; 256-2048 within noise)
-    long long const td_cap = std::getenv("CGX_BFS_TD_CAP") ? std::atoll(std::getenv("CGX_BFS_TD_CAP")) : 1024;
+    long long const td_cap = std::max<int64_t>(1, tu.bfs_td_cap);
     // probe grid: with the level counters spread over kCtrParts slots the block-end
     // atomics no longer serialise, and more waves hide the probe's dependent loads
     // (RMAT-24, 3 reps x 8 roots: 1024 / 2048 / 4096 blocks = 318K / 335K / 339K MTEPS)
-    unsigned const probe_grid = std::getenv("CGX_BFS_PROBE_GRID") ? (unsigned)std::atoi(std::getenv("CGX_BFS_PROBE_GRID"))
-                                                                  : 4096u;
+    unsigned const probe_grid = (unsigned)std::max(1, tu.bfs_probe_grid);
     // Direction switch thresholds (Beamer's form).  Our bottom-up is cheap per edge
     // (hub-first adjacency, early exit), so it pays to stay top-down longer and
     // bottom-up longer than Beamer's alpha 14 / beta 24.  RMAT-24 harmonic-mean MTEPS
     // (alpha, beta): (4, 24) 135K; (14, 24) 211K; (14, 64) 218K; (40, 24) 224K;
     // (40, 64) 226K; (80, 64) 223K; (80, 128) 225K; (150, 64) 209K.
-    // Env overrides are measurement only.
-    double const beta_do  = std::getenv("CGX_BFS_BETA") ? std::atof(std::getenv("CGX_BFS_BETA")) : 64.0;
+    // tuning_t overrides are measurement only.
+    double const beta_do  = tu.bfs_beta;
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
       if (dir_opt) {

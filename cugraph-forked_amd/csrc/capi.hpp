@@ -22,11 +22,43 @@ namespace cgx {
 struct mg_graph_t;  // mg_graph.hpp
 struct mg_context;  // comm.hpp (multi-GPU); nullptr for single GPU
 
+// Measurement / A-B switches of the kernels, per handle (cugraph_amd_set_option,
+// include/cugraph_amd/ext.h).  The defaults are the production choices; the other
+// values select the measured alternatives DESIGN.md records, for the A/B scripts and
+// the bitwise-equality tests.  Nothing here is read from the environment.
+// Schedule-time switches (pr_win_bits, pr_packed, pr_whole) apply to schedules built
+// after they are set: the push schedule is cached on the graph.
+struct tuning_t {
+  int pr_win_bits      = 0;     // 0: by size (push_win_bits); 12 / 13 / 14 force 4K / 8K / 16K windows
+  bool pr_packed       = true;  // 16-bit entries for unweighted graphs (else 32-bit)
+  bool pr_whole        = true;  // windows summed by one item are stored, not added
+  bool pr_calib        = true;  // measured-cost queues after the first launch
+  bool pr_deal_global  = false; // measured items in one longest-first queue instead of 8 XCD queues
+  bool pr_unit_w       = true;  // all-ones weights run the unweighted push
+  bool pr_fuse         = true;  // apply fused into the 16K-window push
+  bool pr_enc          = true;  // x~ as fixed-point words (fp32 single GPU)
+  bool pr_hub          = true;  // hub x~ staged in LDS (16K windows)
+  int mg_chunks        = 0;     // MG overlap chunks (0: by size)
+  double bfs_alpha     = 40.0;  // direction switch (Beamer's alpha / beta)
+  double bfs_beta      = 64.0;
+  bool bfs_probe_vec   = true;  // bottom-up probe by 16-byte loads
+  bool bfs_head        = true;  // bottom-up probe's head table
+  int bfs_res_grid     = 1024;  // residual scan blocks
+  int bfs_probe_grid   = 4096;  // probe blocks
+  int64_t bfs_td_cap   = 1024;  // top-down blocks per degree-class segment
+  bool louvain_hash    = true;  // LDS-hash local move (else sort + reduce-by-key)
+  bool louvain_big_hash = true; // heavy rows on the LDS passes (else the sort path)
+  int louvain_big_cap  = 0;     // (row, bucket) table cap below the built-in one (tests of the fallback)
+  int64_t louvain_big_maxdeg = 0;  // heavy rows above this degree on the sort path (0: the table limit)
+  bool louvain_wide_keys = false;  // 64-bit hash keys below 2^24 ids (tests)
+};
+
 struct handle_t {
   int device         = 0;
   hipStream_t stream = nullptr;
   mg_context* mg     = nullptr;
   bool profiling     = false;
+  tuning_t tune;
   // statistics of the last algorithm call (see include/cugraph_amd/ext.h)
   size_t last_iterations     = 0;
   double last_hot_ms         = 0;

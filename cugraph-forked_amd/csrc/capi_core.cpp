@@ -503,6 +503,47 @@ extern "C" void cugraph_amd_set_profiling(cugraph_resource_handle_t* handle, boo
 {
   H(handle)->profiling = enable == TRUE;
 }
+
+// measurement / A-B switches (tuning_t, capi.hpp): name -> field
+extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t* handle, const char* name,
+                                                       double value, cugraph_error_t** error)
+{
+  *error = nullptr;
+  return guarded(error, [&] {
+    CGX_INPUT(handle && name, "Invalid input argument: handle and name must not be NULL");
+    tuning_t& t = H(handle)->tune;
+    std::string const n(name);
+    auto b   = [&](bool& f) { f = value != 0.0; };
+    auto i32 = [&](int& f) { f = (int)value; };
+    if (n == "pr_win_bits") {
+      CGX_INPUT(value == 0 || value == 12 || value == 13 || value == 14,
+                "Invalid input argument: pr_win_bits must be 0, 12, 13 or 14");
+      i32(t.pr_win_bits);
+    } else if (n == "pr_packed") b(t.pr_packed);
+    else if (n == "pr_whole") b(t.pr_whole);
+    else if (n == "pr_calib") b(t.pr_calib);
+    else if (n == "pr_deal_global") b(t.pr_deal_global);
+    else if (n == "pr_unit_w") b(t.pr_unit_w);
+    else if (n == "pr_fuse") b(t.pr_fuse);
+    else if (n == "pr_enc") b(t.pr_enc);
+    else if (n == "pr_hub") b(t.pr_hub);
+    else if (n == "mg_chunks") i32(t.mg_chunks);
+    else if (n == "bfs_alpha") t.bfs_alpha = value;
+    else if (n == "bfs_beta") t.bfs_beta = value;
+    else if (n == "bfs_probe_vec") b(t.bfs_probe_vec);
+    else if (n == "bfs_head") b(t.bfs_head);
+    else if (n == "bfs_res_grid") i32(t.bfs_res_grid);
+    else if (n == "bfs_probe_grid") i32(t.bfs_probe_grid);
+    else if (n == "bfs_td_cap") t.bfs_td_cap = (int64_t)value;
+    else if (n == "louvain_hash") b(t.louvain_hash);
+    else if (n == "louvain_big_hash") b(t.louvain_big_hash);
+    else if (n == "louvain_big_cap") i32(t.louvain_big_cap);
+    else if (n == "louvain_big_maxdeg") t.louvain_big_maxdeg = (int64_t)value;
+    else if (n == "louvain_wide_keys") b(t.louvain_wide_keys);
+    else if (n == "defaults") t = tuning_t{};
+    else fail(CUGRAPH_INVALID_INPUT, "Invalid input argument: unknown option " + n);
+  });
+}
 extern "C" size_t cugraph_amd_last_iterations(const cugraph_resource_handle_t* handle)
 {
   return H(handle)->last_iterations;

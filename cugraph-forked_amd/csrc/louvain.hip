@@ -1030,7 +1030,8 @@ struct louvain_state {
   dbuf<double> scratch;    // device_sum partials
   dbuf<double> scal;       // 2 scalars
   size_t bytes = 0;        // multi-GPU: bytes this rank sent in the exchanges being counted
-  explicit louvain_state(hipStream_t st) : s(st), scratch(1024, st), scal(2, st) {}
+  tuning_t tune;           // the handle's A/B switches (louvain_*)
+  louvain_state(hipStream_t st, tuning_t const& t) : s(st), scratch(1024, st), scal(2, st), tune(t) {}
 };
 
 // k[v] = weight of row v, self[v] = its self-loop weight, has_edges[v]: segmented
@@ -1174,24 +1175,10 @@ struct sweep_plan {
   std::vector<int64_t> big, big_first, big_deg;  // every heavy row (host)
 };
 
-inline bool hash_sweep_enabled()
+// tuning_t::louvain_big_cap: lower the (row, bucket) table cap (tests of the fallback)
+inline int big_bucket_cap(tuning_t const& tu)
 {
-  char const* e = std::getenv("CGX_LOUVAIN_HASH");  // "0": sort path only (A/B, tests)
-  return !(e && e[0] == '0');
-}
-
-// CGX_LOUVAIN_BIG=sort: heavy rows on the sort path (A/B, tests)
-inline bool big_hash_enabled()
-{
-  char const* e = std::getenv("CGX_LOUVAIN_BIG");
-  return !(e && std::strcmp(e, "sort") == 0);
-}
-
-// CGX_LOUVAIN_BIG_CAP: lower the (row, bucket) table cap (tests of the fallback)
-inline int big_bucket_cap()
-{
-  char const* e = std::getenv("CGX_LOUVAIN_BIG_CAP");
-  int const v   = e ? std::atoi(e) : 0;
+  int const v = tu.louvain_big_cap;
   return v > 0 && v < kBktCap ? v : kBktCap;
 }
 
@@ -1203,7 +1190,7 @@ inline int ceil_log2(int64_t x)
 }
 
 // the heavy rows the LDS passes take; returns the others (sort path)
-std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P)
+std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P, tuning_t const& tu)
 {
   std::vector<int64_t> const& big = P.big;
   std::vector<int64_t> rest;
@@ -1211,8 +1198,8 @@ std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P)
   std::vector<big_seg> segs;
   std::vector<u64> bb;
   int64_t pstart = 0, boff = 0;
-  char const* md       = std::getenv("CGX_LOUVAIN_BIG_MAXDEG");  // tests: a lower limit
-  int64_t const maxdeg = std::min<int64_t>(md ? std::atoll(md) : INT64_MAX, (int64_t)kBigMaxBuckets * kBktCap * 4 / 5);
+  int64_t const md     = tu.louvain_big_maxdeg;  // tests: a lower limit
+  int64_t const maxdeg = std::min<int64_t>(md > 0 ? md : INT64_MAX, (int64_t)kBigMaxBuckets * kBktCap * 4 / 5);
   for (size_t q = 0; q < big.size(); ++q) {
     int64_t const r = big[q], first = P.big_first[q], d = P.big_deg[q];
     int64_t const nseg  = (d + kBigSeg - 1) / kBigSeg;
@@ -1311,7 +1298,7 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, dou
 {
   hipStream_t s    = S.s;
   int64_t const nr = g.nrows, ne = g.ne;
-  if (ne == 0 || nr == 0 || !hash_sweep_enabled()) return;
+  if (ne == 0 || nr == 0 || !S.tune.louvain_hash) return;  // (louvain_hash = 0: sort path only, A/B)
   dbuf<u64> st(2, s);
   fill<u64>(st.data(), 2, 0ull, s);
   hipLaunchKernelGGL(k_level_stats, dim3(std::min<unsigned>(blocks(std::max(ne, nr)), 2048)), dim3(kBlock), 0, s,
@@ -1351,7 +1338,8 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, dou
     P.big_first = to_host(fd.data(), (size_t)tb, s);
     P.big_deg   = to_host(dd.data(), (size_t)tb, s);
   }
-  build_sort_coo(s, g, P, big_hash_enabled() ? plan_big_rows(s, P) : P.big);
+  // (louvain_big_hash = 0: heavy rows on the sort path, A/B)
+  build_sort_coo(s, g, P, S.tune.louvain_big_hash ? plan_big_rows(s, P, S.tune) : P.big);
   P.off  = off;
   P.hash = true;
 }
@@ -1375,7 +1363,7 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
   if (P.big_hash) {
     big_args ba{g.dst.data(), g.w.data(), c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
                 P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, present, k, S.m, S.gamma,
-                P.scale, P.inv_scale, P.best_q.data(), P.best_c.data(), P.overflow.data(), big_bucket_cap(), next,
+                P.scale, P.inv_scale, P.best_q.data(), P.best_c.data(), P.overflow.data(), big_bucket_cap(S.tune), next,
                 up_down, own};
     fill<u64>(P.own.data(), P.nbig, 0ull, s);
     fill<int>(P.overflow.data(), 1, 0, s);
@@ -1399,7 +1387,7 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
   if (P.nchunks) {
     hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), c, (uint32_t)g.base, self, a,
                        present, k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down, own};
-    static bool const wide = std::getenv("CGX_LOUVAIN_WIDE_KEYS") != nullptr;  // tests of the 64-bit keys
+    bool const wide = S.tune.louvain_wide_keys;  // tests of the 64-bit keys
     if (g.nv < (1 << 24) - 1 && !wide)
       hipLaunchKernelGGL(k_sweep_hash<uint32_t>, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
     else
@@ -1485,7 +1473,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
   if (nv0 == 0) return;
 
   adjacency_t& adj = ensure_adjacency(h, g, /*transposed=*/false);
-  louvain_state S(s);
+  louvain_state S(s, h.tune);
   S.gamma = resolution;
   level_graph cur;
   cur.nv    = nv0;
@@ -2345,7 +2333,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
   res.modularity             = 0;
   if (nv0 == 0) return;
 
-  louvain_state S(s);
+  louvain_state S(s, h.tune);
   S.gamma         = resolution;
   S.comm          = &comm;
   level_graph cur = mg_level0<V, R>(h, g);

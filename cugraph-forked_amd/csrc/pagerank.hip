@@ -467,39 +467,22 @@ constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 // destinations, 128 KB of LDS, one 1024-thread block per CU) from 2^23 destinations
 // up (RMAT-24, 542 windows: 0.709 ms/iteration against 0.786 with 13, same box),
 // 13 (8K, 64 KB, two blocks per CU) from 2^22, 12 below (RMAT-22, 586 windows:
-// 0.181 ms against 0.199 with 13 and 0.219 with 14).  CGX_PR_WIN_BITS overrides
-// (12, 13 or 14).
-inline int push_win_bits(int64_t n_rows)
+// 0.181 ms against 0.199 with 13 and 0.219 with 14).  tuning_t::pr_win_bits
+// overrides (12, 13 or 14).
+inline int push_win_bits(int64_t n_rows, tuning_t const& tu)
 {
-  if (char const* e = std::getenv("CGX_PR_WIN_BITS")) {
-    int b = std::atoi(e);
-    if (b == 12 || b == 13 || b == 14) return b;
-  }
+  if (tu.pr_win_bits == 12 || tu.pr_win_bits == 13 || tu.pr_win_bits == 14) return tu.pr_win_bits;
   return n_rows >= (int64_t(1) << 23) ? 14 : n_rows >= (int64_t(1) << 22) ? 13 : 12;
 }
 
 // persistent push blocks: two per CU, one per CU for 16K-destination windows
 inline int push_blocks(int win_bits) { return win_bits >= 14 ? kPushBlocks / 2 : kPushBlocks; }
 
-// 16-bit packed entries for unweighted graphs (push_body16); CGX_PR_PACKED=0 keeps
-// the 32-bit format (measurement / A-B only)
-inline bool env_is(char const* name, char const* value)
-{
-  char const* e = std::getenv(name);
-  return e && std::string(e) == value;
-}
-
 // items per push block on average: a window larger than 1.5 x E / (blocks x this) is
 // cut into shares.  RMAT-24 ms/iteration with 2 / 4 / 8 / 16: 0.593 / 0.589-0.599 /
 // 0.620-0.630 / 0.687 (RMAT-26 4: 2.98, 8: 3.06, 16: 3.23; same box): more shares
 // mean more added (not stored) windows, and the balance gained does not pay for them
 constexpr int64_t kShareDiv = 4;
-
-inline bool packed_enabled()
-{
-  char const* e = std::getenv("CGX_PR_PACKED");
-  return !(e && std::string(e) == "0");
-}
 
 struct push_unit {
   int64_t k0, k1;  // entries [k0, k1)
@@ -1381,10 +1364,10 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
 // Whole items (all of a window's units): kWholeItem on the item's first unit (the
 // push stores that window's sums), 0 in win_multi (k_pr_apply leaves them)
 inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std::vector<push_unit>& hu,
-                             std::vector<int64_t> const& item_u, int64_t nitems)
+                             std::vector<int64_t> const& item_u, int64_t nitems, tuning_t const& tu)
 {
   int64_t const nunits = (int64_t)hu.size();
-  bool const no_whole  = env_is("CGX_PR_WHOLE", "0");  // A/B: every flush adds, the apply clears every sum
+  bool const no_whole  = !tu.pr_whole;  // A/B: every flush adds, the apply clears every sum
   std::vector<uint8_t> multi((size_t)std::max<int64_t>(pp.nwin, 1), 0);
   for (int64_t i = 0; i < nitems; ++i) {
     int64_t const u = item_u[i], last = item_u[i + 1] - 1;
@@ -1441,7 +1424,8 @@ inline void upload_items(hipStream_t s, pr_push_t& pp, std::vector<int64_t> cons
 }
 
 // Items and queues over the units (host logic, once per graph)
-inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, bool xcd_queues)
+inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t nunits, bool xcd_queues,
+                        tuning_t const& tu)
 {
   int64_t const ne = nunits ? to_host(&units[nunits - 1].k1, 1, s)[0] : 0;
   // Items and queues.  From 2^22 rows (8K windows): an item is a window's units,
@@ -1501,7 +1485,7 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
     for (int q = 1; q < kQueues; ++q) pp.qoff[q] = nitems;
   }
   pp.qoff[kQueues] = (int64_t)queue.size();
-  mark_whole_items(s, pp, units, hu, item_u, nitems);
+  mark_whole_items(s, pp, units, hu, item_u, nitems, tu);
   upload_items(s, pp, item_u, queue, nitems);
 }
 
@@ -1516,16 +1500,16 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
 // dealt longest-first to the least-loaded queue, each queue taking its groups
 // costliest-first, so what is left for the last blocks is short.  Queue order does
 // not change any sum (fixed-point adds), only who takes an item when.
-// CGX_PR_CALIB=0 keeps the entry-dealt queues; CGX_PR_DEAL=global puts every item in
-// one queue, longest-first (A/B).
+// tuning_t::pr_calib = 0 keeps the entry-dealt queues; pr_deal_global puts every item
+// in one queue, longest-first (A/B).
 constexpr int kCalGroup = 16;
 
-inline bool calibration_wanted(pr_push_t const& pp)
+inline bool calibration_wanted(pr_push_t const& pp, tuning_t const& tu)
 {
-  return pp.calib == 0 && pp.nitems > 0 && !env_is("CGX_PR_CALIB", "0");
+  return pp.calib == 0 && pp.nitems > 0 && tu.pr_calib;
 }
 
-inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
+inline void calibrate_queues(hipStream_t s, pr_push_t& pp, tuning_t const& tu)
 {
   int64_t const n = pp.nitems;
   auto t          = to_host(pp.item_ticks.data<uint32_t>(), n, s);
@@ -1533,7 +1517,7 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
   queue.reserve(n);
   // below 2^22 rows the items are tiles of <= 8 units in one queue (build_items): that
   // queue, longest-first
-  if (env_is("CGX_PR_DEAL", "global") || pp.win_bits < 13) {
+  if (tu.pr_deal_global || pp.win_bits < 13) {
     for (int64_t i = 0; i < n; ++i) queue.push_back(i);
     std::stable_sort(queue.begin(), queue.end(), [&](int64_t a, int64_t b) { return t[a] > t[b]; });
     pp.qoff.assign(kQueues + 1, n);
@@ -1573,12 +1557,12 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp)
 // or one MG 2D block.
 template <typename C, typename R>
 void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
-                         int64_t n_cols, pr_push_t& pp)
+                         int64_t n_cols, pr_push_t& pp, tuning_t const& tu)
 {
   pp.built = true;
   pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
   if (!pp.ok) return;
-  int const wb       = push_win_bits(n_rows);
+  int const wb       = push_win_bits(n_rows, tu);
   int const sb       = 32 - wb;
   int64_t const nwin = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
   pp.win_bits        = wb;
@@ -1610,7 +1594,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      nwin, ws.data());
   CGX_LAUNCH_CHECK();
   pp.packed = false;
-  if (!w && packed_enabled()) {  // 16-bit entries unless the jumps would grow the entries by more than half
+  if (!w && tu.pr_packed) {  // 16-bit entries unless the jumps would grow the entries by more than half
     uint32_t const dmax = (1u << (16 - wb)) - 2;  // coded deltas 0 .. dmax; dmax + 1 marks a jump
     uint32_t const pmax = (1u << wb) - 1;         // jump payloads 1 .. pmax
     dbuf<uint32_t> mj(ne + 1, s);
@@ -1668,7 +1652,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       CGX_LAUNCH_CHECK();
       pp.ent.release();
       pp.ew.release();
-      build_items(s, pp, units, nunits, wb >= 13);
+      build_items(s, pp, units, nunits, wb >= 13, tu);
       pp.nunits = nunits;
       HIP_CHECK(hipStreamSynchronize(s));
       return;
@@ -1703,7 +1687,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                      vals_out.data(), rows, w, flag.data(), uid.data(), units, ne, wb, pp.ent.data<uint32_t>(),
                      w ? pp.ew.data<R>() : nullptr);
   CGX_LAUNCH_CHECK();
-  build_items(s, pp, units, nunits, wb >= 13);
+  build_items(s, pp, units, nunits, wb >= 13, tu);
   pp.nunits = nunits;
   HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -1732,7 +1716,7 @@ bool unit_weights(handle_t& h, graph_t& g, adjacency_t& adj)
       hipLaunchKernelGGL(k_count_non_unit<R>, dim3(grid_for((size_t)g.num_edges, kBlock, 4096)), dim3(kBlock), 0, s,
                          adj.weights.data<R>(), (size_t)g.num_edges, bad.data());
     CGX_LAUNCH_CHECK();
-    adj.unit_weights = (to_host_scalar(bad.data(), s) == 0 && !env_is("CGX_PR_UNIT_W", "0")) ? 1 : 0;  // A/B
+    adj.unit_weights = (to_host_scalar(bad.data(), s) == 0 && h.tune.pr_unit_w) ? 1 : 0;  // A/B
   }
   return adj.unit_weights == 1;
 }
@@ -1754,7 +1738,7 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_
                        nv, ne, rows.data());
   CGX_LAUNCH_CHECK();
   build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), use_weights ? adj.weights.data<R>() : nullptr, ne,
-                            nv, nv, adj.pr);
+                            nv, nv, adj.pr, h.tune);
 }
 
 template <typename V, typename R>
@@ -1823,11 +1807,11 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 }
 
 // fused apply (fused_finish): 16K windows, items, few windows without items (the last
-// block applies those alone); CGX_PR_FUSE=0 keeps the separate k_pr_apply (A/B)
-inline bool fuse_apply(pr_push_t const& pp)
+// block applies those alone); tuning_t::pr_fuse = 0 keeps the separate k_pr_apply (A/B)
+inline bool fuse_apply(pr_push_t const& pp, tuning_t const& tu)
 {
   return pp.win_bits >= 14 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
-         !env_is("CGX_PR_FUSE", "0");
+         tu.pr_fuse;
 }
 
 // the push kernel for the schedule's window bits and entry format
@@ -1968,8 +1952,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   bool const push_w = g.weighted && !(push && unit_weights<R>(h, g, adj));  // entry weights in the push
   if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj, push_w);
   push = push && adj.pr.ok;
-  // fp32 packed push: x~ as enc_fixed words (CGX_PR_ENC=0: plain floats, A/B)
-  a.enc  = push && adj.pr.packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
+  // fp32 packed push: x~ as enc_fixed words (tuning_t::pr_enc = 0: plain floats, A/B)
+  a.enc  = push && adj.pr.packed && std::is_same<R, float>::value && h.tune.pr_enc;
   a.fp64 = push ? 0 : 1;
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
@@ -1978,7 +1962,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
 
   push_args<V, E, R> sa{};
   int nblk_push = 0, nblk_apply = 0;
-  bool const fuse = push && fuse_apply(adj.pr);
+  bool const fuse = push && fuse_apply(adj.pr, h.tune);
   auto pkernel    = push_kernel<V, E, R>(adj.pr, push_w, a.enc != 0);
   if (push) {
     set_queue_args(sa, adj.pr, s);
@@ -1987,10 +1971,10 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     nblk_push  = sa.nitems ? push_blocks(sa.win_bits) : 0;
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
     sa.fuse    = fuse ? 1 : 0;
-    sa.nhub    = env_is("CGX_PR_HUB", "0") ? 0 : nv;  // hub x~ staged in LDS (16K windows; A/B switch)
+    sa.nhub    = h.tune.pr_hub ? nv : 0;  // hub x~ staged in LDS (16K windows; A/B switch)
   }
   // measured-cost queues: the first launch on this schedule records item durations
-  bool calibrating = push && calibration_wanted(adj.pr);
+  bool calibrating = push && calibration_wanted(adj.pr, h.tune);
   if (calibrating) {
     adj.pr.item_ticks.set_stream(s);
     adj.pr.item_ticks.resize(adj.pr.nitems * sizeof(uint32_t));
@@ -2047,7 +2031,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     HIP_CHECK(hipStreamSynchronize(s));
     hst = *hpin;
     if (calibrating) {  // re-deal the queues by the recorded costs (the stream is idle here)
-      calibrate_queues(s, adj.pr);
+      calibrate_queues(s, adj.pr, h.tune);
       for (int q = 0; q <= kQueues; ++q) sa.qoff[q] = adj.pr.qoff[q];
       calibrating = false;
     }
@@ -2216,11 +2200,10 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
                        cols.data());
   CGX_LAUNCH_CHECK();
   // row chunks: K = 4 from 64K rows per owner when the column has several ranks
-  // (CGX_MG_CHUNKS: any K, for the tests), else one chunk = the whole block
+  // (tuning_t::mg_chunks: any K, for the tests), else one chunk = the whole block
   int K = 1;
   if (R_ > 1) {
-    char const* ek = std::getenv("CGX_MG_CHUNKS");
-    K = ek ? std::max(1, std::atoi(ek)) : (blk->nmax_col >= 4 * 16384 ? 4 : 1);
+    K = h.tune.mg_chunks > 0 ? h.tune.mg_chunks : (blk->nmax_col >= 4 * 16384 ? 4 : 1);
     K = (int)std::min<int64_t>(K, std::max<int64_t>(blk->nmax_col, 1));
   }
   blk->K  = K;
@@ -2230,7 +2213,7 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
   R const* const w_in    = g.weighted ? mg.w.data<R>() : nullptr;
   (void)n_rows;
   if (K == 1) {  // (cs = nmax_col: the rows are already owner * cs + owner-local row)
-    build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), w_in, ne, n_rows_k, n_cols, blk->ch[0].pp);
+    build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), w_in, ne, n_rows_k, n_cols, blk->ch[0].pp, h.tune);
   } else {
     dbuf<uint32_t> chunk(ne, s), chunk_s(ne, s), iv(ne, s), perm(ne, s), rows_s(ne, s), cols_s(ne, s);
     dbuf<R> w_s(w_in ? ne : 1, s);
@@ -2250,7 +2233,7 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
     for (int k = 0; k < K; ++k)
       build_push_from_coo<uint32_t, R>(s, rows_s.data() + st[k], cols_s.data() + st[k],
                                        w_in ? w_s.data() + st[k] : nullptr, st[k + 1] - st[k], n_rows_k, n_cols,
-                                       blk->ch[k].pp);
+                                       blk->ch[k].pp, h.tune);
   }
   bool ok = true;
   for (auto const& c_ : blk->ch) ok = ok && c_.pp.ok;
@@ -2497,7 +2480,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   // GPU -- when every chunk with edges has the packed format (the words are shared)
   bool all_packed = true;
   for (auto const& c_ : blk.ch) all_packed = all_packed && (c_.pp.packed || c_.pp.nunits == 0);
-  a.enc = all_packed && std::is_same<R, float>::value && !env_is("CGX_PR_ENC", "0");
+  a.enc = all_packed && std::is_same<R, float>::value && h.tune.pr_enc;
   int const nblk_init = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 1024);
   hipLaunchKernelGGL((k_pr_init<V, E, R>), dim3(nblk_init), dim3(kBlock), 0, s, a);
   CGX_LAUNCH_CHECK();
@@ -2536,7 +2519,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       nblk_push[k] -= kCommCUs * (pp.win_bits >= 14 ? 1 : 2);  // (blocks per CU)
     pker[k]         = push_kernel<V, E, R>(pp, g.weighted, a.enc != 0);
     // measured-cost queues (calibrate_queues), per rank and chunk: no collective
-    calibrating[k] = nblk_push[k] && calibration_wanted(pp);
+    calibrating[k] = nblk_push[k] && calibration_wanted(pp, h.tune);
     if (calibrating[k]) {
       pp.item_ticks.set_stream(s);
       pp.item_ticks.resize(pp.nitems * sizeof(uint32_t));
@@ -2552,10 +2535,10 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
   sap.win_multi = col_reduce ? nullptr : blk.ch[0].pp.win_multi.data<uint8_t>();
   if (K > 1) sap.tile_ctr = nullptr;  // (every chunk's heads are reset on the comm stream)
   int const nblk_apply = (int)grid_for(std::max<int64_t>(n_own, 1), kBlock, 512);
-  bool const fused     = !col_reduce && K == 1 && nblk_push[0] && fuse_apply(blk.ch[0].pp);
+  bool const fused     = !col_reduce && K == 1 && nblk_push[0] && fuse_apply(blk.ch[0].pp, h.tune);
   if (fused) {
     spk[0].fuse = 1;
-    spk[0].nhub = env_is("CGX_PR_HUB", "0") ? 0 : C * blk.nmax_row;  // hub x~ in LDS (row-local source ids)
+    spk[0].nhub = h.tune.pr_hub ? C * blk.nmax_row : 0;  // hub x~ in LDS (row-local source ids)
   }
 
   size_t launched = 0;
@@ -2615,7 +2598,7 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
       hst = *hpin;
       for (int k = 0; k < K; ++k) {
         if (!calibrating[k]) continue;
-        calibrate_queues(s, blk.ch[k].pp);
+        calibrate_queues(s, blk.ch[k].pp, h.tune);
         for (int q = 0; q <= kQueues; ++q) spk[k].qoff[q] = blk.ch[k].pp.qoff[q];
         calibrating[k] = 0;
       }

@@ -57,6 +57,13 @@ class ResourceHandle:
     def set_profiling(self, enable=True):
         _lib.lib.cugraph_amd_set_profiling(self.c_resource_handle_ptr, 1 if enable else 0)
 
+    def set_option(self, name, value):
+        """Measurement / A-B switch of the kernels (cugraph_amd_set_option); ``None``
+        or "defaults" restores the production settings."""
+        if name is None:
+            name, value = "defaults", 0
+        _lib.call("cugraph_amd_set_option", self.c_resource_handle_ptr, name.encode(), float(value))
+
     def last_iterations(self):
         return _lib.lib.cugraph_amd_last_iterations(self.c_resource_handle_ptr)
 

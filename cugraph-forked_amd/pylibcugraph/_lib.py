@@ -134,6 +134,7 @@ _proto("cugraph_amd_graph_get_adjacency", c_int, P, P, c_int, PP, PP, PP, PP)
 _proto("cugraph_amd_graph_get_out_weight_sums", c_int, P, P, PP, PP)
 _proto("cugraph_amd_device_array_views_copy", c_int, P, c_size_t, P, P, PP)
 _proto("cugraph_amd_set_profiling", None, P, c_int)
+_proto("cugraph_amd_set_option", c_int, P, ctypes.c_char_p, c_double, PP)
 _proto("cugraph_amd_last_iterations", c_size_t, P)
 _proto("cugraph_amd_last_hot_kernel_ms", c_double, P)
 _proto("cugraph_amd_last_hot_kernel_launches", c_size_t, P)

@@ -107,6 +107,18 @@ cugraph_error_code_t cugraph_amd_device_array_views_copy(const cugraph_resource_
  */
 void cugraph_amd_set_profiling(cugraph_resource_handle_t* handle, bool_t enable);
 size_t cugraph_amd_last_iterations(const cugraph_resource_handle_t* handle);
+/*
+ * Measurement / A-B switches, per handle (the reference's tuning constants are
+ * constexpr; these select the alternatives DESIGN.md measured, for A/B scripts and
+ * the bitwise-equality tests).  Names: pr_win_bits (0 | 12 | 13 | 14), pr_packed,
+ * pr_whole, pr_calib, pr_deal_global, pr_unit_w, pr_fuse, pr_enc, pr_hub,
+ * mg_chunks, bfs_alpha, bfs_beta, bfs_probe_vec, bfs_head, bfs_res_grid,
+ * bfs_probe_grid, bfs_td_cap, louvain_hash, louvain_big_hash, louvain_big_cap,
+ * louvain_big_maxdeg, louvain_wide_keys; "defaults" resets them all.  Booleans
+ * are 0 / 1.  Unknown names: CUGRAPH_INVALID_INPUT.
+ */
+cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t* handle, const char* name, double value,
+                                            cugraph_error_t** error);
 double cugraph_amd_last_hot_kernel_ms(const cugraph_resource_handle_t* handle);
 size_t cugraph_amd_last_hot_kernel_launches(const cugraph_resource_handle_t* handle);
 /* BFS: edges examined, levels, top-down/bottom-up steps of the last call */

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PageRank A/B on the bench graphs (scripts/pr_ab.py: one resident graph per setting,
 # 16 iterations per call, HIP-event ms per iteration), each scale under its own limit.
-# usage: TAG=r04b SCALES="22 24" SETTINGS="base CGX_PR_MASKJ=1" bash scripts/gpu_ab.sh
+# usage: TAG=r04b SCALES="22 24" SETTINGS="base pr_hub=0" bash scripts/gpu_ab.sh
 set -o pipefail
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"

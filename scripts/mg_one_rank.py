@@ -6,8 +6,8 @@ One process, torch.distributed world of 1, the library's RCCL communicators
 (pylibcugraph.comms.init_rccl(1)): the MG path's every step -- x~ allgather, push,
 apply or fused apply, u64 allreduce, state kernel -- runs through RCCL with one rank.
 Prints ms per iteration (HIP events on the library stream, 16-iteration calls) for SG
-and MG and their ratio; then, per VARIANT (env assignments joined by ',', "-" = the
-defaults; switches read per call), the MG converged result against SG's: iterations,
+and MG and their ratio; then, per VARIANT (handle options NAME=VALUE joined by ',',
+"-" = the defaults), the MG converged result against SG's: iterations,
 bit equality, worst relative error and the degrees of the vertices that differ.
 """
 import os
@@ -71,10 +71,10 @@ def main():
     except RuntimeError as e:
         print(f"  SG BFS: {e}", flush=True)
     if os.environ.get("SG_PACKED0"):  # the 32-bit-entry push on a second SG graph
-        os.environ["CGX_PR_PACKED"] = "0"
+        h.set_option("pr_packed", 0)
         g2, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
         v2, x2 = p.pagerank(h, g2, None, None, None, None, 0.85, 1e-6, 500, False)
-        del os.environ["CGX_PR_PACKED"]
+        h.set_option("pr_packed", 1)
         r2 = sg_x[v2.cpu().numpy().astype(np.int64)]
         print(f"  SG 32-bit entries: iterations {h.last_iterations()}, bitwise equal "
               f"{bool(np.array_equal(x2.cpu().numpy().view(np.int32), r2.view(np.int32)))}", flush=True)
@@ -98,13 +98,12 @@ def main():
     print(f"RMAT-{scale}: SG {sg_ms:.4f} ms/iteration, 1-rank RCCL MG {mg_ms:.4f} ms/iteration "
           f"(ratio {mg_ms / sg_ms:.3f}); SG iterations {it_sg}", flush=True)
     for var in variants:
-        envs = [] if var == "-" else [kv.split("=", 1) for kv in var.split(",")]
-        for k, val in envs:
-            os.environ[k] = val
+        opts = [] if var == "-" else [kv.split("=", 1) for kv in var.split(",")]
+        for k, val in opts:
+            hm.set_option(k, float(val))
         vm, xm = p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False)
         it_mg = hm.last_iterations()
-        for k, _ in envs:
-            del os.environ[k]
+        hm.set_option(None, 0)
         ids = vm.cpu().numpy().astype(np.int64)
         mx = xm.cpu().numpy()
         ref = sg_x[ids]

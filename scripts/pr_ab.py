@@ -1,10 +1,10 @@
 """PageRank A/B on one resident graph (measurement aid, not product).
 
 usage: pr_ab.py SCALE [NAME=VAL,NAME=VAL ...] ...
-Builds the bench's R-MAT graph for every argument (a comma list of
-environment settings, or "base") runs 2 warm and 5 timed PageRank calls and prints
-ms per iteration from the library's HIP events (h.last_hot_kernel_ms / launches).
-Settings read at call time only (CGX_PR_ABLATE_XMASK, CGX_PR_ENC, ...).  Every call
+Builds the bench's R-MAT graph for every argument (a comma list of handle
+options, include/cugraph_amd/ext.h cugraph_amd_set_option, e.g. pr_enc=0,pr_hub=0,
+or "base") runs 2 warm and 5 timed PageRank calls and prints ms per iteration from
+the library's HIP events (h.last_hot_kernel_ms / launches).  Every call
 runs exactly 16 iterations (epsilon 0, max 16: the "failed to converge" error is
 expected and ignored), so ablations that change the ranks keep the same work.
 """
@@ -31,11 +31,12 @@ def main():
     scale = int(sys.argv[1])
     h = p.ResourceHandle()
     for arg in sys.argv[2:] or ["base"]:
-        env = {} if arg == "base" else dict(kv.split("=", 1) for kv in arg.split(","))
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
+        opts = {} if arg == "base" else {k: float(v) for k, v in (kv.split("=", 1) for kv in arg.split(","))}
+        h.set_option(None, 0)
+        for k, v in opts.items():
+            h.set_option(k, v)
         try:
-            # a fresh graph per setting: schedule-time settings (CGX_PR_SLICE, ...) apply
+            # a fresh graph per setting: schedule-time settings (pr_win_bits, ...) apply
             g, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
             E = g.number_of_edges()
             for _ in range(2):
@@ -54,11 +55,6 @@ def main():
         finally:
             g = None
             p.trim_device_cache()
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
 
 
 if __name__ == "__main__":

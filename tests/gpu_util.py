@@ -9,9 +9,13 @@ def plc():
 
 
 def make_graph(src, dst, w=None, transposed=False, renumber=True, symmetric=False, vdtype=np.int32,
-               wdtype=np.float32, handle=None):
+               wdtype=np.float32, handle=None, options=None):
+    """options: measurement / A-B switches set on the new handle (set_option,
+    include/cugraph_amd/ext.h) before the graph is built."""
     p = plc()
     h = handle or p.ResourceHandle()
+    for k, v in (options or {}).items():
+        h.set_option(k, v)
     props = p.GraphProperties(is_symmetric=symmetric, is_multigraph=False)
     s = np.asarray(src, dtype=vdtype)
     d = np.asarray(dst, dtype=vdtype)

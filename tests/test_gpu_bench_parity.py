@@ -297,6 +297,136 @@ def test_mg_one_rank_rccl_rmat24_equals_sg(rmat24):
         dist.destroy_process_group()
 
 
+class _OneRankRccl:
+    """A torch.distributed world of one (gloo, for the unique-id broadcast) and the
+    library's RCCL communicators over it: the MG code path with the one rank a box
+    allows."""
+
+    def __enter__(self):
+        import os
+        import torch.distributed as dist
+        bench, p = _bench()
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(bench.free_port())
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        self.ctx = p.comms.init_rccl(1)
+        return self
+
+    def __exit__(self, *exc):
+        import torch
+        import torch.distributed as dist
+        _, p = _bench()
+        torch.cuda.synchronize()
+        p.trim_device_cache()
+        self.ctx.free()
+        dist.destroy_process_group()
+        return False
+
+
+def _by_ext(vertices, values, n_ext, fill=-2):
+    """values scattered to external ids (int64 device tensor; `fill` where absent)."""
+    import torch
+    out = torch.full((n_ext,), fill, dtype=torch.int64, device=values.device)
+    out[vertices.to(torch.int64)] = values.to(torch.int64)
+    return out
+
+
+def test_mg_one_rank_rccl_rmat26_equals_sg():
+    """The multi-GPU path at the size of configs[3] and [4] (RMAT-26: V 32.8M, E 2.10G
+    stored edges, 8.4 GB of edge ids through the MG build's alltoallv) through the
+    library's RCCL communicators with one rank, against the single-GPU path on the same
+    graph (the reference compares MG with SG at its RMAT use-case sizes,
+    mg_pagerank_test.cpp:258-270, mg_louvain_test.cpp:40-46):
+    * PageRank bit for bit per external id, same iteration count;
+    * BFS from the largest hub: distances and predecessors equal;
+    * Louvain on the uniform [0, 1) fp32 weights of configs[4]: with one rank the MG
+      algorithm is the SG one, so the clustering, the modularity's bits
+      and the level count are identical."""
+    import torch
+    bench, p = _bench()
+    scale = 26
+    n_ext = 1 << scale
+    # -- single GPU: PageRank and BFS on the unweighted graph
+    h = p.ResourceHandle()
+    g, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
+    E = g.number_of_edges()
+    v, x = p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False)
+    it_sg = h.last_iterations()
+    sg_x = _by_ext(v, x.view(torch.int32), n_ext)
+    root = int(v[0])  # internal id 0: the largest degree
+    d, pr, vb = p.bfs(h, g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+    sg_d, sg_p = _by_ext(vb, d, n_ext).cpu(), _by_ext(vb, pr, n_ext).cpu()
+    sg_x = sg_x.cpu()
+    del v, x, d, pr, vb
+    g = None
+    torch.cuda.synchronize()
+    p.trim_device_cache()
+    # -- single GPU: Louvain on the weighted graph
+    g, _, _ = bench.build_rmat_graph(p, h, scale, weighted=True, transposed=False)
+    v, c, q_sg = p.louvain(h, g, 100, 1.0, False)
+    lv_sg = h.last_louvain_levels()
+    sg_c = _by_ext(v, c, n_ext).cpu()
+    del v, c
+    g = None
+    torch.cuda.synchronize()
+    p.trim_device_cache()
+    torch.cuda.empty_cache()
+    # -- one-rank RCCL multi-GPU path
+    with _OneRankRccl() as rc:
+        hm = p.ResourceHandle(rc.ctx.ptr)
+        gm, _, _ = bench.build_rmat_graph(p, hm, scale, transposed=True, mg=(0, 1))
+        assert gm.number_of_edges() == E
+        vm, xm = p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert hm.last_iterations() == it_sg
+        assert torch.equal(xm.view(torch.int32).cpu().to(torch.int64), sg_x[vm.cpu().to(torch.int64)]), \
+            "MG PageRank differs from SG at RMAT-26"
+        dm, pm, vmb = p.bfs(hm, gm, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+        ids = vmb.cpu().to(torch.int64)
+        assert torch.equal(dm.cpu().to(torch.int64), sg_d[ids]), "MG BFS distances differ from SG at RMAT-26"
+        assert torch.equal(pm.cpu().to(torch.int64), sg_p[ids]), "MG BFS predecessors differ from SG at RMAT-26"
+        del vm, xm, dm, pm, vmb
+        gm = None
+        torch.cuda.synchronize()
+        p.trim_device_cache()
+        gm, _, _ = bench.build_rmat_graph(p, hm, scale, weighted=True, transposed=False, mg=(0, 1))
+        vm, cm, q_mg = p.louvain(hm, gm, 100, 1.0, False)
+        assert hm.last_louvain_levels() == lv_sg
+        assert q_mg == q_sg, (q_mg, q_sg)
+        ids = vm.cpu().to(torch.int64)
+        assert torch.equal(cm.cpu().to(torch.int64), sg_c[ids]), "MG Louvain clustering differs from SG at RMAT-26"
+        print(f"RMAT-26 one-rank RCCL MG == SG: PageRank {it_sg} iterations, BFS from {root}, "
+              f"Louvain Q {q_sg:.9f} in {lv_sg} levels")
+        del vm, cm
+        gm = None
+        hm = None
+
+
+def test_mg_one_rank_rccl_louvain_rmat20_integer_equals_sg():
+    """Integer weights (every sum exact on either path): one-rank RCCL MG Louvain on
+    RMAT-20 gives SG's clustering, modularity bits and level count."""
+    import torch
+    bench, p = _bench()
+    h = p.ResourceHandle()
+    n = 16 << 20
+    s, d = p.generators.generate_rmat_edgelist(h, 20, n, 0.57, 0.19, 0.19, 7, False, True)
+    w = torch.floor(p.generators.generate_edge_weights(h, n, 8) * 8.0) + 1.0
+    s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
+    props = p.GraphProperties(is_symmetric=True, is_multigraph=False)
+    g = p.SGGraph(h, props, s, d, w, store_transposed=False, renumber=True)
+    v, c, q_sg = p.louvain(h, g, 100, 1.0, False)
+    lv_sg = h.last_louvain_levels()
+    sg_c = _by_ext(v, c, 1 << 20)
+    g = None
+    with _OneRankRccl() as rc:
+        hm = p.ResourceHandle(rc.ctx.ptr)
+        gm = p.MGGraph(hm, props, s, d, w, store_transposed=False, num_edges=s.numel())
+        vm, cm, q_mg = p.louvain(hm, gm, 100, 1.0, False)
+        assert hm.last_louvain_levels() == lv_sg and q_mg == q_sg, (q_mg, q_sg)
+        assert torch.equal(cm.to(torch.int64), sg_c[vm.to(torch.int64)])
+        gm = None
+        hm = None
+
+
 def _louvain_q_recomputed(scale):
     """Louvain on a bench graph (symmetric R-MAT, fp32 [0,1) weights, bench.py
     louvain_leg): the reported Q is the modularity of the returned partition,
@@ -369,7 +499,7 @@ def test_louvain_bench_graph_modularity(scale):
     assert q > 0.05
 
 
-def test_louvain_hash_equals_sort_rmat20(monkeypatch):
+def test_louvain_hash_equals_sort_rmat20():
     """RMAT-20 with integer weights: the LDS-hash local move (multi-segment heavy
     rows, many buckets per row) and the sort local move give the same clustering."""
     import torch
@@ -381,8 +511,8 @@ def test_louvain_hash_equals_sort_rmat20(monkeypatch):
     s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
     props = p.GraphProperties(is_symmetric=True, is_multigraph=False)
     out = []
-    for mode in ("1", "0"):
-        monkeypatch.setenv("CGX_LOUVAIN_HASH", mode)
+    for mode in (1, 0):
+        h.set_option("louvain_hash", mode)
         g = p.SGGraph(h, props, s, d, w, store_transposed=False, renumber=True)
         v, c, q = p.louvain(h, g, 100, 1.0, False)
         out.append((v.cpu().numpy(), c.cpu().numpy(), q, h.last_louvain_levels()))

@@ -169,23 +169,23 @@ def test_extract_paths_rmat_renumbered():
 
 
 @pytest.mark.parametrize("scale", [14, 18])
-def test_probe_vector_loads_same_result(scale, monkeypatch):
+def test_probe_vector_loads_same_result(scale):
     """Every bottom-up probe form gives the same distances and predecessors: the
     default (bfs.hip k_bu_probe<HEAD, STAGE2>: the 16-byte head table's first 3
     neighbours, then neighbours 3..10 by 16-byte loads of the padded adjacency), the
-    head table alone (CGX_BFS_PROBE_VEC=0, which also turns off the vector loads), and
-    the adjacency probe without the head table (CGX_BFS_HEAD=0: 8 neighbours by
+    head table alone (option bfs_probe_vec = 0, which also turns off the vector loads), and
+    the adjacency probe without the head table (bfs_head = 0: 8 neighbours by
     16-byte loads)."""
     s, d = rmat_sym(scale)
     h, G = make_graph(s, d, None, renumber=True, symmetric=True)
     deg = np.bincount(s)
     srcs = [int(np.argmax(deg)), int(s[len(s) // 3]), int(d[-1])]
-    monkeypatch.setenv("CGX_BFS_PROBE_VEC", "0")
+    h.set_option("bfs_probe_vec", 0)
     base = [run(h, G, [x], True) for x in srcs]
-    monkeypatch.delenv("CGX_BFS_PROBE_VEC")
-    monkeypatch.setenv("CGX_BFS_HEAD", "0")
+    h.set_option("bfs_probe_vec", 1)
+    h.set_option("bfs_head", 0)
     nohead = [run(h, G, [x], True) for x in srcs]
-    monkeypatch.delenv("CGX_BFS_HEAD")
+    h.set_option("bfs_head", 1)
     for (v0, d0, p0), (v1, d1, p1) in zip(base, nohead):
         assert np.array_equal(v1, v0) and np.array_equal(d1, d0) and np.array_equal(p1, p0)
     for x, (v0, d0, p0) in zip(srcs, base):

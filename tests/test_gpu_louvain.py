@@ -146,13 +146,13 @@ def test_dendrogram_levels_compose_to_clusters():
     assert np.array_equal(flat, host(c))
 
 
-@pytest.mark.parametrize("renumber,env", [(True, {}), (False, {}), (True, {"CGX_LOUVAIN_BIG": "sort"}),
-                                          (False, {"CGX_LOUVAIN_BIG_CAP": "16"}),
-                                          (False, {"CGX_LOUVAIN_BIG_MAXDEG": "3000"})])
-def test_hash_sweep_equals_sort_sweep(renumber, env, monkeypatch):
+@pytest.mark.parametrize("renumber,opts", [(True, {}), (False, {}), (True, {"louvain_big_hash": 0}),
+                                           (False, {"louvain_big_cap": 16}),
+                                           (False, {"louvain_big_maxdeg": 3000})])
+def test_hash_sweep_equals_sort_sweep(renumber, opts):
     """The LDS-hash local move (louvain.hip: k_sweep_hash for rows of <= 2048 edges,
     k_big_partials / k_big_buckets / k_big_move for heavier rows; fixed-point pair
-    sums) against the sort + reduce_by_key local move (CGX_LOUVAIN_HASH=0) on
+    sums) against the sort + reduce_by_key local move (option louvain_hash = 0) on
     RMAT-16 with integer weights: every sum is exact in both, so the clustering,
     modularity and level count are identical.  Variants: heavy rows on the sort
     path inside the hash schedule (not a prefix of the rows without renumbering:
@@ -165,45 +165,26 @@ def test_hash_sweep_equals_sort_sweep(renumber, env, monkeypatch):
     s, d, w = og.symmetrize_dedup(s, d, w)
     deg = np.bincount(s)
     assert deg.max() > 2048 and deg[0] <= 2048  # hub rows exist, and row 0 is not one
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    h, G = make_graph(s, d, w, renumber=renumber, symmetric=True)
+    h, G = make_graph(s, d, w, renumber=renumber, symmetric=True, options=opts)
     v, c, q = run(h, G)
     lv = h.last_louvain_levels()
-    for k in env:
-        monkeypatch.delenv(k)
-    monkeypatch.setenv("CGX_LOUVAIN_HASH", "0")
-    h2, G2 = make_graph(s, d, w, renumber=renumber, symmetric=True)
+    h2, G2 = make_graph(s, d, w, renumber=renumber, symmetric=True, options={"louvain_hash": 0})
     v2, c2, q2 = run(h2, G2)
     assert np.array_equal(v, v2) and np.array_equal(c, c2)
     assert q == q2 and lv == h2.last_louvain_levels()
 
 
 def test_hash_sweep_wide_keys():
-    """k_sweep_hash<u64> (levels with >= 2^24 - 1 ids) forced on RMAT-14, in a child
-    process since the switch is read once: same clustering as the sort path."""
-    import os
-    import subprocess
-    import sys
-    code = (
-        "import sys, numpy as np; sys.path[:0] = ['tests', '.', 'cugraph-forked_amd']\n"
-        "from gpu_util import make_graph, plc, host\n"
-        "from oracle import rmat, graph as og\n"
-        "s, d = rmat.rmat(14, 16 << 14, seed=5)\n"
-        "w = np.floor(rmat.rmat_weights(s.size, seed=6).astype(np.float64) * 8.0) + 1.0\n"
-        "s, d, w = og.symmetrize_dedup(s, d, w)\n"
-        "h, G = make_graph(s, d, w, renumber=True, symmetric=True)\n"
-        "v, c, q = plc().louvain(h, G, 100, 1.0, False)\n"
-        "np.save(sys.argv[1], host(c)); print(repr(q))\n")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    """k_sweep_hash<u64> (levels with >= 2^24 - 1 ids) forced on RMAT-14 (option
+    louvain_wide_keys): same clustering as the sort path."""
+    s, d = rmat.rmat(14, 16 << 14, seed=5)
+    w = np.floor(rmat.rmat_weights(s.size, seed=6).astype(np.float64) * 8.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
     out = {}
-    for mode, env in (("wide", {"CGX_LOUVAIN_WIDE_KEYS": "1"}), ("sort", {"CGX_LOUVAIN_HASH": "0"})):
-        f = f"/tmp/cgx_lv_{mode}_{os.getpid()}.npy"
-        r = subprocess.run([sys.executable, "-c", code, f], cwd=root, env={**os.environ, **env}, capture_output=True,
-                           text=True, timeout=240)
-        assert r.returncode == 0, r.stderr[-2000:]
-        out[mode] = (np.load(f), float(r.stdout.strip().splitlines()[-1]))
-        os.remove(f)
+    for mode, opts in (("wide", {"louvain_wide_keys": 1}), ("sort", {"louvain_hash": 0})):
+        h, G = make_graph(s, d, w, renumber=True, symmetric=True, options=opts)
+        v, c, q = plc().louvain(h, G, 100, 1.0, False)
+        out[mode] = (host(c), q)
     assert np.array_equal(out["wide"][0], out["sort"][0]) and out["wide"][1] == out["sort"][1]
 
 

@@ -531,8 +531,6 @@ def _mg_sg_worker(rank, world, port, C, scale, chunks=None):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    if chunks:
-        os.environ["CGX_MG_CHUNKS"] = str(chunks)
     _rank_setup(port, rank)
     import torch
     import torch.distributed as dist
@@ -545,6 +543,8 @@ def _mg_sg_worker(rank, world, port, C, scale, chunks=None):
     lo, hi = _slice(rank, world, E)
     ctx = plc.comms.init_torch(C)
     h = plc.ResourceHandle(ctx.ptr)
+    if chunks:
+        h.set_option("mg_chunks", chunks)
     props = plc.GraphProperties(is_symmetric=True, is_multigraph=False)
     dev = lambda a: torch.as_tensor(np.ascontiguousarray(a).astype(np.int32), device="cuda")  # noqa: E731
     Gp = plc.MGGraph(h, props, dev(s[lo:hi]), dev(d[lo:hi]), None, store_transposed=True, num_edges=E)
@@ -608,7 +608,7 @@ def test_mg_equals_sg(world, C, scale, chunks):
     """The reference's 8-GPU grid (4 x 2) at RMAT-18 and the flat 1 x 8 grid, rehearsed
     with 8 ranks on the one test GPU (torch.distributed/gloo callbacks).  chunks: the
     PageRank block's rows in that many chunks, pushed one after another with each
-    chunk's column reduce-scatter on the comm stream (CGX_MG_CHUNKS; the default cuts
+    chunk's column reduce-scatter on the comm stream (option mg_chunks; the default cuts
     4 chunks only from 64K rows per owner) -- still bitwise SG."""
     _spawn(_mg_sg_worker, (world, _free_port(), C, scale, chunks), world, deadline=300.0)
 

@@ -228,16 +228,15 @@ def test_sparse_wide_push(nv, ne):
 
 
 @pytest.mark.parametrize("scale,renumber", [(12, True), (20, True), (20, False)])
-def test_packed_entries_bitwise_equal_plain(scale, renumber, monkeypatch):
+def test_packed_entries_bitwise_equal_plain(scale, renumber):
     """The 16-bit packed push entries (pagerank.hip push_body16: source deltas, jump
     entries, per-wave-segment bases) must give the same fixed-point sums -- so the
-    same bits -- as the 32-bit entries (CGX_PR_PACKED=0)."""
+    same bits -- as the 32-bit entries (option pr_packed = 0)."""
     s, d, _ = rmat_graph(scale, False, True)
     h, G = make_graph(s, d, None, transposed=True, renumber=renumber, symmetric=True)
     r_packed = host(plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)[1])
     it = h.last_iterations()
-    monkeypatch.setenv("CGX_PR_PACKED", "0")
-    h2, G2 = make_graph(s, d, None, transposed=True, renumber=renumber, symmetric=True)
+    h2, G2 = make_graph(s, d, None, transposed=True, renumber=renumber, symmetric=True, options={"pr_packed": 0})
     r_plain = host(plc().pagerank(h2, G2, None, None, None, None, 0.85, 1e-6, 500, False)[1])
     assert h2.last_iterations() == it
     assert np.array_equal(r_packed, r_plain)
@@ -254,10 +253,10 @@ def _star_plus_ring(n_leaves):
 
 
 @pytest.mark.parametrize("graph", ["rmat20", "star"])
-def test_encoded_x_bitwise_equal_float(graph, monkeypatch):
+def test_encoded_x_bitwise_equal_float(graph):
     """The single-GPU fp32 packed push reads x~ as enc_fixed words (pagerank.hip:
     M << s, tiny values rounded to nearest-even once per vertex in the apply); it
-    must give the same bits as the float x~ converted per entry (CGX_PR_ENC=0),
+    must give the same bits as the float x~ converted per entry (pr_enc = 0),
     and stay within REL of the oracle."""
     if graph == "rmat20":
         s, d, _ = rmat_graph(20, False, True)
@@ -269,8 +268,7 @@ def test_encoded_x_bitwise_equal_float(graph, monkeypatch):
     v, pr = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
     r_enc = host(pr)
     it = h.last_iterations()
-    monkeypatch.setenv("CGX_PR_ENC", "0")
-    h2, G2 = make_graph(s, d, None, transposed=True, renumber=True, symmetric=sym)
+    h2, G2 = make_graph(s, d, None, transposed=True, renumber=True, symmetric=sym, options={"pr_enc": 0})
     r_flt = host(plc().pagerank(h2, G2, None, None, None, None, 0.85, 1e-6, 500, False)[1])
     assert h2.last_iterations() == it
     assert np.array_equal(r_enc, r_flt)
@@ -282,10 +280,10 @@ def test_encoded_x_bitwise_equal_float(graph, monkeypatch):
 
 
 @pytest.mark.parametrize("scale", [12, 20])
-def test_unit_weights_take_unweighted_push(scale, monkeypatch):
+def test_unit_weights_take_unweighted_push(scale):
     """All-ones fp32 weights (cugraph.Graph's unweighted graphs, simpleGraph.py:840-843)
     are detected and run the unweighted 16-bit push: the ranks are bitwise those of
-    the same graph without weights; the entry-weight push (CGX_PR_UNIT_W=0) agrees
+    the same graph without weights; the entry-weight push (pr_unit_w = 0) agrees
     within 1e-6 relative of the oracle."""
     s, d, _ = rmat_graph(scale, False, True)
     ones = np.ones(s.size, np.float32)
@@ -295,14 +293,12 @@ def test_unit_weights_take_unweighted_push(scale, monkeypatch):
     v1, r1 = plc().pagerank(hw, Gw, None, None, None, None, 0.85, 1e-6, 500, False)
     assert np.array_equal(host(v0), host(v1)) and np.array_equal(host(r0), host(r1))
     assert hw.last_iterations() == h.last_iterations()
-    monkeypatch.setenv("CGX_PR_UNIT_W", "0")
-    hq, Gq = make_graph(s, d, ones, transposed=True, symmetric=True)
+    hq, Gq = make_graph(s, d, ones, transposed=True, symmetric=True, options={"pr_unit_w": 0})
     v2, r2 = plc().pagerank(hq, Gq, None, None, None, None, 0.85, 1e-6, 500, False)
     assert np.array_equal(host(v0), host(v2))
     rel = np.abs(host(r2).astype(np.float64) - host(r0)) / host(r0)
     assert rel.max() < 2e-6
     # a weight that is not 1 keeps the entry-weight push
-    monkeypatch.delenv("CGX_PR_UNIT_W")
     if scale != 12:
         return
     w = ones.copy()
@@ -319,16 +315,15 @@ def test_unit_weights_take_unweighted_push(scale, monkeypatch):
 
 
 @pytest.mark.parametrize("scale", [12, 20])
-def test_window_bits_bitwise_equal(scale, monkeypatch):
-    """4K, 8K and 16K-destination windows (CGX_PR_WIN_BITS 12 / 13 / 14; 14 runs one
+def test_window_bits_bitwise_equal(scale):
+    """4K, 8K and 16K-destination windows (pr_win_bits 12 / 13 / 14; 14 runs one
     128 KB-LDS block per CU) sum the same fixed-point terms: the same bits."""
     s, d, _ = rmat_graph(scale, False, True)
     out = []
-    for wb in ("12", "13", "14"):
-        monkeypatch.setenv("CGX_PR_WIN_BITS", wb)
-        for packed in ("1", "0"):
-            monkeypatch.setenv("CGX_PR_PACKED", packed)
-            h, G = make_graph(s, d, None, transposed=True, symmetric=True)
+    for wb in (12, 13, 14):
+        for packed in (1, 0):
+            h, G = make_graph(s, d, None, transposed=True, symmetric=True,
+                              options={"pr_win_bits": wb, "pr_packed": packed})
             v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
             out.append((host(v), host(r), h.last_iterations()))
     for o in out[1:]:
@@ -351,13 +346,12 @@ def _empty_window_graph():
 
 
 @pytest.mark.parametrize("graph", ["rmat20", "empty_windows"])
-def test_fused_apply_bitwise_equal(graph, monkeypatch):
+def test_fused_apply_bitwise_equal(graph):
     """The push with the apply fused in (pagerank.hip fused_finish: the block that
     finishes a window applies it, from LDS for whole-window items; the last one
     applies the windows without items and updates the state) gives the same bits
-    and iteration count as the separate k_pr_apply (CGX_PR_FUSE=0), with and
-    without whole-window items (CGX_PR_WHOLE=0)."""
-    monkeypatch.setenv("CGX_PR_WIN_BITS", "14")
+    and iteration count as the separate k_pr_apply (pr_fuse = 0), with and
+    without whole-window items (pr_whole = 0)."""
     if graph == "rmat20":
         s, d, _ = rmat_graph(20, False, True)
         kw = dict(renumber=True, symmetric=True)
@@ -366,10 +360,9 @@ def test_fused_apply_bitwise_equal(graph, monkeypatch):
         s, d, n = _empty_window_graph()
         kw = dict(renumber=False, symmetric=False)
     out = []
-    for fuse, whole in (("1", "1"), ("0", "1"), ("1", "0")):
-        monkeypatch.setenv("CGX_PR_FUSE", fuse)
-        monkeypatch.setenv("CGX_PR_WHOLE", whole)
-        h, G = make_graph(s, d, None, transposed=True, **kw)
+    for fuse, whole in ((1, 1), (0, 1), (1, 0)):
+        h, G = make_graph(s, d, None, transposed=True, **kw,
+                          options={"pr_win_bits": 14, "pr_fuse": fuse, "pr_whole": whole})
         v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
         # a second call on the same schedule: queue heads and window counts were reset
         _, r2 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
@@ -386,22 +379,20 @@ def test_fused_apply_bitwise_equal(graph, monkeypatch):
 
 
 @pytest.mark.parametrize("graph", ["rmat12", "rmat20", "star"])
-def test_hub_lds_bitwise_equal(graph, monkeypatch):
+def test_hub_lds_bitwise_equal(graph):
     """The 16K-window push that reads the hubs' x~ from LDS (pagerank.hip push_body16
     HUB: segments whose sources are all below the staged count) gives the same bits
-    as gathering every x~ from global memory (CGX_PR_HUB=0), with encoded and plain
+    as gathering every x~ from global memory (pr_hub = 0), with encoded and plain
     float x~.  RMAT-12 has fewer vertices than the LDS holds (every segment reads
     LDS); the star graph has long runs of one hub source."""
-    monkeypatch.setenv("CGX_PR_WIN_BITS", "14")
     if graph == "star":
         s, d = _star_plus_ring(300_000)
     else:
         s, d, _ = rmat_graph(int(graph[4:]), False, True)
     out = []
-    for hub, enc in (("1", "1"), ("0", "1"), ("1", "0")):
-        monkeypatch.setenv("CGX_PR_HUB", hub)
-        monkeypatch.setenv("CGX_PR_ENC", enc)
-        h, G = make_graph(s, d, None, transposed=True, symmetric=graph != "star")
+    for hub, enc in ((1, 1), (0, 1), (1, 0)):
+        h, G = make_graph(s, d, None, transposed=True, symmetric=graph != "star",
+                          options={"pr_win_bits": 14, "pr_hub": hub, "pr_enc": enc})
         v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
         out.append((host(v), host(r), h.last_iterations()))
     for o in out[1:]:
@@ -410,21 +401,18 @@ def test_hub_lds_bitwise_equal(graph, monkeypatch):
 
 
 @pytest.mark.parametrize("deal", ["xcd", "global"])
-def test_calibrated_queues_bitwise_equal(deal, monkeypatch):
+def test_calibrated_queues_bitwise_equal(deal):
     """Measured-cost queues (pagerank.hip calibrate_queues): the first call on a
     schedule records every item's duration and re-deals the queues after its first
     chunk; that call, a later one on the re-dealt queues, and entry-dealt queues
-    (CGX_PR_CALIB=0) give the same bits and iteration counts, for 4K (one queue of
+    (pr_calib = 0) give the same bits and iteration counts, for 4K (one queue of
     tiles, re-sorted longest-first), 8K and 16K windows."""
     s, d, _ = rmat_graph(20, False, True)
-    if deal == "global":
-        monkeypatch.setenv("CGX_PR_DEAL", "global")
-    for wb in ("12", "13", "14"):
-        monkeypatch.setenv("CGX_PR_WIN_BITS", wb)
+    for wb in (12, 13, 14):
         out = []
-        for calib in ("1", "0"):
-            monkeypatch.setenv("CGX_PR_CALIB", calib)
-            h, G = make_graph(s, d, None, transposed=True, symmetric=True)
+        for calib in (1, 0):
+            h, G = make_graph(s, d, None, transposed=True, symmetric=True,
+                              options={"pr_win_bits": wb, "pr_calib": calib, "pr_deal_global": int(deal == "global")})
             for _ in range(2):  # calibrating call, then a call on the re-dealt queues
                 v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
                 out.append((host(v), host(r), h.last_iterations()))
