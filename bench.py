@@ -58,8 +58,11 @@ sys.path.insert(0, os.path.join(ROOT, "cugraph-forked_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-BFS_KERNELS = ("k_topdown", "k_bu_probe", "k_bu_residual", "k_bottomup", "k_mark_queues", "k_bitmap_to_queues",
-               "k_bfs_init_sources", "k_finish_pred", "k_sources_to_bitmap", "k_bfs_")
+# (k_bfs_head, the bottom-up probe's per-graph head table, is matched first and kept out
+# of the per-traversal sums: built once per graph, like the PageRank push schedule)
+BFS_KERNELS = ("k_bfs_head", "k_topdown", "k_bu_probe", "k_bu_residual", "k_bottomup", "k_mark_queues",
+               "k_bitmap_to_queues", "k_bfs_init_sources", "k_finish_pred", "k_sources_to_bitmap", "k_bfs_")
+BFS_PER_GRAPH = ("k_bfs_head",)
 PR_KERNELS = ("k_pr_push", "k_pr_apply")
 
 
@@ -284,15 +287,18 @@ def pagerank_traffic(args):
 
 
 def bfs_traffic(args, traversals):
-    """HBM bytes per BFS traversal (all BFS kernels of the child's traversals), and the
-    per-kernel split (KiB per traversal) of each counter."""
-    per, by_kernel = {}, {}
+    """HBM bytes per BFS traversal (the BFS kernels of the child's traversals, without
+    the per-graph head table), the per-kernel split (KiB per traversal) of each counter,
+    and the head table's bytes (per graph)."""
+    per, by_kernel, graph = {}, {}, {}
     child = ["--traffic-child", "bfs", "--bfs-scale", str(args.bfs_scale), "--bfs-roots", str(args.bfs_roots)]
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         vals = pmc_pass(ctr, child, BFS_KERNELS)
-        per[ctr] = sum(sum(v) for v in vals.values()) / traversals
-        by_kernel[ctr] = {k: round(sum(v) / traversals, 1) for k, v in vals.items() if v}
+        per[ctr] = sum(sum(v) for k, v in vals.items() if k not in BFS_PER_GRAPH) / traversals
+        by_kernel[ctr] = {k: round(sum(v) / traversals, 1) for k, v in vals.items() if v and k not in BFS_PER_GRAPH}
+        graph[ctr] = {k: round(sum(v), 1) for k, v in vals.items() if v and k in BFS_PER_GRAPH}
     per["per_kernel_kib"] = by_kernel
+    per["per_graph_kib"] = graph
     return (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0, per
 
 
@@ -379,6 +385,18 @@ def bfs_leg(p, args, child=False):
         deg_int = (off[1:] - off[:-1]).to(torch.int64)
     rates, stored, levels, bu, times, bytes_alg, spread = [], [], [], [], [], [], []
     number_map = None
+    first_ms = None
+    if not child:
+        # first traversal on the fresh graph: the per-graph work (the bottom-up probe's
+        # head table, the CSR's max degree) is inside it; module load was done by the
+        # build's kernels and is not (the BFS kernels load with the library)
+        src0 = torch.tensor([int(roots[0])] if args.rank == 0 else [], dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        barrier(args)
+        t0 = time.perf_counter()
+        p.bfs(h, g, src0, True, 0, True, False)
+        torch.cuda.synchronize()
+        first_ms = max_over_ranks(args, time.perf_counter() - t0) * 1e3
     for r in roots:
         mine = [int(r)] if args.rank == 0 else []
         src = torch.tensor(mine, dtype=torch.int32, device="cuda")
@@ -430,14 +448,22 @@ def bfs_leg(p, args, child=False):
            "timing": "median of reps_per_root timed traversals per root (after one warm traversal); MTEPS per root "
                      "from its median, harmonic mean over the roots",
            "levels": levels, "bottom_up_steps": bu,
+           "first_call_ms": round(first_ms, 3),
+           "first_call_note": "the first cugraph_bfs on the freshly built graph (from the first root; includes the "
+                              "per-graph head table k_bfs_head); ms_per_root_median[0] is the same root's steady "
+                              "traversal",
            "direction_optimizing": True, "n_gpus": args.world,
            "teps_counting": "Graph500: undirected edges of the source component / time (max over ranks)",
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "achieved_kind": "algorithmic-equivalent: the bytes a top-down pull over the source's "
+                                         "component would read (4 E_cc + 16 V_cc, SURVEY.md §8d) / time; a "
+                                         "direction-optimising traversal reads far fewer, so see frac_counter "
+                                         "(counter bytes / time) for the memory system's actual load",
                         "algorithmic_bytes_per_launch": sum(bytes_alg) / len(bytes_alg) / args.world,
+                        "ms_per_traversal": 1e3 * sum(times) / len(times),
                         "kernel": "one traversal (all levels, host wall time between synchronisations); "
-                                  "bytes = 4 E_cc + 16 V_cc (SURVEY.md §8d), per rank at N > 1; a direction-"
-                                  "optimising traversal may read fewer bytes than that"}}
+                                  "bytes = 4 E_cc + 16 V_cc (SURVEY.md §8d), per rank at N > 1"}}
     if args.rank == 0 and args.world == 1 and not args.no_cpu_baseline:
         try:
             import numpy as np
@@ -462,7 +488,7 @@ def bfs_leg(p, args, child=False):
 
 
 # ----------------------------------------------------------------------------- Louvain
-def louvain_leg(p, args):
+def louvain_leg(p, args, scale=None):
     """configs[4]: Louvain time-to-solution on a symmetrised R-MAT graph with uniform
     [0, 1) fp32 weights (seed 42, cugraph_funcs.py:56-58), max_level 100,
     resolution 1.0.  SG at N=1, the MG path (rows by source owner, RCCL) at N>1."""
@@ -471,7 +497,7 @@ def louvain_leg(p, args):
     small, _, _ = build_rmat_graph(p, h, 10, weighted=True, transposed=False, mg=args.mg)
     p.louvain(h, small, 100, 1.0, False)  # module load + allocator warm-up off the clock
     del small
-    scale = args.louvain_scale
+    scale = scale or args.louvain_scale
     t0 = time.perf_counter()
     g, _, _ = build_rmat_graph(p, h, scale, weighted=True, transposed=False, mg=args.mg)
     build_s = time.perf_counter() - t0
@@ -543,6 +569,8 @@ def main():
     ap.add_argument("--bfs-scale", type=int, default=24)
     ap.add_argument("--bfs-roots", type=int, default=8)
     ap.add_argument("--bfs-reps", type=int, default=5, help="timed traversals per root (median reported)")
+    ap.add_argument("--no-rmat26", dest="rmat26", action="store_false", default=True,
+                    help="skip the one-GPU RMAT-26 PageRank and Louvain legs (configs[3]/[4]'s graph)")
     ap.add_argument("--louvain", dest="louvain", action="store_true", default=True)
     ap.add_argument("--no-louvain", dest="louvain", action="store_false")
     ap.add_argument("--louvain-scale", type=int, default=None, help="default 23 + log2(N): RMAT-26 at 8 GPUs")
@@ -700,6 +728,13 @@ def main():
                                         "32-bit entries + fp32 entry weights (option pr_unit_w = 0)")
                     del r2
                     release_caches(p)
+                # configs[3]'s graph on one GPU: the single-GPU anchor of the 8-GPU run
+                if args.rmat26:
+                    r2 = pagerank_leg(p, args, 26, max(1, args.steps // 2), 1)
+                    out["pagerank_rmat26"] = pagerank_summary(r2, args, "sg")
+                    out["pagerank_rmat26"]["note"] = "configs[3]'s graph (RMAT-26) on one GPU"
+                    del r2
+                    release_caches(p)
             else:
                 alt = p.comms.flat_row_comm_size(world) if C != p.comms.flat_row_comm_size(world) \
                     else p.comms.default_row_comm_size(world)
@@ -727,9 +762,13 @@ def main():
                 try:
                     tb, detail = bfs_traffic(args, args.bfs_roots)
                     out["bfs"]["roofline"]["traffic"] = tb
+                    ms_t = out["bfs"]["roofline"]["ms_per_traversal"]
+                    out["bfs"]["roofline"]["achieved_counter"] = tb / (ms_t * 1e-3) / 1e9
+                    out["bfs"]["roofline"]["frac_counter"] = tb / (ms_t * 1e-3) / 1e9 / HBM_PEAK_GBS
                     out["bfs"]["roofline"]["traffic_note"] = (
-                        "HBM bytes per traversal (every BFS kernel) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from "
-                        f"separate rocprofv3 --pmc passes over one traversal per root: {detail}")
+                        "HBM bytes per traversal (every BFS kernel but the per-graph head table k_bfs_head, "
+                        "reported as per_graph_kib) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from separate rocprofv3 "
+                        f"--pmc passes over one traversal per root: {detail}")
                 except Exception as e:  # noqa: BLE001
                     out["bfs"]["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]
         except Exception as e:  # noqa: BLE001
@@ -742,6 +781,15 @@ def main():
                 f"Q={out['louvain']['modularity']:.6f} levels={out['louvain']['levels']}")
         except Exception as e:  # noqa: BLE001
             out["louvain"] = {"status": "failed", "error": repr(e)[:300]}
+    if args.louvain and args.rmat26 and world == 1:
+        try:  # configs[4]'s graph on one GPU (SG Louvain RMAT-26)
+            release_caches(p)
+            out["louvain_rmat26"] = louvain_leg(p, args, 26)
+            out["louvain_rmat26"]["note"] = "configs[4]'s graph (RMAT-26, uniform weights) on one GPU"
+            log(f"[bench] louvain: RMAT-26 {out['louvain_rmat26']['time_s']:.3f}s "
+                f"Q={out['louvain_rmat26']['modularity']:.6f} levels={out['louvain_rmat26']['levels']}")
+        except Exception as e:  # noqa: BLE001
+            out["louvain_rmat26"] = {"status": "failed", "error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             nxb = networkx_cpu_legs(args)

@@ -172,8 +172,12 @@ class rccl_comm final : public comm_t {
     size_t const es = comm_dtype_size(dt);
     // this rank's own share is a device copy, not a send to itself; a peer's share
     // goes in pieces of at most kPiece bytes (both sides cut it alike: the sender's
-    // count is the receiver's).  A 1-rank MG build of RMAT-24 (2.08 GB of edge ids
-    // sent to itself in one ncclSend) came back with a different graph.
+    // count is the receiver's).  Measured on MI355X (RCCL 2.27.7, ROCm 7.2,
+    // scripts/ubench/rccl_self.hip, gpurun_out/r05a-b): one ncclSend/ncclRecv pair of a
+    // rank to itself is byte-exact up to 2^30 bytes and wrong from 2^30 + 8 on -- the
+    // second half of the buffer, whatever the element type (uint8 / int32 / int64
+    // counts alike); the same sizes in 2^30-byte pieces inside one group are exact.
+    // So kPiece is that limit (peer sends could not be tested: one GPU per box).
     constexpr size_t kPiece = size_t(1) << 30;
     size_t const pe         = kPiece / es;
     if (sc[rank]) {

@@ -160,6 +160,11 @@ struct dbuf {  // typed view over a buffer
     b.resize(count * sizeof(T));
     n = count;
   }
+  void free()  // release the block now (stream-ordered), before the dbuf goes out of scope
+  {
+    b.release();
+    n = 0;
+  }
 };
 
 // ---------------------------------------------------------------- launch helpers

@@ -34,7 +34,6 @@
 #include "prims.hpp"
 
 #include <rocprim/device/device_reduce_by_key.hpp>
-#include <rocprim/device/device_segmented_reduce.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
@@ -214,14 +213,6 @@ struct plain_f {
 };
 
 // self-loop weight of edge e (its row is src[e] + base)
-struct self_w_f {
-  uint32_t const* s;
-  uint32_t const* d;
-  double const* w;
-  uint32_t base;
-  __device__ double operator()(int64_t e) const { return d[e] == s[e] + base ? w[e] : 0.0; }
-};
-
 __global__ void k_has_edges(int64_t const* off, int64_t n, uint8_t* has)
 {
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
@@ -809,24 +800,44 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
     move_whole_row(p, rw, key, val, nslot, (unsigned)bits, bq, bc, old_sh);
     return;
   }
-  uint32_t const cu = p.c[rw.row + p.base];
-  for (int i = tid; i < nslot; i += kBigThreads) {
-    uint32_t const cc = key[i];
-    if (cc == kEmpty32) continue;
-    if (cc == cu) atomicAdd(&p.own[sg.j], val[i]);
-    atomicAdd(&hist[bucket_of(cc, rw.logb)], 1u);
+  // The segment's distinct (cluster, partial) pairs, grouped by bucket: each thread
+  // keeps its slots in registers, the pairs are placed in bucket order in the LDS table
+  // itself (positions < distinct <= edges <= nslot / 2) and written out as one
+  // contiguous run -- coalesced, where a store per pair at its bucket's position wrote
+  // one partial line per 4- and 8-byte value
+  constexpr int kSPT = kBigSlots / kBigThreads;
+  uint32_t const cu  = p.c[rw.row + p.base];
+  uint32_t ck[kSPT], cpos[kSPT];
+  u64 cv[kSPT];
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q) {
+    int const i = tid + q * kBigThreads;
+    ck[q]       = i < nslot ? key[i] : kEmpty32;
+    cv[q]       = i < nslot ? val[i] : 0ull;
+    if (ck[q] != kEmpty32) {
+      if (ck[q] == cu) atomicAdd(&p.own[sg.j], cv[q]);
+      atomicAdd(&hist[bucket_of(ck[q], rw.logb)], 1u);
+    }
   }
   __syncthreads();
   uint32_t const total = block_excl_scan<kBigThreads, kBigMaxBuckets / kBigThreads>(hist, nbk, wsum);
   for (int b = tid; b < nbk; b += kBigThreads) p.boffs[sg.boff + b] = (int32_t)hist[b];
   if (tid == 0) p.boffs[sg.boff + nbk] = (int32_t)total;
   __syncthreads();
-  for (int i = tid; i < nslot; i += kBigThreads) {
-    uint32_t const cc = key[i];
-    if (cc == kEmpty32) continue;
-    uint32_t const pos     = atomicAdd(&hist[bucket_of(cc, rw.logb)], 1u);
-    p.pkey[sg.pbase + pos] = cc;
-    p.pval[sg.pbase + pos] = val[i];
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q)
+    if (ck[q] != kEmpty32) cpos[q] = atomicAdd(&hist[bucket_of(ck[q], rw.logb)], 1u);
+  __syncthreads();  // every slot is in registers before the table is overwritten
+#pragma unroll
+  for (int q = 0; q < kSPT; ++q)
+    if (ck[q] != kEmpty32) {
+      key[cpos[q]] = ck[q];
+      val[cpos[q]] = cv[q];
+    }
+  __syncthreads();
+  for (uint32_t i = tid; i < total; i += kBigThreads) {
+    p.pkey[sg.pbase + i] = key[i];
+    p.pval[sg.pbase + i] = val[i];
   }
 }
 
@@ -1019,6 +1030,79 @@ __global__ void k_big_info(int64_t const* rows, int64_t const* off, int64_t n, i
   }
 }
 
+// Heavy-row schedule on the device (plan_big_rows' host loop and its uploads were a
+// 2.2 ms gap per level at RMAT-23).  Per heavy row j (rows[j], ascending): segments of
+// kBigSeg edges, 2^logb buckets, partial slots = degree, bucket-offset slots.  Pass 0
+// counts (cnt[4][n + 1], a zero after each list so the exclusive scans end with the
+// totals) and flags rows the LDS passes cannot take (the host plan then runs as
+// before); pass 1 writes big_row / big_seg / the (row, bucket) blocks at the scanned
+// positions.  Segment order, buckets and offsets are plan_big_rows' exactly.
+__device__ __forceinline__ int ceil_log2_dev(int64_t x)
+{
+  int l = 0;
+  while ((int64_t(1) << l) < x) ++l;
+  return l;
+}
+
+__global__ void k_big_plan(int64_t const* rows, int64_t const* off, int64_t n, int64_t maxdeg, int pass,
+                           u64* cnt, u64 const* pos, big_row* brows, big_seg* bsegs, u64* bblocks, int* rest)
+{
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const r = rows[j], first = off[r], d = off[r + 1] - first;
+    int64_t const nseg = (d + kBigSeg - 1) / kBigSeg;
+    bool const single  = nseg == 1;
+    int const logb     = single ? 0 : min(ceil_log2_dev((d + kBigPerBucket - 1) / kBigPerBucket),
+                                          ceil_log2_dev(kBigMaxBuckets));
+    int64_t const nbk  = single ? 0 : (int64_t(1) << logb);
+    if (pass == 0) {
+      if (nseg > kBigMaxSegs || d > maxdeg) atomicOr(rest, 1);
+      cnt[0 * (n + 1) + j] = (u64)nseg;
+      cnt[1 * (n + 1) + j] = (u64)nbk;
+      cnt[2 * (n + 1) + j] = single ? 0ull : (u64)(nseg * (nbk + 1));
+      cnt[3 * (n + 1) + j] = (u64)d;
+      if (j == 0)
+        for (int q = 0; q < 4; ++q) cnt[q * (n + 1) + n] = 0ull;
+      continue;
+    }
+    int64_t const sb = (int64_t)pos[0 * (n + 1) + j], bb = (int64_t)pos[1 * (n + 1) + j];
+    int64_t const ob = (int64_t)pos[2 * (n + 1) + j], pb = (int64_t)pos[3 * (n + 1) + j];
+    big_row rw;
+    rw.first  = first;
+    rw.row    = (uint32_t)r;
+    rw.logb   = (uint32_t)logb;
+    rw.sbeg   = (uint32_t)sb;
+    rw.send   = (uint32_t)(sb + nseg);
+    rw.bbeg   = (uint32_t)bb;
+    rw.single = single ? 1u : 0u;
+    brows[j]  = rw;
+    for (int64_t q = 0; q < nseg; ++q) {
+      big_seg sg;
+      sg.e0    = first + q * kBigSeg;
+      sg.e1    = min(first + d, sg.e0 + kBigSeg);
+      sg.pbase = pb + q * kBigSeg;
+      sg.boff  = single ? ob : ob + q * (nbk + 1);
+      sg.j     = (uint32_t)j;
+      sg.pad   = 0;
+      bsegs[sb + q] = sg;
+    }
+    for (int64_t b = 0; b < nbk; ++b) bblocks[bb + b] = ((u64)j << 32) | (u64)b;
+  }
+}
+
+__global__ void k_plan_totals(u64 const* pos, int64_t n, int const* rest, u64* tot)
+{
+  if (threadIdx.x < 4) tot[threadIdx.x] = pos[threadIdx.x * (n + 1) + n];
+  if (threadIdx.x == 4) tot[4] = (u64)*rest;
+}
+
+// the two chunk-walk totals (chunks, heavy rows) in one read
+__global__ void k_walk_totals(int64_t const* cp, uint32_t const* cc, int64_t const* bp, uint32_t const* bc, int64_t n,
+                              int64_t* tot)
+{
+  if (threadIdx.x == 0) tot[0] = cp[n - 1] + (int64_t)cc[n - 1];
+  if (threadIdx.x == 1) tot[1] = bp[n - 1] + (int64_t)bc[n - 1];
+}
+
 inline unsigned blocks(int64_t n) { return grid_for(n > 0 ? n : 1, kBlock, 16384); }
 
 // ---------------------------------------------------------------- driver
@@ -1034,28 +1118,107 @@ struct louvain_state {
   louvain_state(hipStream_t st, tuning_t const& t) : s(st), scratch(1024, st), scal(2, st), tune(t) {}
 };
 
-// k[v] = weight of row v, self[v] = its self-loop weight, has_edges[v]: segmented
-// reductions over the row offsets (rocPRIM hands segments to blocks), so a hub row
-// no longer runs as one thread's serial loop (20 ms per level at RMAT-23)
+// k[v] = weight of row v, self[v] = its self-loop weight, has_edges[v], in one pass
+// over the level COO (the two rocPRIM segmented reductions this replaces read the 2 GB
+// of RMAT-23 level-0 weights twice at ~0.6 TB/s: 3.4 + 3.6 ms).  A wave takes 64
+// consecutive rows: a row of <= kVwLane edges is summed by its own lane in edge
+// order; a longer row by the whole wave, lane l summing edges l, l + 64, ... in
+// order and the 64 partials combined by a fixed xor tree (lane 0's value).  The
+// order depends only on the row's edges and degree, so every rank layout that
+// holds the row gives the same bits.  The same pass flags negative (or NaN)
+// weights and takes the largest row weight (level_stats: the fixed-point scale of
+// the hash sweeps), so plan_sweeps needs no pass of its own over the weights.
+constexpr int kVwLane = 16;
+
+__global__ __launch_bounds__(256) void k_vertex_weights(int64_t const* off, uint32_t const* dst, double const* w,
+                                                         int64_t nr, uint32_t base, double* k, double* self,
+                                                         uint8_t* has, u64* stats)
+{
+  int const lane    = threadIdx.x & 63;
+  int64_t const nw  = (int64_t)gridDim.x * (blockDim.x >> 6);
+  u64 neg = 0, kmax = 0;
+  for (int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t * 64 < nr; t += nw) {
+    int64_t const r = t * 64 + lane;
+    bool const ok   = r < nr;
+    int64_t const b = ok ? off[r] : 0, e = ok ? off[r + 1] : 0;
+    double kv = 0.0, sv = 0.0;
+    if (e - b <= kVwLane) {
+      for (int64_t i = b; i < e; ++i) {
+        double const x = w[i];
+        neg |= !(x >= 0.0);
+        kv += x;
+        sv += dst[i] == (uint32_t)r + base ? x : 0.0;
+      }
+    }
+    u64 longm = __ballot(ok && e - b > kVwLane);
+    while (longm) {
+      int const j       = __builtin_ctzll(longm);
+      longm &= longm - 1;
+      int64_t const rj  = t * 64 + j;
+      int64_t const bj  = __shfl(b, j, 64), ej = __shfl(e, j, 64);
+      double pk = 0.0, ps = 0.0;
+      for (int64_t i = bj + lane; i < ej; i += 64) {
+        double const x = w[i];
+        neg |= !(x >= 0.0);
+        pk += x;
+        ps += dst[i] == (uint32_t)rj + base ? x : 0.0;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        pk += __shfl_xor(pk, o, 64);
+        ps += __shfl_xor(ps, o, 64);
+      }
+      double const pk0 = __shfl(pk, 0, 64);  // lane 0's sums (the xor tree associates per lane)
+      double const ps0 = __shfl(ps, 0, 64);
+      if (lane == j) {
+        kv = pk0;
+        sv = ps0;
+      }
+    }
+    if (ok) {
+      k[r]    = kv;
+      self[r] = sv;
+      has[r]  = e > b ? 1 : 0;
+      u64 const bits = (u64)__double_as_longlong(kv);
+      kmax           = bits > kmax ? bits : kmax;
+    }
+  }
+  // block reduce of (neg, kmax), one atomic pair per block
+  __shared__ u64 sn[4], sk[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    neg |= __shfl_xor(neg, o, 64);
+    u64 const y = __shfl_xor(kmax, o, 64);
+    kmax        = y > kmax ? y : kmax;
+  }
+  if (lane == 0) {
+    sn[threadIdx.x >> 6] = neg;
+    sk[threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 n = 0, m = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      n |= sn[i];
+      m = sk[i] > m ? sk[i] : m;
+    }
+    if (n) atomicOr(&stats[0], 1ull);
+    atomicMax(&stats[1], m);
+  }
+}
+
+// stats (u64[2], device): [0] nonzero if a weight is negative or NaN, [1] the bits of
+// the largest row weight -- plan_sweeps' inputs
 void vertex_weights(louvain_state& S, level_graph const& g, int64_t const* off, double* k, double* self,
-                    uint8_t* has_edges)
+                    uint8_t* has_edges, u64* stats)
 {
   hipStream_t s    = S.s;
   int64_t const nr = g.nrows;
+  fill<u64>(stats, 2, 0ull, s);
   if (nr == 0) return;
-  auto selfw = rocprim::make_transform_iterator(rocprim::make_counting_iterator<int64_t>(0),
-                                                self_w_f{g.src.data(), g.dst.data(), g.w.data(), (uint32_t)g.base});
-  size_t t1 = 0, t2 = 0;
-  HIP_CHECK(rocprim::segmented_reduce(nullptr, t1, g.w.data(), k, (unsigned)nr, off, off + 1,
-                                      rocprim::plus<double>(), 0.0, s));
-  HIP_CHECK(rocprim::segmented_reduce(nullptr, t2, selfw, self, (unsigned)nr, off, off + 1, rocprim::plus<double>(),
-                                      0.0, s));
-  buffer tmp(std::max<size_t>(std::max(t1, t2), 1), s);
-  HIP_CHECK(rocprim::segmented_reduce(tmp.data(), t1, g.w.data(), k, (unsigned)nr, off, off + 1,
-                                      rocprim::plus<double>(), 0.0, s));
-  HIP_CHECK(rocprim::segmented_reduce(tmp.data(), t2, selfw, self, (unsigned)nr, off, off + 1,
-                                      rocprim::plus<double>(), 0.0, s));
-  hipLaunchKernelGGL(k_has_edges, dim3(blocks(nr)), dim3(kBlock), 0, s, off, nr, has_edges);
+  unsigned const grid = grid_for((size_t)((nr + 63) / 64), 4, 16384);
+  hipLaunchKernelGGL(k_vertex_weights, dim3(grid), dim3(256), 0, s, off, g.dst.data(), g.w.data(), nr,
+                     (uint32_t)g.base, k, self, has_edges, stats);
   CGX_LAUNCH_CHECK();
 }
 
@@ -1172,8 +1335,24 @@ struct sweep_plan {
   dbuf<u64> pval;
   dbuf<int32_t> boffs;
   dbuf<int> overflow;
-  std::vector<int64_t> big, big_first, big_deg;  // every heavy row (host)
+  std::vector<int64_t> big, big_first, big_deg;  // every heavy row (host; filled when a host plan needs them)
+  dbuf<int64_t> bigd;                            // the heavy rows, ascending (device)
+  int64_t tb = 0;
 };
+
+// the heavy rows' (row, first edge, degree) on the host, for the host plan and the
+// sort-path fallback
+inline void big_rows_to_host(hipStream_t s, sweep_plan& P)
+{
+  if (P.tb == 0 || !P.big.empty()) return;
+  dbuf<int64_t> fd(P.tb, s), dd(P.tb, s);
+  hipLaunchKernelGGL(k_big_info, dim3(grid_for(P.tb, kBlock, 16384)), dim3(kBlock), 0, s, P.bigd.data(), P.off, P.tb,
+                     fd.data(), dd.data());
+  CGX_LAUNCH_CHECK();
+  P.big       = to_host(P.bigd.data(), (size_t)P.tb, s);
+  P.big_first = to_host(fd.data(), (size_t)P.tb, s);
+  P.big_deg   = to_host(dd.data(), (size_t)P.tb, s);
+}
 
 // tuning_t::louvain_big_cap: lower the (row, bucket) table cap (tests of the fallback)
 inline int big_bucket_cap(tuning_t const& tu)
@@ -1257,6 +1436,50 @@ std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P, tuning_t const&
   return rest;
 }
 
+// plan_big_rows on the device (k_big_plan); false: some heavy row needs the sort path,
+// and nothing was planned (the caller runs the host plan)
+bool plan_big_rows_device(hipStream_t s, sweep_plan& P, tuning_t const& tu)
+{
+  int64_t const n = P.tb;
+  if (n == 0) return true;
+  int64_t const md     = tu.louvain_big_maxdeg;
+  int64_t const maxdeg = std::min<int64_t>(md > 0 ? md : INT64_MAX, (int64_t)kBigMaxBuckets * kBktCap * 4 / 5);
+  dbuf<u64> cnt(4 * (n + 1), s), pos(4 * (n + 1), s);
+  dbuf<int> rest(1, s);
+  fill<int>(rest.data(), 1, 0, s);
+  unsigned const g = grid_for(n, kBlock, 16384);
+  hipLaunchKernelGGL(k_big_plan, dim3(g), dim3(kBlock), 0, s, P.bigd.data(), P.off, n, maxdeg, 0, cnt.data(),
+                     (u64 const*)nullptr, (big_row*)nullptr, (big_seg*)nullptr, (u64*)nullptr, rest.data());
+  CGX_LAUNCH_CHECK();
+  for (int q = 0; q < 4; ++q)
+    exclusive_scan<u64, u64>(cnt.data() + q * (n + 1), pos.data() + q * (n + 1), (size_t)(n + 1), s);
+  // one read: the four totals and the rest flag
+  dbuf<u64> tot(5, s);
+  hipLaunchKernelGGL(k_plan_totals, dim3(1), dim3(64), 0, s, pos.data(), n, rest.data(), tot.data());
+  CGX_LAUNCH_CHECK();
+  auto const t = to_host(tot.data(), 5, s);
+  if (t[4]) return false;
+  P.nbig     = n;
+  P.nsegs    = (int64_t)t[0];
+  P.nbblocks = (int64_t)t[1];
+  P.brows.resize(n, s);
+  P.bsegs.resize(P.nsegs, s);
+  P.bblocks.resize(std::max<int64_t>(P.nbblocks, 1), s);
+  hipLaunchKernelGGL(k_big_plan, dim3(g), dim3(kBlock), 0, s, P.bigd.data(), P.off, n, maxdeg, 1, (u64*)nullptr,
+                     pos.data(), P.brows.data(), P.bsegs.data(), P.bblocks.data(), rest.data());
+  CGX_LAUNCH_CHECK();
+  P.own.resize(n, s);
+  P.best_q.resize(std::max<int64_t>(P.nbblocks, 1), s);
+  P.best_c.resize(std::max<int64_t>(P.nbblocks, 1), s);
+  P.pkey.resize(std::max<u64>(t[3], 1), s);
+  P.pval.resize(std::max<u64>(t[3], 1), s);
+  P.boffs.resize(std::max<u64>(t[2], 1), s);
+  P.overflow.resize(1, s);
+  HIP_CHECK(hipStreamSynchronize(s));  // cnt / pos / rest / tot go out of scope
+  P.big_hash = true;
+  return true;
+}
+
 // the edges of `rows` for the sort path: the level COO itself when they are a
 // prefix of the rows, else gathered
 void build_sort_coo(hipStream_t s, level_graph const& g, sweep_plan& P, std::vector<int64_t> const& rows)
@@ -1294,17 +1517,13 @@ void build_sort_coo(hipStream_t s, level_graph const& g, sweep_plan& P, std::vec
   P.bw   = P.gw.data();
 }
 
-void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, double const* k, sweep_plan& P)
+// stats: vertex_weights' (negative-weight flag, largest row weight) of this level
+void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, u64 const* stats, sweep_plan& P)
 {
   hipStream_t s    = S.s;
   int64_t const nr = g.nrows, ne = g.ne;
   if (ne == 0 || nr == 0 || !S.tune.louvain_hash) return;  // (louvain_hash = 0: sort path only, A/B)
-  dbuf<u64> st(2, s);
-  fill<u64>(st.data(), 2, 0ull, s);
-  hipLaunchKernelGGL(k_level_stats, dim3(std::min<unsigned>(blocks(std::max(ne, nr)), 2048)), dim3(kBlock), 0, s,
-                     g.w.data(), ne, k, nr, st.data());
-  CGX_LAUNCH_CHECK();
-  auto sh = to_host(st.data(), 2, s);
+  auto sh = to_host(stats, 2, s);
   if (sh[0]) return;  // negative weights: the fixed-point sums assume w >= 0
   double kmax;
   std::memcpy(&kmax, &sh[1], sizeof(double));
@@ -1322,25 +1541,26 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, dou
   CGX_LAUNCH_CHECK();
   exclusive_scan<uint32_t, int64_t>(cc.data(), cp.data(), (size_t)nblk, s);
   exclusive_scan<uint32_t, int64_t>(bc.data(), bp.data(), (size_t)nblk, s);
-  int64_t const tc = to_host_scalar(cp.data() + nblk - 1, s) + to_host_scalar(cc.data() + nblk - 1, s);
-  int64_t const tb = to_host_scalar(bp.data() + nblk - 1, s) + to_host_scalar(bc.data() + nblk - 1, s);
+  dbuf<int64_t> tot(2, s);
+  hipLaunchKernelGGL(k_walk_totals, dim3(1), dim3(64), 0, s, cp.data(), cc.data(), bp.data(), bc.data(), nblk,
+                     tot.data());
+  CGX_LAUNCH_CHECK();
+  auto const th    = to_host(tot.data(), 2, s);
+  int64_t const tc = th[0], tb = th[1];
   P.nchunks        = tc;
   P.chunks.resize(std::max<int64_t>(2 * tc, 1), s);
-  dbuf<int64_t> bigd(std::max<int64_t>(tb, 1), s);
+  P.bigd.resize(std::max<int64_t>(tb, 1), s);
+  P.tb = tb;
   hipLaunchKernelGGL(k_chunk_walk, dim3(wg), dim3(kBlock), 0, s, off, nr, 1, cc.data(), bc.data(), cp.data(), bp.data(),
-                     P.chunks.data(), bigd.data());
+                     P.chunks.data(), P.bigd.data());
   CGX_LAUNCH_CHECK();
-  if (tb) {
-    dbuf<int64_t> fd(tb, s), dd(tb, s);
-    hipLaunchKernelGGL(k_big_info, dim3(blocks(tb)), dim3(kBlock), 0, s, bigd.data(), off, tb, fd.data(), dd.data());
-    CGX_LAUNCH_CHECK();
-    P.big       = to_host(bigd.data(), (size_t)tb, s);
-    P.big_first = to_host(fd.data(), (size_t)tb, s);
-    P.big_deg   = to_host(dd.data(), (size_t)tb, s);
-  }
+  P.off = off;
   // (louvain_big_hash = 0: heavy rows on the sort path, A/B)
-  build_sort_coo(s, g, P, S.tune.louvain_big_hash ? plan_big_rows(s, P, S.tune) : P.big);
-  P.off  = off;
+  if (!S.tune.louvain_big_hash || !plan_big_rows_device(s, P, S.tune)) {
+    big_rows_to_host(s, P);
+    build_sort_coo(s, g, P, S.tune.louvain_big_hash ? plan_big_rows(s, P, S.tune) : P.big);
+  }
+  HIP_CHECK(hipStreamSynchronize(s));  // the walk's scratch goes out of scope
   P.hash = true;
 }
 
@@ -1377,6 +1597,7 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     } else {
       P.big_hash = false;  // a bucket outgrew its table: this level's heavy rows use the sort path
       HIP_CHECK(hipMemcpyAsync(next, c + g.base, g.nrows * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      big_rows_to_host(s, P);
       build_sort_coo(s, g, P, P.big);
       sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down, own);
       sorted_all = true;
@@ -1513,13 +1734,14 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     CGX_LAUNCH_CHECK();
     dbuf<double> k(nv, s), self(nv, s), a(nv, s);
     dbuf<uint8_t> has_edges(nv, s), present(nv, s);
-    vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
+    dbuf<u64> vstats(2, s);
+    vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data(), vstats.data());
     HIP_CHECK(hipMemcpyAsync(a.data(), k.data(), nv * sizeof(double), hipMemcpyDeviceToDevice, s));
     fill<uint8_t>(present.data(), nv, 1, s);
     dbuf<uint32_t> clusters(nv, s), next(nv, s);
     iota<uint32_t>(clusters.data(), nv, 0u, s);
     sweep_plan plan;
-    plan_sweeps(S, cur, off.data(), k.data(), plan);
+    plan_sweeps(S, cur, off.data(), vstats.data(), plan);
     dbuf<double> own(nv, s);
     // every sweep also returns the internal weight of the clustering it started from
     // (modularity_own): sweep k + 1 runs before the loop decides on clustering k
@@ -1543,7 +1765,14 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     }
     if (cur_q <= best_q) break;
     best_q = cur_q;
-    cur    = contract(S, cur, level);
+    // the level's sweep state goes before the contraction's sort buffers are allocated
+    plan = sweep_plan{};
+    for (auto* b : {&own, &k, &self, &a}) b->free();
+    for (auto* b : {&clusters, &next}) b->free();
+    has_edges.free();
+    present.free();
+    off.free();
+    cur = contract(S, cur, level);
     lap("contract", cur.nv, cur.ne, best_q);
   }
   // flatten_dendrogram (louvain_impl.cuh:239-255)
@@ -1680,27 +1909,37 @@ level_graph mg_level0(handle_t& h, graph_t& g)
   dbuf<int64_t> voff_d(P + 1, s);
   HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   int64_t const ne = mg.ne, n1 = std::max<int64_t>(ne, 1);
-  dbuf<int> dest(n1, s), d2(n1, s);
-  dbuf<int64_t> iv(n1, s), perm(n1, s), bnd(P + 1, s);
-  dbuf<V> ps(n1, s), pd(n1, s);
-  dbuf<R> pw(n1, s);
-  if (ne) {
-    hipLaunchKernelGGL(k_owner_of_src<V>, dim3(blocks(ne)), dim3(kBlock), 0, s, mg.src.data<V>(), ne, voff_d.data(),
-                       P, dest.data());
+  // Every temporary is released as soon as its last reader is enqueued (RMAT-26 on one
+  // rank: 2.1G edges, 8-16 B each per array)
+  dbuf<int64_t> bnd(P + 1, s), perm(n1, s);
+  {
+    dbuf<int> dest(n1, s), d2(n1, s);
+    dbuf<int64_t> iv(n1, s);
+    if (ne) {
+      hipLaunchKernelGGL(k_owner_of_src<V>, dim3(blocks(ne)), dim3(kBlock), 0, s, mg.src.data<V>(), ne,
+                         voff_d.data(), P, dest.data());
+      CGX_LAUNCH_CHECK();
+      iota<int64_t>(iv.data(), ne, 0, s);
+      if (!radix_sort_pairs_db<int, int64_t>(dest.data(), d2.data(), iv.data(), perm.data(), ne, 0, bits_for(P), s)) {
+        std::swap(dest, d2);  // sorted owners in d2, the permutation in perm
+        std::swap(iv, perm);
+      }
+    }
+    hipLaunchKernelGGL(k_rank_bounds, dim3(1), dim3(256), 0, s, d2.data(), ne, P, bnd.data());
     CGX_LAUNCH_CHECK();
-    iota<int64_t>(iv.data(), ne, 0, s);
-    radix_sort_pairs<int, int64_t>(dest.data(), d2.data(), iv.data(), perm.data(), ne, 0, bits_for(P), s);
-    gather<V, int64_t>(ps.data(), mg.src.data<V>(), perm.data(), ne, s);
-    gather<V, int64_t>(pd.data(), mg.dst.data<V>(), perm.data(), ne, s);
-    gather<R, int64_t>(pw.data(), mg.w.data<R>(), perm.data(), ne, s);
   }
-  hipLaunchKernelGGL(k_rank_bounds, dim3(1), dim3(256), 0, s, d2.data(), ne, P, bnd.data());
-  CGX_LAUNCH_CHECK();
   auto c64 = bounds_to_counts(bnd, P, s);
   std::vector<size_t> counts(c64.begin(), c64.end()), rc;
-  auto rs = exchange<V>(comm, ps.data(), counts, rc, s);
-  auto rd = exchange<V>(comm, pd.data(), counts, rc, s);
-  auto rw = exchange<R>(comm, pw.data(), counts, rc, s);
+  auto moved = [&](auto const* col, auto tag) {  // one column in owner order, exchanged
+    using T = decltype(tag);
+    dbuf<T> t(n1, s);
+    if (ne) gather<T, int64_t>(t.data(), col, perm.data(), ne, s);
+    return exchange<T>(comm, t.data(), counts, rc, s);
+  };
+  auto rs = moved(mg.src.data<V>(), V{});
+  auto rd = moved(mg.dst.data<V>(), V{});
+  auto rw = moved(mg.w.data<R>(), R{});
+  perm.free();
   level_graph out;
   out.nv    = g.num_vertices;
   out.base  = mg.voff[mg.p];
@@ -1716,11 +1955,15 @@ level_graph mg_level0(handle_t& h, graph_t& g)
     hipLaunchKernelGGL(k_mg_row_keys<V>, dim3(blocks(m)), dim3(kBlock), 0, s, rs.data(), rd.data(), m, out.base,
                        k1.data());
     CGX_LAUNCH_CHECK();
+    rs.free();
+    rd.free();
     convert<double, R>(w1.data(), rw.data(), m, s);
-    radix_sort_pairs<u64, double>(k1.data(), k2.data(), w1.data(), out.w.data(), (size_t)m, 0,
-                                  32 + bits_for(std::max<int64_t>(out.nrows - 1, 0)), s);
-    hipLaunchKernelGGL(k_split_pairs, dim3(blocks(m)), dim3(kBlock), 0, s, k2.data(), m, out.src.data(),
-                       out.dst.data(), /*cb=*/32);
+    rw.free();
+    bool const in1 = radix_sort_pairs_db<u64, double>(k1.data(), k2.data(), w1.data(), out.w.data(), (size_t)m, 0,
+                                                      32 + bits_for(std::max<int64_t>(out.nrows - 1, 0)), s);
+    if (!in1) std::swap(out.w, w1);
+    hipLaunchKernelGGL(k_split_pairs, dim3(blocks(m)), dim3(kBlock), 0, s, in1 ? k2.data() : k1.data(), m,
+                       out.src.data(), out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
   }
   return out;
@@ -2213,18 +2456,32 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
   int64_t const ne = g.ne, nr = L.nr, lo = L.lo, nv = L.nv;
   int64_t const n1 = std::max<int64_t>(ne, 1);
   int const lb = bits_for((unsigned long long)std::max<int64_t>(nv - 1, 1));
-  // 1. local coarse pairs, summed
-  dbuf<u64> keys(n1, s), keys2(n1, s);
-  dbuf<double> w2(n1, s), cw(n1, s);
+  // 1. local coarse pairs, summed (double-buffered sort, the reduction into the free
+  //    pair of buffers: 32 B per edge at the peak, RMAT-26 on one rank 67 GB)
+  dbuf<u64> keys, ka(n1, s);
+  dbuf<double> cw, wa(n1, s);
   int64_t nce = 0;
-  if (ne) {
-    hipLaunchKernelGGL(k_mg_pair_keys_loc, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(), lab_own,
-                       lab_gh, (uint32_t)nr, ne, keys.data());
-    CGX_LAUNCH_CHECK();
-    radix_sort_pairs<u64, double>(keys.data(), keys2.data(), g.w.data(), w2.data(), (size_t)ne, 0, 32 + lb, s);
-    nce = reduce_by_key(keys2.data(), w2.data(), (size_t)ne, keys.data(), cw.data(), rocprim::plus<double>(),
-                        rocprim::equal_to<u64>(), s);
+  {
+    dbuf<u64> kb(n1, s);
+    dbuf<double> wb(n1, s);
+    if (ne) {
+      hipLaunchKernelGGL(k_mg_pair_keys_loc, dim3(blocks(ne)), dim3(kBlock), 0, s, g.src.data(), g.dst.data(),
+                         lab_own, lab_gh, (uint32_t)nr, ne, ka.data());
+      CGX_LAUNCH_CHECK();
+      HIP_CHECK(hipMemcpyAsync(wa.data(), g.w.data(), ne * sizeof(double), hipMemcpyDeviceToDevice, s));
+      if (radix_sort_pairs_db<u64, double>(ka.data(), kb.data(), wa.data(), wb.data(), (size_t)ne, 0, 32 + lb, s)) {
+        std::swap(ka, kb);
+        std::swap(wa, wb);
+      }
+      // sorted pairs in ka / wa; sums into kb / wb
+      nce = reduce_by_key(ka.data(), wa.data(), (size_t)ne, kb.data(), wb.data(), rocprim::plus<double>(),
+                          rocprim::equal_to<u64>(), s);
+    }
+    keys = std::move(kb);
+    cw   = std::move(wb);
   }
+  ka.free();
+  wa.free();
   // 2. to the owner of label(u) (keys sorted, owner ranges ascending)
   dbuf<int64_t> bnd(P + 1, s);
   hipLaunchKernelGGL(k_key_bounds, dim3(1), dim3(256), 0, s, keys.data(), nce, L.voff_d.data(), P, bnd.data());
@@ -2232,16 +2489,26 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
   auto c64 = bounds_to_counts(bnd, P, s);
   std::vector<size_t> counts(c64.begin(), c64.end()), rc;
   auto rk = exchange<u64>(comm, keys.data(), counts, rc, s);
+  keys.free();
   auto rw = exchange<double>(comm, cw.data(), counts, rc, s);
+  cw.free();
   int64_t const nrcv = (int64_t)rk.n, r1 = std::max<int64_t>(nrcv, 1);
-  dbuf<u64> mk(r1, s), mk2(r1, s);
-  dbuf<double> mw(r1, s), mw2(r1, s);
+  dbuf<u64> mk, mk2(r1, s);
+  dbuf<double> mw, mw2(r1, s);
   int64_t nm = 0;
   if (nrcv) {
-    radix_sort_pairs<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0, 32 + lb, s);
-    nm = reduce_by_key(mk2.data(), mw2.data(), (size_t)nrcv, mk.data(), mw.data(), rocprim::plus<double>(),
+    if (radix_sort_pairs_db<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0, 32 + lb, s)) {
+      std::swap(rk, mk2);
+      std::swap(rw, mw2);
+    }
+    // sorted in rk / rw; merged sums into mk2 / mw2
+    nm = reduce_by_key(rk.data(), rw.data(), (size_t)nrcv, mk2.data(), mw2.data(), rocprim::plus<double>(),
                        rocprim::equal_to<u64>(), s);
   }
+  mk = std::move(mk2);
+  mw = std::move(mw2);
+  mk2 = std::move(rk);  // (scratch for the relabelled keys below)
+  rw.free();
   // 3. used labels: every rank sends its rows' distinct labels to their owners
   dbuf<uint32_t> ul;
   int64_t const nul = sort_unique_u32(lab_own, nr, ul, lb, s);
@@ -2299,8 +2566,11 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
     hipLaunchKernelGGL(k_relabel_pairs_mg, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, nl_own.data(),
                        (uint32_t)lo, wk.data(), wv.data(), nw, new_lo, mk2.data());
     CGX_LAUNCH_CHECK();
-    radix_sort_pairs<u64, double>(mk2.data(), mk.data(), mw.data(), out.w.data(), (size_t)nm, 0,
-                                  32 + bits_for(std::max<int64_t>(nu - 1, 0)), s);
+    if (!radix_sort_pairs_db<u64, double>(mk2.data(), mk.data(), mw.data(), out.w.data(), (size_t)nm, 0,
+                                          32 + bits_for(std::max<int64_t>(nu - 1, 0)), s)) {
+      std::swap(mk2, mk);  // sorted keys in mk, weights in out.w
+      std::swap(mw, out.w);
+    }
     hipLaunchKernelGGL(k_split_pairs, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, out.src.data(),
                        out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
@@ -2384,7 +2654,8 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     dbuf<uint8_t> has_edges(r1, s);
     // vertex weights on the global destinations (self loops: dst == row + base), then
     // the destinations become local ids
-    if (nr) vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data());
+    dbuf<u64> vstats(2, s);
+    vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data(), vstats.data());
     S.bytes = 0;
     mg_setup_level(S, cur, L, has_edges.data(), k.data());
     if (dendrogram.empty()) {  // the 1D partition's shape at level 0 (handle statistics)
@@ -2400,7 +2671,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     if (L.ng)
       HIP_CHECK(hipMemcpyAsync(level_gh.data(), L.c_gh.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     sweep_plan plan;
-    plan_sweeps(S, cur, off.data(), k.data(), plan);
+    plan_sweeps(S, cur, off.data(), vstats.data(), plan);
     phase("plan", dendrogram.size());
     dbuf<double> own(r1, s);
     dbuf<uint32_t> next(r1, s);
@@ -2447,7 +2718,14 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     }
     if (cur_q <= best_q) break;
     best_q = cur_q;
-    cur    = mg_contract(S, cur, L, level, level_gh.data(), voff);
+    // the level's sweep state goes before the contraction's sort buffers are allocated
+    plan = sweep_plan{};
+    W    = mg_sweep_view{};
+    for (auto* b : {&own, &k, &self}) b->free();
+    next.free();
+    has_edges.free();
+    off.free();
+    cur = mg_contract(S, cur, L, level, level_gh.data(), voff);
     phase("contract", dendrogram.size());
   }
   // flatten_dendrogram for the owned level-0 vertices: level i's owners answer

@@ -7,6 +7,15 @@
 //                                             from a hash (no index stream): every gather
 //                                             touches a line no other gather of the launch
 //                                             is likely to share when the table is large
+//   gatherk <table_MB> <n_millions> <grid> <aux>  the same through raw buffer loads with
+//                                             cache-policy bits aux (gfx940+: 1 sc0, 2 nt,
+//                                             16 sc1): which policy fills a 4-B miss with
+//                                             fewer fabric bytes (TCC_EA0_RDREQ_32B_sum)
+//   streamgather <table_MB> <stream_MB> <grid> <aux>  per lane: one 16-B load of a stream
+//                                             read once (cache policy aux) and 4 random
+//                                             4-B gathers from a small table (plain): does
+//                                             the stream's policy keep the table in L2?
+//                                             (the push's entry stream beside its x~ gathers)
 //
 // Prints one line per run: mode, bytes the kernel asks for, ms per launch (HIP events,
 // median of reps), GB/s or Ggathers/s.  Under `rocprofv3 --pmc FETCH_SIZE` (or
@@ -91,6 +100,45 @@ __global__ void k_gather(float const* __restrict__ table, unsigned nwords, long 
     for (int j = 0; j < 8; ++j) acc += v[j];
   }
   if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int AUX>
+__global__ void k_gather_aux(float const* __restrict__ table, unsigned nwords, long ngather, float* out)
+{
+  __amdgpu_buffer_rsrc_t const r =
+    __builtin_amdgcn_make_buffer_rsrc((void*)table, (short)0, (int)(nwords * 4u), 0x00020000);
+  long const stride = (long)gridDim.x * blockDim.x * 8;
+  float acc         = 0.f;
+  for (long b = (blockIdx.x * (long)blockDim.x + threadIdx.x) * 8; b < ngather; b += stride) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (mix((unsigned long long)(b + j)) % nwords) * 4u, 0, AUX));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int AUX>
+__global__ void k_stream_gather(u32x4 const* __restrict__ stream, long n16, float const* __restrict__ table,
+                                unsigned nwords, float* out)
+{
+  __amdgpu_buffer_rsrc_t const r = __builtin_amdgcn_make_buffer_rsrc((void*)stream, (short)0, 0x7fffffff, 0x00020000);
+  long const stride = (long)gridDim.x * blockDim.x;
+  unsigned acc      = 0;
+  float facc        = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16; i += stride) {
+    // offsets within the first 2 GB of the stream (n16 * 16 < 2^31)
+    u32x4 const v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(i * 16), 0, AUX));
+    float g[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = table[mix((unsigned long long)(i * 4 + j)) % nwords];
+    acc += v.x ^ v.w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) facc += g[j];
+  }
+  if (acc == 0x9e3779b9u || facc == 1234.5f) out[0] = facc;
 }
 
 template <typename F>
@@ -184,6 +232,58 @@ int main(int argc, char** argv)
                 mb, ng, grid, ms, ng / (ms * 1e-3) / 1e9, 128.0 * ng / (ms * 1e-3) / 1e9,
                 64.0 * ng / (ms * 1e-3) / 1e9, 32.0 * ng / (ms * 1e-3) / 1e9);
     CK(hipFree(t));
+    CK(hipFree(out));
+  } else if (mode == "gatherk") {
+    size_t const mb  = std::strtoull(argv[2], nullptr, 10);
+    long const ng    = (long)(std::atof(argv[3]) * 1e6);
+    int const grid   = std::atoi(argv[4]);
+    int const aux    = std::atoi(argv[5]);
+    unsigned const nw = (unsigned)((mb << 20) / 4);
+    float* t;
+    float* out;
+    CK(hipMalloc(&t, (size_t)nw * 4));
+    CK(hipMalloc(&out, 4));
+    CK(hipMemset(t, 0, (size_t)nw * 4));
+    auto launch = [&]() {
+      switch (aux) {
+#define CASE(A) case A: hipLaunchKernelGGL(k_gather_aux<A>, dim3(grid), dim3(256), 0, 0, t, nw, ng, out); break;
+        CASE(0) CASE(1) CASE(2) CASE(3) CASE(16) CASE(17) CASE(18) CASE(19)
+#undef CASE
+        default: std::fprintf(stderr, "aux must be 0,1,2,3,16,17,18,19\n"); std::exit(2);
+      }
+    };
+    float const ms = time_ms(launch, reps);
+    std::printf("gatherk aux=%d table_MB=%zu gathers=%ld grid=%d ms=%.4f Ggather/s=%.2f\n", aux, mb, ng, grid, ms,
+                ng / (ms * 1e-3) / 1e9);
+    CK(hipFree(t));
+    CK(hipFree(out));
+  } else if (mode == "streamgather") {
+    size_t const tmb = std::strtoull(argv[2], nullptr, 10);
+    size_t const smb = std::strtoull(argv[3], nullptr, 10);
+    int const grid   = std::atoi(argv[4]);
+    int const aux    = std::atoi(argv[5]);
+    unsigned const nw = (unsigned)((tmb << 20) / 4);
+    long const n16    = (long)(smb << 20) / 16;
+    float *t, *out;
+    u32x4* st;
+    CK(hipMalloc(&t, (size_t)nw * 4));
+    CK(hipMalloc(&st, (size_t)n16 * 16));
+    CK(hipMalloc(&out, 4));
+    CK(hipMemset(t, 0, (size_t)nw * 4));
+    CK(hipMemset(st, 1, (size_t)n16 * 16));
+    auto launch = [&]() {
+      switch (aux) {
+#define CASE(A) case A: hipLaunchKernelGGL(k_stream_gather<A>, dim3(grid), dim3(256), 0, 0, st, n16, t, nw, out); break;
+        CASE(0) CASE(1) CASE(2) CASE(3) CASE(16) CASE(17) CASE(18) CASE(19)
+#undef CASE
+        default: std::fprintf(stderr, "aux must be 0,1,2,3,16,17,18,19\n"); std::exit(2);
+      }
+    };
+    float const ms = time_ms(launch, reps);
+    std::printf("streamgather aux=%d table_MB=%zu stream_MB=%zu grid=%d ms=%.4f stream GB/s=%.1f Ggather/s=%.2f\n",
+                aux, tmb, smb, grid, ms, n16 * 16.0 / (ms * 1e-3) / 1e9, n16 * 4.0 / (ms * 1e-3) / 1e9);
+    CK(hipFree(t));
+    CK(hipFree(st));
     CK(hipFree(out));
   } else {
     std::fprintf(stderr, "unknown mode\n");

@@ -331,49 +331,69 @@ def _by_ext(vertices, values, n_ext, fill=-2):
     return out
 
 
+def _free_device():
+    """Return the library's and torch's cached device memory; (free, total) GB after."""
+    import torch
+    _, p = _bench()
+    torch.cuda.synchronize()
+    p.trim_device_cache()
+    torch.cuda.empty_cache()
+    f, t = torch.cuda.mem_get_info()
+    return round(f / 2**30, 1), round(t / 2**30, 1)
+
+
 def test_mg_one_rank_rccl_rmat26_equals_sg():
     """The multi-GPU path at the size of configs[3] and [4] (RMAT-26: V 32.8M, E 2.10G
     stored edges, 8.4 GB of edge ids through the MG build's alltoallv) through the
     library's RCCL communicators with one rank, against the single-GPU path on the same
     graph (the reference compares MG with SG at its RMAT use-case sizes,
     mg_pagerank_test.cpp:258-270, mg_louvain_test.cpp:40-46):
-    * PageRank bit for bit per external id, same iteration count;
-    * BFS from the largest hub: distances and predecessors equal;
     * Louvain on the uniform [0, 1) fp32 weights of configs[4]: with one rank the MG
       algorithm is the SG one, so the clustering, the modularity's bits
-      and the level count are identical."""
+      and the level count are identical;
+    * PageRank bit for bit per external id, same iteration count;
+    * BFS from the largest hub: distances and predecessors equal.
+    Results are kept on the host between the phases: RMAT-26 Louvain's level graphs
+    take > 100 GB of the device."""
     import torch
     bench, p = _bench()
     scale = 26
     n_ext = 1 << scale
-    # -- single GPU: PageRank and BFS on the unweighted graph
-    h = p.ResourceHandle()
-    g, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
-    E = g.number_of_edges()
-    v, x = p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False)
-    it_sg = h.last_iterations()
-    sg_x = _by_ext(v, x.view(torch.int32), n_ext)
-    root = int(v[0])  # internal id 0: the largest degree
-    d, pr, vb = p.bfs(h, g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
-    sg_d, sg_p = _by_ext(vb, d, n_ext).cpu(), _by_ext(vb, pr, n_ext).cpu()
-    sg_x = sg_x.cpu()
-    del v, x, d, pr, vb
-    g = None
-    torch.cuda.synchronize()
-    p.trim_device_cache()
+    print("device memory free/total GB at start", _free_device())
     # -- single GPU: Louvain on the weighted graph
+    h = p.ResourceHandle()
     g, _, _ = bench.build_rmat_graph(p, h, scale, weighted=True, transposed=False)
     v, c, q_sg = p.louvain(h, g, 100, 1.0, False)
     lv_sg = h.last_louvain_levels()
     sg_c = _by_ext(v, c, n_ext).cpu()
     del v, c
     g = None
-    torch.cuda.synchronize()
-    p.trim_device_cache()
-    torch.cuda.empty_cache()
+    _free_device()
+    # -- single GPU: PageRank and BFS on the unweighted graph
+    g, _, _ = bench.build_rmat_graph(p, h, scale, transposed=True)
+    E = g.number_of_edges()
+    v, x = p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False)
+    it_sg = h.last_iterations()
+    sg_x = _by_ext(v, x.view(torch.int32), n_ext).cpu()
+    root = int(v[0])  # internal id 0: the largest degree
+    d, pr, vb = p.bfs(h, g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+    sg_d, sg_p = _by_ext(vb, d, n_ext).cpu(), _by_ext(vb, pr, n_ext).cpu()
+    del v, x, d, pr, vb
+    g = None
+    h = None
+    print("device memory free/total GB after the SG phases", _free_device())
     # -- one-rank RCCL multi-GPU path
     with _OneRankRccl() as rc:
         hm = p.ResourceHandle(rc.ctx.ptr)
+        gm, _, _ = bench.build_rmat_graph(p, hm, scale, weighted=True, transposed=False, mg=(0, 1))
+        vm, cm, q_mg = p.louvain(hm, gm, 100, 1.0, False)
+        assert hm.last_louvain_levels() == lv_sg
+        assert q_mg == q_sg, (q_mg, q_sg)
+        ids = vm.cpu().to(torch.int64)
+        assert torch.equal(cm.cpu().to(torch.int64), sg_c[ids]), "MG Louvain clustering differs from SG at RMAT-26"
+        del vm, cm, ids
+        gm = None
+        _free_device()
         gm, _, _ = bench.build_rmat_graph(p, hm, scale, transposed=True, mg=(0, 1))
         assert gm.number_of_edges() == E
         vm, xm = p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False)
@@ -384,21 +404,12 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
         ids = vmb.cpu().to(torch.int64)
         assert torch.equal(dm.cpu().to(torch.int64), sg_d[ids]), "MG BFS distances differ from SG at RMAT-26"
         assert torch.equal(pm.cpu().to(torch.int64), sg_p[ids]), "MG BFS predecessors differ from SG at RMAT-26"
-        del vm, xm, dm, pm, vmb
-        gm = None
-        torch.cuda.synchronize()
-        p.trim_device_cache()
-        gm, _, _ = bench.build_rmat_graph(p, hm, scale, weighted=True, transposed=False, mg=(0, 1))
-        vm, cm, q_mg = p.louvain(hm, gm, 100, 1.0, False)
-        assert hm.last_louvain_levels() == lv_sg
-        assert q_mg == q_sg, (q_mg, q_sg)
-        ids = vm.cpu().to(torch.int64)
-        assert torch.equal(cm.cpu().to(torch.int64), sg_c[ids]), "MG Louvain clustering differs from SG at RMAT-26"
         print(f"RMAT-26 one-rank RCCL MG == SG: PageRank {it_sg} iterations, BFS from {root}, "
               f"Louvain Q {q_sg:.9f} in {lv_sg} levels")
-        del vm, cm
+        del vm, xm, dm, pm, vmb
         gm = None
         hm = None
+    _free_device()
 
 
 def test_mg_one_rank_rccl_louvain_rmat20_integer_equals_sg():
