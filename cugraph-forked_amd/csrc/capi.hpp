@@ -38,6 +38,8 @@ struct tuning_t {
   bool pr_fuse         = true;  // apply fused into the 16K-window push
   bool pr_enc          = true;  // x~ as fixed-point words (fp32 single GPU)
   bool pr_hub          = true;  // hub x~ staged in LDS (16K windows)
+  int64_t pr_band_cut  = -1;    // banded push source cut (-1: by size, 0: no bands)
+  bool pr_fast_build   = true;  // symmetric unweighted schedules through one-word keys (else the general build)
   int mg_chunks        = 0;     // MG overlap chunks (0: by size)
   double bfs_alpha     = 40.0;  // direction switch (Beamer's alpha / beta)
   double bfs_beta      = 64.0;
@@ -174,6 +176,12 @@ struct pr_push_t {
   // records every item's duration, the host then re-deals the items by those costs
   buffer item_ticks;      // uint32[nitems], s_memrealtime ticks
   int calib = 0;          // 0 not yet, 1 recorded (re-deal pending), 2 done or off
+  // source bands (pagerank.hip, banded push): every window's entries are split at a
+  // source cut into two virtual windows, vw = band * nwin_real + window; the stream
+  // and the items are band-major, so the whole grid sweeps the low sources first
+  bool bands = false;
+  int64_t nwin_real = 0;  // real windows (nwin counts the virtual ones)
+  buffer win_pub;         // uint32[nwin_real]: items of the window that published this iteration
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

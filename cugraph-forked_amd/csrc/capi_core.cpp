@@ -527,6 +527,8 @@ extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t
     else if (n == "pr_fuse") b(t.pr_fuse);
     else if (n == "pr_enc") b(t.pr_enc);
     else if (n == "pr_hub") b(t.pr_hub);
+    else if (n == "pr_band_cut") t.pr_band_cut = (int64_t)value;
+    else if (n == "pr_fast_build") b(t.pr_fast_build);
     else if (n == "mg_chunks") i32(t.mg_chunks);
     else if (n == "bfs_alpha") t.bfs_alpha = value;
     else if (n == "bfs_beta") t.bfs_beta = value;

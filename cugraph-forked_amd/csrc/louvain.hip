@@ -1122,17 +1122,49 @@ struct louvain_state {
 // over the level COO (the two rocPRIM segmented reductions this replaces read the 2 GB
 // of RMAT-23 level-0 weights twice at ~0.6 TB/s: 3.4 + 3.6 ms).  A wave takes 64
 // consecutive rows: a row of <= kVwLane edges is summed by its own lane in edge
-// order; a longer row by the whole wave, lane l summing edges l, l + 64, ... in
-// order and the 64 partials combined by a fixed xor tree (lane 0's value).  The
-// order depends only on the row's edges and degree, so every rank layout that
-// holds the row gives the same bits.  The same pass flags negative (or NaN)
-// weights and takes the largest row weight (level_stats: the fixed-point scale of
-// the hash sweeps), so plan_sweeps needs no pass of its own over the weights.
-constexpr int kVwLane = 16;
+// order; a row of <= kVwWave edges by the whole wave, lane l summing edges l, l + 64,
+// ... in order and the 64 partials combined by a fixed xor tree (lane 0's value); the
+// longer rows (the hubs: a wave that met the top 64 of RMAT-23 spent 14 ms on them)
+// are listed for k_vertex_weights_big, one 1024-thread block per row, thread t summing
+// edges t, t + 1024, ... and the 16 wave values added in wave order.  Every order
+// depends only on the row's edges and degree, so every rank layout that holds the row
+// gives the same bits.  The same passes flag negative (or NaN) weights and take the
+// largest row weight (the fixed-point scale of the hash sweeps), so plan_sweeps needs
+// no pass of its own over the weights.
+constexpr int kVwLane   = 16;
+constexpr int kVwWave   = 4096;
+constexpr int kVwBigThr = 1024;
 
+__device__ __forceinline__ void vw_stats_flush(u64 neg, u64 kmax, u64* stats)
+{
+  __shared__ u64 sn[16], sk[16];
+  int const lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    neg |= __shfl_xor(neg, o, 64);
+    u64 const y = __shfl_xor(kmax, o, 64);
+    kmax        = y > kmax ? y : kmax;
+  }
+  if (lane == 0) {
+    sn[threadIdx.x >> 6] = neg;
+    sk[threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 n = 0, m = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      n |= sn[i];
+      m = sk[i] > m ? sk[i] : m;
+    }
+    if (n) atomicOr(&stats[0], 1ull);
+    atomicMax(&stats[1], m);
+  }
+}
+
+// big: [0] rows listed, [1] rows taken by k_vertex_weights_big; list: the rows
 __global__ __launch_bounds__(256) void k_vertex_weights(int64_t const* off, uint32_t const* dst, double const* w,
                                                          int64_t nr, uint32_t base, double* k, double* self,
-                                                         uint8_t* has, u64* stats)
+                                                         uint8_t* has, u64* stats, unsigned* big, uint32_t* list)
 {
   int const lane    = threadIdx.x & 63;
   int64_t const nw  = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -1150,7 +1182,14 @@ __global__ __launch_bounds__(256) void k_vertex_weights(int64_t const* off, uint
         sv += dst[i] == (uint32_t)r + base ? x : 0.0;
       }
     }
-    u64 longm = __ballot(ok && e - b > kVwLane);
+    u64 const bigm = __ballot(ok && e - b > kVwWave);
+    if (bigm) {  // one atomic per wave: the hubs go to the block kernel
+      unsigned at = 0;
+      if (lane == 0) at = atomicAdd(&big[0], (unsigned)__popcll(bigm));
+      at = __shfl(at, 0, 64);
+      if ((bigm >> lane) & 1ull) list[at + __popcll(bigm & ((1ull << lane) - 1ull))] = (uint32_t)r;
+    }
+    u64 longm = __ballot(ok && e - b > kVwLane && e - b <= kVwWave);
     while (longm) {
       int const j       = __builtin_ctzll(longm);
       longm &= longm - 1;
@@ -1176,35 +1215,68 @@ __global__ __launch_bounds__(256) void k_vertex_weights(int64_t const* off, uint
       }
     }
     if (ok) {
-      k[r]    = kv;
-      self[r] = sv;
-      has[r]  = e > b ? 1 : 0;
+      has[r] = e > b ? 1 : 0;
+      if (e - b <= kVwWave) {
+        k[r]           = kv;
+        self[r]        = sv;
+        u64 const bits = (u64)__double_as_longlong(kv);
+        kmax           = bits > kmax ? bits : kmax;
+      }
+    }
+  }
+  vw_stats_flush(neg, kmax, stats);
+}
+
+// the listed rows, one at a time per block (taken by an atomic counter: which block
+// sums a row does not change its bits)
+__global__ __launch_bounds__(kVwBigThr) void k_vertex_weights_big(int64_t const* off, uint32_t const* dst,
+                                                                   double const* w, uint32_t base, double* k,
+                                                                   double* self, u64* stats, unsigned* big,
+                                                                   uint32_t const* list)
+{
+  __shared__ double wk[kVwBigThr / 64], wsf[kVwBigThr / 64];
+  __shared__ unsigned s_i;
+  int const lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u64 neg = 0, kmax = 0;
+  unsigned const n = big[0];
+  while (true) {
+    if (threadIdx.x == 0) s_i = atomicAdd(&big[1], 1u);
+    __syncthreads();
+    unsigned const i = s_i;
+    __syncthreads();
+    if (i >= n) break;
+    uint32_t const r = list[i];
+    int64_t const b = off[r], e = off[r + 1];
+    double pk = 0.0, ps = 0.0;
+    for (int64_t q = b + threadIdx.x; q < e; q += kVwBigThr) {
+      double const x = w[q];
+      neg |= !(x >= 0.0);
+      pk += x;
+      ps += dst[q] == r + base ? x : 0.0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      pk += __shfl_xor(pk, o, 64);
+      ps += __shfl_xor(ps, o, 64);
+    }
+    if (lane == 0) {
+      wk[wv]  = pk;
+      wsf[wv] = ps;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double kv = 0.0, sv = 0.0;
+      for (int j = 0; j < kVwBigThr / 64; ++j) {
+        kv += wk[j];
+        sv += wsf[j];
+      }
+      k[r]           = kv;
+      self[r]        = sv;
       u64 const bits = (u64)__double_as_longlong(kv);
       kmax           = bits > kmax ? bits : kmax;
     }
   }
-  // block reduce of (neg, kmax), one atomic pair per block
-  __shared__ u64 sn[4], sk[4];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    neg |= __shfl_xor(neg, o, 64);
-    u64 const y = __shfl_xor(kmax, o, 64);
-    kmax        = y > kmax ? y : kmax;
-  }
-  if (lane == 0) {
-    sn[threadIdx.x >> 6] = neg;
-    sk[threadIdx.x >> 6] = kmax;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    u64 n = 0, m = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
-      n |= sn[i];
-      m = sk[i] > m ? sk[i] : m;
-    }
-    if (n) atomicOr(&stats[0], 1ull);
-    atomicMax(&stats[1], m);
-  }
+  vw_stats_flush(neg, kmax, stats);
 }
 
 // stats (u64[2], device): [0] nonzero if a weight is negative or NaN, [1] the bits of
@@ -1216,9 +1288,16 @@ void vertex_weights(louvain_state& S, level_graph const& g, int64_t const* off, 
   int64_t const nr = g.nrows;
   fill<u64>(stats, 2, 0ull, s);
   if (nr == 0) return;
+  int64_t const nbig = std::min<int64_t>(nr, g.ne / kVwWave + 1);
+  dbuf<unsigned> big(2, s);
+  dbuf<uint32_t> list(std::max<int64_t>(nbig, 1), s);
+  fill<unsigned>(big.data(), 2, 0u, s);
   unsigned const grid = grid_for((size_t)((nr + 63) / 64), 4, 16384);
   hipLaunchKernelGGL(k_vertex_weights, dim3(grid), dim3(256), 0, s, off, g.dst.data(), g.w.data(), nr,
-                     (uint32_t)g.base, k, self, has_edges, stats);
+                     (uint32_t)g.base, k, self, has_edges, stats, big.data(), list.data());
+  CGX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_vertex_weights_big, dim3((unsigned)std::min<int64_t>(nbig, 512)), dim3(kVwBigThr), 0, s, off,
+                     g.dst.data(), g.w.data(), (uint32_t)g.base, k, self, stats, big.data(), list.data());
   CGX_LAUNCH_CHECK();
 }
 

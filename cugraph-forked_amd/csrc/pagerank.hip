@@ -475,6 +475,15 @@ inline int push_win_bits(int64_t n_rows, tuning_t const& tu)
   return n_rows >= (int64_t(1) << 23) ? 14 : n_rows >= (int64_t(1) << 22) ? 13 : 12;
 }
 
+// Source-band cut of the single-GPU 16K-window push (build_push_from_coo): tuning_t::
+// pr_band_cut > 0 sets it, 0 turns bands off, -1 picks by size (off until measured)
+inline int64_t push_band_cut(int64_t n, tuning_t const& tu)
+{
+  if (tu.pr_band_cut >= 0) return tu.pr_band_cut;
+  (void)n;
+  return 0;
+}
+
 // persistent push blocks: two per CU, one per CU for 16K-destination windows
 inline int push_blocks(int win_bits) { return win_bits >= 14 ? kPushBlocks / 2 : kPushBlocks; }
 
@@ -518,6 +527,10 @@ struct push_args {
   int64_t const* empty_wins;   // windows without items: applied by the last window's block
   int64_t nempty;
   int64_t nwin_items;          // windows with items
+  // source bands (pr_push_t::bands): item windows are virtual, vw = band * nwin_real + w
+  int bands;
+  int64_t nwin_real;
+  uint32_t* win_pub;           // per real window: items that published their sums this iteration
   int64_t nhub;                // sources whose x~ the 16K-window push stages in LDS (0: none)
   // CGX_PR_TIMELINE (measurement only): per item {launch << 32 | block, item, start, end}
   // in s_memrealtime ticks (100 MHz), tl[0] = records written
@@ -651,7 +664,121 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
   }
 }
 
+// Source bands: the sums of real window rw are its two virtual windows' -- the own
+// item's LDS when it is the whole of its virtual window (lds), else the plane in acc
+// at vw << WB: read and cleared (atomic exchange) when several items add into it
+// (win_multi), read (device-scope load) when one item stores it every iteration
 template <int WB, typename V, typename E, typename R>
+__device__ __forceinline__ void apply_window_banded(push_args<V, E, R> const& sa, int64_t rw, unsigned long long* lds,
+                                                    int64_t own_vw, unsigned long long& my_diff,
+                                                    unsigned long long& my_dang)
+{
+  auto const& a     = sa.a;
+  double const base = a.st->base;
+  double const pf   = a.st->pers_factor;
+  int64_t const v0  = rw << WB;
+  int const n       = (int)min((int64_t)1 << WB, a.nv - v0);
+  int64_t const vw0 = rw, vw1 = rw + sa.nwin_real;
+  bool const multi0 = sa.win_multi[vw0] != 0, multi1 = sa.win_multi[vw1] != 0;
+  unsigned long long* const p0 = sa.acc + (vw0 << WB);
+  unsigned long long* const p1 = sa.acc + (vw1 << WB);
+  auto plane = [&](unsigned long long* p, bool multi, int i) -> unsigned long long {
+    return multi ? __hip_atomic_exchange(p + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  constexpr int kB = 2;
+  for (int i0 = threadIdx.x; i0 < n; i0 += kB * kPushThreads) {
+    unsigned long long f[kB];
+    R old[kB], ow[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      int const i = i0 + j * kPushThreads;
+      if (i < n) {
+        unsigned long long x0, x1;
+        if (lds && own_vw == vw0) {
+          x0     = lds[i];
+          lds[i] = 0ull;
+        } else {
+          x0 = plane(p0, multi0, i);
+        }
+        if (lds && own_vw == vw1) {
+          x1     = lds[i];
+          lds[i] = 0ull;
+        } else {
+          x1 = plane(p1, multi1, i);
+        }
+        f[j]   = x0 + x1;
+        old[j] = a.pr[v0 + i];
+        ow[j]  = a.outw[v0 + i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      int const i = i0 + j * kPushThreads;
+      if (i < n)
+        vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf,
+                                    my_diff, my_dang);
+    }
+  }
+}
+
+// fused finish of a banded item: count the item off its real window first; an item
+// that is not the window's last publishes its sums (stores them when it is the whole
+// of its virtual window, else adds them) and then counts itself published; the last
+// waits for the others' publications -- blocks already past their counting, so the
+// wait always ends -- and applies the window from its LDS and the planes.  The last
+// item of a whole virtual window never writes its sums out: with two bands per window
+// one 128 KB plane is written and read per window instead of none.
+template <int WB, typename V, typename E, typename R>
+__device__ __forceinline__ bool banded_finish(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w,
+                                              unsigned long long& my_diff, unsigned long long& my_dang)
+{
+  __shared__ int s_last;
+  int const tid     = threadIdx.x;
+  int64_t const vw  = win_w & kWinMask;
+  bool const whole  = (win_w & kWholeItem) != 0;
+  int64_t const rw  = vw >= sa.nwin_real ? vw - sa.nwin_real : vw;
+  __syncthreads();  // the item's LDS sums are complete
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_sub(sa.win_left + rw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
+  __syncthreads();
+  bool const last = s_last != 0;
+  if (!last || !whole) {
+    unsigned long long* g = sa.acc + (vw << WB);
+    if (whole) {
+      for (int i = tid; i < (1 << WB); i += kPushThreads) {
+        __hip_atomic_store(g + i, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[i] = 0ull;
+      }
+    } else {
+      for (int i = tid; i < (1 << WB); i += kPushThreads) {
+        unsigned long long const v = acc[i];
+        if (v) {
+          __hip_atomic_fetch_add(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          acc[i] = 0ull;
+        }
+      }
+    }
+    wait_vmem();  // this thread's stores / adds are performed before the item counts as published
+    __syncthreads();
+    if (!last) {
+      if (tid == 0) __hip_atomic_fetch_add(sa.win_pub + rw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  if (tid == 0) {
+    uint32_t const need = sa.win_items[rw] - 1u;
+    while (__hip_atomic_load(sa.win_pub + rw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+      __builtin_amdgcn_s_sleep(2);
+    __hip_atomic_store(sa.win_pub + rw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sa.win_left + rw, sa.win_items[rw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  apply_window_banded<WB, V, E, R>(sa, rw, whole ? acc : nullptr, vw, my_diff, my_dang);
+  return true;
+}
+
+template <int WB, typename V, typename E, typename R, bool BANDS = false>
 __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
 {
   __shared__ unsigned long long s_red[kPushThreads / 64];
@@ -660,6 +787,9 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
   int64_t const w     = win_w & kWinMask;
   bool const whole    = (win_w & kWholeItem) != 0;
   unsigned long long my_diff = 0, my_dang = 0;
+  if constexpr (BANDS) {
+    if (!banded_finish<WB, V, E, R>(sa, acc, win_w, my_diff, my_dang)) return;
+  } else {
   __syncthreads();  // the item's LDS sums are complete
   if (!whole) {
     unsigned long long* g = sa.acc + (w << WB);
@@ -680,6 +810,7 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
       __hip_atomic_store(sa.win_left + w, sa.win_items[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   apply_window<WB, V, E, R>(sa, w, whole ? acc : nullptr, my_diff, my_dang);
+  }
   unsigned long long const bd = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const bg = block_sum_u64<kPushThreads>(my_dang, s_red);
   if (tid == 0) {
@@ -692,7 +823,10 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
   __syncthreads();
   if (!s_flag) return;  // (a whole window's LDS was cleared by apply_window)
   my_diff = my_dang = 0;
-  for (int64_t k = 0; k < sa.nempty; ++k) apply_window<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, my_diff, my_dang);
+  for (int64_t k = 0; k < sa.nempty; ++k) {
+    if constexpr (BANDS) apply_window_banded<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, -1, my_diff, my_dang);
+    else apply_window<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, my_diff, my_dang);
+  }
   unsigned long long const ed = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const eg = block_sum_u64<kPushThreads>(my_dang, s_red);
   if (tid == 0) {
@@ -716,9 +850,13 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
 // kernel has the fused finish (16K windows only, decided at run time by sa.fuse).  In
 // the 64-VGPR kernels of 4K / 8K windows its code costs 140-156 B of scratch per lane:
 // measured on RMAT-22, 0.274 against 0.176 ms/iteration unfused (same box)
-template <int WB, typename V, typename E, typename R, bool FUSE>
+template <int WB, typename V, typename E, typename R, bool FUSE, bool BANDS = false>
 __device__ __forceinline__ void end_item(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
 {
+  if constexpr (BANDS) {  // (a banded schedule is always fused)
+    fused_finish<WB, V, E, R, true>(sa, acc, win_w);
+    return;
+  }
   if constexpr (FUSE) {
     if (sa.fuse) {
       fused_finish<WB, V, E, R>(sa, acc, win_w);
@@ -898,7 +1036,7 @@ __device__ __forceinline__ void wave_incl_scan_rows(uint32_t (&v)[N])
 // the texture path -- the push's busiest unit (TA 71 %, TD 80 % busy).  Sources are
 // sorted within a window, so almost every segment is all-hub or hub-free; a segment
 // that straddles the boundary gathers from global memory.
-template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false>
+template <int WB, typename V, typename E, typename R, bool ENC, bool HUB = false, bool FUSE = false, bool BANDS = false>
 __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
 {
   // ENC: x~ holds enc_fixed words (fp32 single-GPU), decoded with dec_fixed.
@@ -1034,7 +1172,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       nB = n2;
       bB = __builtin_amdgcn_readfirstlane(b2);
     }
-    end_item<WB, V, E, R, FUSE>(sa, acc, win);
+    end_item<WB, V, E, R, FUSE, BANDS>(sa, acc, win);
     // (the item id from LDS too: s_item holds it until thread 0 takes the next)
     if (sa.item_ticks && tid == 0) sa.item_ticks[s_item] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - s_t0);
     if (sa.tl && tid == 0) {
@@ -1061,10 +1199,12 @@ __global__ __launch_bounds__(kPushThreads, 8) void k_pr_push16(push_args<V, E, R
 }
 
 // 16K-destination windows: 128 KB of LDS, one block (16 waves) per CU, no 8-waves bound
-template <typename V, typename E, typename R, bool ENC>
+// (BANDS: source-banded schedules, a kernel of its own: the banded finish in the same
+// kernel took it from 115 VGPRs to 127 and 12 B of scratch)
+template <typename V, typename E, typename R, bool ENC, bool BANDS = false>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, R> sa)
 {
-  push_body16<14, V, E, R, ENC, true, true>(sa);
+  push_body16<14, V, E, R, ENC, true, true, BANDS>(sa);
 }
 
 template <typename V, typename E, typename R, bool WEIGHTED>
@@ -1154,41 +1294,145 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 }
 
 // ---- push schedule construction (once per graph, cached on the pull adjacency)
+// the row of every edge.  A block takes 4096 consecutive edges: thread 0 finds the
+// rows of the first and the last (binary search over all offsets), the offsets of the
+// rows between go to LDS when there are at most 4096 of them, and each edge searches
+// only those (one thread per edge searching all V offsets was 5.7 ms of a first
+// PageRank call at RMAT-24)
+constexpr int kRowsTile = 4096;
 template <typename E>
-__global__ void k_edge_rows(E const* off, int64_t nv, int64_t ne, uint32_t* rows)
+__device__ __forceinline__ int64_t row_of_edge(E const* off, int64_t lo, int64_t hi, int64_t e)
 {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t lo = 0, hi = nv - 1;  // last row with off[row] <= e
-    while (lo < hi) {
-      int64_t mid = (lo + hi + 1) >> 1;
-      if ((int64_t)off[mid] <= e) lo = mid;
-      else hi = mid - 1;
+  while (lo < hi) {  // last row in [lo, hi] with off[row] <= e
+    int64_t const mid = (lo + hi + 1) >> 1;
+    if ((int64_t)off[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void k_edge_rows(E const* off, int64_t nv, int64_t ne, uint32_t* rows)
+{
+  __shared__ int64_t s_r[2];
+  __shared__ E s_off[kRowsTile + 1];
+  for (int64_t e0 = (int64_t)blockIdx.x * kRowsTile; e0 < ne; e0 += (int64_t)gridDim.x * kRowsTile) {
+    int64_t const e1 = min(e0 + kRowsTile, ne);
+    if (threadIdx.x == 0) {
+      s_r[0] = row_of_edge(off, 0, nv - 1, e0);
+      s_r[1] = row_of_edge(off, s_r[0], nv - 1, e1 - 1);
     }
-    rows[e] = (uint32_t)lo;
+    __syncthreads();
+    int64_t const r0 = s_r[0], r1 = s_r[1];
+    bool const staged = r1 - r0 < kRowsTile;
+    if (staged)
+      for (int64_t i = threadIdx.x; i <= r1 - r0; i += blockDim.x) s_off[i] = off[r0 + i];
+    __syncthreads();
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      int64_t r;
+      if (staged) {
+        int64_t lo = 0, hi = r1 - r0;
+        while (lo < hi) {
+          int64_t const mid = (lo + hi + 1) >> 1;
+          if ((int64_t)s_off[mid] <= e) lo = mid;
+          else hi = mid - 1;
+        }
+        r = r0 + lo;
+      } else {
+        r = row_of_edge(off, r0, r1, e);
+      }
+      rows[e] = (uint32_t)r;
+    }
+    __syncthreads();
   }
 }
 
-// key = window << 32 | source, value = edge position
+// key = window << 32 | source, value = edge position; with source bands (cut > 0) the
+// window is the virtual one, band * nwin_real + window, band = source >= cut
 template <typename C>
-__global__ void k_push_keys(C const* cols, uint32_t const* rows, int64_t ne, int wb, uint64_t* keys, uint32_t* vals)
+__global__ void k_push_keys(C const* cols, uint32_t const* rows, int64_t ne, int wb, uint32_t cut, int64_t nwin_real,
+                            uint64_t* keys, uint32_t* vals)
 {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-    keys[e] = ((uint64_t)(rows[e] >> wb) << 32) | (uint32_t)cols[e];
-    vals[e] = (uint32_t)e;
+    uint32_t const c = (uint32_t)cols[e];
+    uint64_t const w = (uint64_t)(rows[e] >> wb) + (cut && c >= cut ? (uint64_t)nwin_real : 0ull);
+    keys[e]          = (w << 32) | c;
+    vals[e]          = (uint32_t)e;
   }
 }
+
+// Key codecs of the schedule sort.  key_w32: window << 32 | source, the edge position
+// in a value array beside it (weighted graphs, any input order).  key_p: one word per
+// entry, window << shv | source << wb | slot -- the symmetric unweighted build, whose
+// keys come out of the out-edge adjacency already in source order (k_push_keys_p): a
+// keys-only sort of the window bits moves 8 B per entry and pass instead of 12, and the
+// packing reads the slot from the key instead of gathering the destination.
+struct key_w32 {
+  __device__ __forceinline__ int64_t win(uint64_t k) const { return (int64_t)(k >> 32); }
+  __device__ __forceinline__ uint32_t src(uint64_t k) const { return (uint32_t)k; }
+};
+struct key_p {
+  int shv, wb;
+  uint64_t smask;
+  __device__ __forceinline__ int64_t win(uint64_t k) const { return (int64_t)(k >> shv); }
+  __device__ __forceinline__ uint32_t src(uint64_t k) const { return (uint32_t)((k >> wb) & smask); }
+  __device__ __forceinline__ uint32_t slot(uint64_t k) const { return (uint32_t)k & ((1u << wb) - 1u); }
+};
 
 // first position of every window w in [0, nwin] among the sorted keys
-__global__ void k_win_starts(uint64_t const* keys, int64_t ne, int64_t nwin, int64_t* ws)
+template <typename KC = key_w32>
+__global__ void k_win_starts(uint64_t const* keys, int64_t ne, int64_t nwin, int64_t* ws, KC kc = {})
 {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x) {
     int64_t lo = 0, hi = ne;
     while (lo < hi) {
       int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)(keys[mid] >> 32) < w) lo = mid + 1;
+      if (kc.win(keys[mid]) < w) lo = mid + 1;
       else hi = mid;
     }
     ws[w] = lo;
+  }
+}
+
+// key_p keys of a symmetric graph's out-edges (row = source, index = destination), in
+// the adjacency's source order; rows found per 4096-edge tile as k_edge_rows does
+template <typename E>
+__global__ __launch_bounds__(256) void k_push_keys_p(E const* off, uint32_t const* idx, int64_t nv, int64_t ne,
+                                                     int wb, int shv, uint32_t cut, int64_t nwin_real, uint64_t* keys)
+{
+  __shared__ int64_t s_r[2];
+  __shared__ E s_off[kRowsTile + 1];
+  uint32_t const low = (1u << wb) - 1u;
+  for (int64_t e0 = (int64_t)blockIdx.x * kRowsTile; e0 < ne; e0 += (int64_t)gridDim.x * kRowsTile) {
+    int64_t const e1 = min(e0 + kRowsTile, ne);
+    if (threadIdx.x == 0) {
+      s_r[0] = row_of_edge(off, 0, nv - 1, e0);
+      s_r[1] = row_of_edge(off, s_r[0], nv - 1, e1 - 1);
+    }
+    __syncthreads();
+    int64_t const r0 = s_r[0], r1 = s_r[1];
+    bool const staged = r1 - r0 < kRowsTile;
+    if (staged)
+      for (int64_t i = threadIdx.x; i <= r1 - r0; i += blockDim.x) s_off[i] = off[r0 + i];
+    __syncthreads();
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      int64_t r;
+      if (staged) {
+        int64_t lo = 0, hi = r1 - r0;
+        while (lo < hi) {
+          int64_t const mid = (lo + hi + 1) >> 1;
+          if ((int64_t)s_off[mid] <= e) lo = mid;
+          else hi = mid - 1;
+        }
+        r = r0 + lo;
+      } else {
+        r = row_of_edge(off, r0, r1, e);
+      }
+      uint32_t const d = idx[e], src = (uint32_t)r;
+      uint64_t const w = (uint64_t)(d >> wb) + (cut && src >= cut ? (uint64_t)nwin_real : 0ull);
+      keys[e]          = (w << shv) | ((uint64_t)src << wb) | (d & low);
+    }
+    __syncthreads();
   }
 }
 
@@ -1245,13 +1489,14 @@ __global__ void k_push_pack(uint64_t const* keys, uint32_t const* vals, uint32_t
 // jumps in front of real entry k: its source gap D to the previous entry of the
 // window (0 before the window's first) is coded in the entry when D <= dmax,
 // else by ceil(D / pmax) jumps and an entry of delta 0
+template <typename KC = key_w32>
 __global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t dmax, uint32_t pmax,
-                              uint32_t* mj)
+                              uint32_t* mj, KC kc = {})
 {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
-    int64_t const w     = (int64_t)(keys[k] >> 32);
-    uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
-    uint32_t const D    = (uint32_t)keys[k] - prev;
+    int64_t const w     = kc.win(keys[k]);
+    uint32_t const prev = k == ws[w] ? 0u : kc.src(keys[k - 1]);
+    uint32_t const D    = kc.src(keys[k]) - prev;
     mj[k]               = D > dmax ? (D + pmax - 1) / pmax : 0u;
   }
 }
@@ -1283,18 +1528,46 @@ __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t co
   }
 }
 
+// the same from key_p keys (the slot in the key); cm a 32-bit prefix when the edges
+// are below 2^31 (no jump total can wrap it), else 64-bit
+template <typename CM>
+__global__ void k_pack16_p(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t const* mj, CM const* cm,
+                           unsigned long long const* pb, key_p kc, uint32_t pmax, uint16_t* ent16)
+{
+  int const wb        = kc.wb;
+  uint32_t const jump = (1u << (16 - wb)) - 1;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ne; k += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t const key  = keys[k];
+    int64_t const w     = kc.win(key);
+    uint32_t const prev = k == ws[w] ? 0u : kc.src(keys[k - 1]);
+    uint32_t const D    = kc.src(key) - prev;
+    uint32_t const m    = mj[k];
+    int64_t const pos   = k + (int64_t)cm[k] + (int64_t)pb[w];
+    uint32_t const slot = kc.slot(key);
+    if (m == 0) {
+      ent16[seg_store_index(pos)] = (uint16_t)((D << wb) | slot);
+    } else {
+      for (uint32_t j = 0; j < m; ++j) {
+        uint32_t const pay                  = j + 1 < m ? pmax : D - pmax * (m - 1);
+        ent16[seg_store_index(pos - m + j)] = (uint16_t)((jump << wb) | pay);
+      }
+      ent16[seg_store_index(pos)] = (uint16_t)slot;  // delta 0
+    }
+  }
+}
+
 // Every window's packed stream starts at a multiple of kSegEntries and is padded
 // with jumps of 0 (no edge) to a multiple of it, so every wave segment of a unit
 // is whole and the push needs no per-entry bound check.
 // unpadded packed start of window w (w == nwin: total)
-__device__ __forceinline__ int64_t packed_start(int64_t const* ws, unsigned long long const* cm, int64_t w,
-                                                int64_t nwin, int64_t total)
+template <typename CM>
+__device__ __forceinline__ int64_t packed_start(int64_t const* ws, CM const* cm, int64_t w, int64_t nwin, int64_t total)
 {
   return w == nwin ? total : ws[w] + (ws[w] > 0 ? (int64_t)cm[ws[w] - 1] : 0);
 }
 // padding after every window (pad[nwin] = 0)
-__global__ void k_packed_pads(int64_t const* ws, unsigned long long const* cm, int64_t nwin, int64_t total,
-                              unsigned long long* pad)
+template <typename CM>
+__global__ void k_packed_pads(int64_t const* ws, CM const* cm, int64_t nwin, int64_t total, unsigned long long* pad)
 {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x) {
     int64_t const len = w == nwin ? 0 : packed_start(ws, cm, w + 1, nwin, total) - packed_start(ws, cm, w, nwin, total);
@@ -1302,11 +1575,28 @@ __global__ void k_packed_pads(int64_t const* ws, unsigned long long const* cm, i
   }
 }
 // padded window starts (pb = exclusive prefix of the pads; nws[nwin] = padded total)
-__global__ void k_packed_win_starts(int64_t const* ws, unsigned long long const* cm, unsigned long long const* pb,
-                                    int64_t nwin, int64_t total, int64_t* nws)
+template <typename CM>
+__global__ void k_packed_win_starts(int64_t const* ws, CM const* cm, unsigned long long const* pb, int64_t nwin,
+                                    int64_t total, int64_t* nws)
 {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x)
     nws[w] = packed_start(ws, cm, w, nwin, total) + (int64_t)pb[w];
+}
+
+// units straight from the padded window starts: window w's units start at nws[w] + j *
+// kPushUnit (what the flag marks + scan + heads below give, without a pass over every
+// packed position)
+__global__ void k_unit_counts(int64_t const* nws, int64_t nwin, uint32_t* cnt)
+{
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x)
+    cnt[w] = w == nwin ? 0u : (uint32_t)((nws[w + 1] - nws[w] + kPushUnit - 1) / kPushUnit);
+}
+__global__ void k_units_direct(int64_t const* nws, int64_t nwin, uint32_t const* upos, push_unit* units)
+{
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwin; w += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t u = upos[w];
+    for (int64_t p = nws[w]; p < nws[w + 1]; p += kPushUnit) units[u++] = push_unit{p, 0, 0, w};
+  }
 }
 
 // unit heads: every window start and every kPushUnit entries into a window
@@ -1331,10 +1621,10 @@ __global__ void k_packed_unit_heads(uint32_t const* flag, uint32_t const* uid, i
 }
 
 // running source before the first entry of every (unit, wave segment)
+template <typename KC, typename CM>
 __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t const* keys, int64_t ne,
-                            int64_t const* ws, uint32_t const* mj, unsigned long long const* cm,
-                            unsigned long long const* pb, uint32_t dmax, uint32_t pmax,
-                            uint32_t* seg_base)
+                            int64_t const* ws, uint32_t const* mj, CM const* cm, unsigned long long const* pb,
+                            uint32_t dmax, uint32_t pmax, uint32_t* seg_base, KC kc)
 {
   int64_t const n = nunits * kSegsPerUnit;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1345,15 +1635,15 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
       int64_t lo = 0, hi = ne - 1;  // first real entry at a packed position >= p
       while (lo < hi) {
         int64_t mid = (lo + hi) >> 1;
-        if (mid + (int64_t)cm[mid] + (int64_t)pb[keys[mid] >> 32] < p) lo = mid + 1;
+        if (mid + (int64_t)cm[mid] + (int64_t)pb[kc.win(keys[mid])] < p) lo = mid + 1;
         else hi = mid;
       }
       int64_t const k     = lo;
       uint32_t const m    = mj[k];
-      int64_t const w     = (int64_t)(keys[k] >> 32);
+      int64_t const w     = kc.win(keys[k]);
       int64_t const j     = p - (k + (int64_t)cm[k] + (int64_t)pb[w] - m);
-      uint32_t const prev = k == ws[w] ? 0u : (uint32_t)keys[k - 1];
-      uint32_t const src  = (uint32_t)keys[k];
+      uint32_t const prev = k == ws[w] ? 0u : kc.src(keys[k - 1]);
+      uint32_t const src  = kc.src(keys[k]);
       uint32_t const D    = src - prev;
       base = j < (int64_t)m ? prev + pmax * (uint32_t)j : src - (m ? 0u : (D <= dmax ? D : 0u));
     }
@@ -1383,16 +1673,23 @@ inline void mark_whole_items(hipStream_t s, pr_push_t& pp, push_unit* units, std
   to_device(units, hu.data(), (size_t)nunits, s);
   // items per window (fused apply)
   {
-    std::vector<uint32_t> cnt((size_t)std::max<int64_t>(pp.nwin, 1), 0u);
+    // (source bands: the items of a real window over both of its virtual windows)
+    int64_t const nreal = pp.bands ? pp.nwin_real : pp.nwin;
+    std::vector<uint32_t> cnt((size_t)std::max<int64_t>(nreal, 1), 0u);
     for (int64_t i = 0; i < nitems; ++i) {
       int64_t const wu = hu[item_u[i]].win & kWinMask;
-      if (wu < pp.nwin) ++cnt[wu];
+      if (wu < pp.nwin) ++cnt[pp.bands ? wu % nreal : wu];
     }
     std::vector<int64_t> empty;
     pp.nwin_items = 0;
-    for (int64_t w = 0; w < pp.nwin; ++w) {
+    for (int64_t w = 0; w < nreal; ++w) {
       if (cnt[w]) ++pp.nwin_items;
       else empty.push_back(w);
+    }
+    if (pp.bands) {
+      pp.win_pub.set_stream(s);
+      pp.win_pub.resize(cnt.size() * sizeof(uint32_t));
+      HIP_CHECK(hipMemsetAsync(pp.win_pub.data(), 0, cnt.size() * sizeof(uint32_t), s));
     }
     pp.nempty = (int64_t)empty.size();
     pp.win_items.set_stream(s);
@@ -1539,6 +1836,15 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp, tuning_t const& tu)
       qg[best].push_back(g);
       load[best] += gc[g];
     }
+    if (pp.bands) {  // source bands: each queue takes its band-0 groups first (items are band-major)
+      std::vector<int> gband(ng, 0);
+      {
+        auto hu = to_host(pp.units.data<push_unit>(), (size_t)pp.nunits, s);
+        auto iu = to_host(pp.items.data<int64_t>(), (size_t)n, s);
+        for (int64_t g = 0; g < ng; ++g) gband[g] = (hu[iu[g * G]].win & kWinMask) >= pp.nwin_real ? 1 : 0;
+      }
+      for (auto& l : qg) std::stable_sort(l.begin(), l.end(), [&](int64_t a, int64_t b) { return gband[a] < gband[b]; });
+    }
     pp.qoff.assign(kQueues + 1, 0);
     for (int q = 0; q < kQueues; ++q) {
       pp.qoff[q] = (int64_t)queue.size();
@@ -1554,19 +1860,32 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp, tuning_t const& tu)
 
 // Push schedule of an edge list given as (row = destination, col = source) with
 // destinations in [0, n_rows) and sources in [0, n_cols) -- the SG pull adjacency
-// or one MG 2D block.
+// or one MG 2D block.  col_sorted: the list is in (source, destination) order (the
+// out-edge adjacency of a symmetric graph), so a stable sort on the window bits alone
+// gives the (window, source, destination) order the full key sort gives -- 2 radix
+// passes over the edges instead of 6 (RMAT-24: the first call's largest step)
+//
+// band_cut > 0 (16K-window packed pushes only): source bands -- each window's entries
+// split at the source cut into two virtual windows, vw = band * nwin_real + window, so
+// the stream, the items and the queues run every window's low-source entries first
+// and the whole grid gathers one band of x~ at a time (push_body16 BANDS)
 template <typename C, typename R>
 void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
-                         int64_t n_cols, pr_push_t& pp, tuning_t const& tu)
+                         int64_t n_cols, pr_push_t& pp, tuning_t const& tu, bool col_sorted = false,
+                         int64_t band_cut = 0)
 {
   pp.built = true;
   pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
   if (!pp.ok) return;
-  int const wb       = push_win_bits(n_rows, tu);
-  int const sb       = 32 - wb;
-  int64_t const nwin = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
+  int const wb = push_win_bits(n_rows, tu);
+  int const sb = 32 - wb;
+  if (wb < 14 || w || !tu.pr_packed || band_cut >= n_cols) band_cut = 0;
+  int64_t const nwin_real = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
+  int64_t const nwin      = band_cut > 0 ? 2 * nwin_real : nwin_real;
   pp.win_bits        = wb;
   pp.nwin            = nwin;
+  pp.bands           = band_cut > 0;
+  pp.nwin_real       = nwin_real;
   pp.nacc            = nwin << wb;
   pp.acc.set_stream(s);
   pp.acc.resize(pp.nacc * sizeof(unsigned long long));
@@ -1584,14 +1903,15 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     dbuf<uint64_t> keys(ne, s);
     dbuf<uint32_t> vals(ne, s);
     hipLaunchKernelGGL(k_push_keys<C>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, cols, rows, ne, wb,
-                       keys.data(), vals.data());
+                       (uint32_t)band_cut, nwin_real, keys.data(), vals.data());
     CGX_LAUNCH_CHECK();
-    radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne, 0,
+    radix_sort_pairs<uint64_t, uint32_t>(keys.data(), keys_out.data(), vals.data(), vals_out.data(), (size_t)ne,
+                                         col_sorted ? 32 : 0,
                                          32 + bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)), s);
   }
   dbuf<int64_t> ws(nwin + 1, s);
-  hipLaunchKernelGGL(k_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                     nwin, ws.data());
+  hipLaunchKernelGGL(k_win_starts<key_w32>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s,
+                     keys_out.data(), ne, nwin, ws.data(), key_w32{});
   CGX_LAUNCH_CHECK();
   pp.packed = false;
   if (!w && tu.pr_packed) {  // 16-bit entries unless the jumps would grow the entries by more than half
@@ -1599,8 +1919,8 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     uint32_t const pmax = (1u << wb) - 1;         // jump payloads 1 .. pmax
     dbuf<uint32_t> mj(ne + 1, s);
     dbuf<unsigned long long> ex(ne + 1, s);
-    hipLaunchKernelGGL(k_jump_counts, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
-                       ws.data(), dmax, pmax, mj.data());
+    hipLaunchKernelGGL(k_jump_counts<key_w32>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s,
+                       keys_out.data(), ne, ws.data(), dmax, pmax, mj.data(), key_w32{});
     CGX_LAUNCH_CHECK();
     fill<uint32_t>(mj.data() + ne, 1, 0u, s);
     exclusive_scan<uint32_t, unsigned long long>(mj.data(), ex.data(), ne + 1, s);
@@ -1608,7 +1928,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     unsigned long long const* cm = ex.data() + 1;  // inclusive prefix
     // windows padded to whole wave segments (k_packed_pads)
     dbuf<unsigned long long> pad(nwin + 1, s), pb(nwin + 1, s);
-    hipLaunchKernelGGL(k_packed_pads, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nwin,
+    hipLaunchKernelGGL(k_packed_pads<unsigned long long>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nwin,
                        total0, pad.data());
     CGX_LAUNCH_CHECK();
     exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nwin + 1, s);
@@ -1627,7 +1947,7 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
                          pp.ent16.data<uint16_t>());
       CGX_LAUNCH_CHECK();
       dbuf<int64_t> nws(nwin + 1, s);
-      hipLaunchKernelGGL(k_packed_win_starts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
+      hipLaunchKernelGGL(k_packed_win_starts<unsigned long long>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
                          cm, pb.data(), nwin, total0, nws.data());
       dbuf<uint32_t> pflag(total + 1, s), puid(total + 1, s);
       fill<uint32_t>(pflag.data(), (size_t)(total + 1), 0u, s);
@@ -1646,9 +1966,9 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       CGX_LAUNCH_CHECK();
       pp.seg_base.set_stream(s);
       pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
-      hipLaunchKernelGGL(k_seg_bases, dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0, s, units,
+      hipLaunchKernelGGL((k_seg_bases<key_w32, unsigned long long>), dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0, s, units,
                          nunits, keys_out.data(), ne, ws.data(), mj.data(), cm, pb.data(), dmax, pmax,
-                         pp.seg_base.data<uint32_t>());
+                         pp.seg_base.data<uint32_t>(), key_w32{});
       CGX_LAUNCH_CHECK();
       pp.ent.release();
       pp.ew.release();
@@ -1657,6 +1977,13 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       HIP_CHECK(hipStreamSynchronize(s));
       return;
     }
+  }
+  if (band_cut > 0) {  // bands need the packed format: the same schedule without them
+    keys_out.free();
+    vals_out.free();
+    ws.free();
+    build_push_from_coo<C, R>(s, rows, cols, w, ne, n_rows, n_cols, pp, tu, col_sorted, 0);
+    return;
   }
   dbuf<uint32_t> flag(ne + 1, s), uid(ne + 1, s);
   hipLaunchKernelGGL(k_unit_flags, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys_out.data(), ne,
@@ -1721,6 +2048,128 @@ bool unit_weights(handle_t& h, graph_t& g, adjacency_t& adj)
   return adj.unit_weights == 1;
 }
 
+// The packed schedule of a symmetric unweighted graph straight from its adjacency
+// (build_push_from_coo's packed path with key_p keys; same stream, units, bases and
+// items bit for bit): one word per entry through a keys-only sort of the window bits,
+// no destination gather while packing, units from the window starts.  RMAT-24's first
+// call spent 29 ms in the general build.  false: the keys do not fit a word or the
+// stream would not pack -- nothing built, the caller takes the general path.
+template <typename E, typename CM>
+bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, int64_t ne, int64_t nv, pr_push_t& pp,
+                              tuning_t const& tu, int64_t band_cut)
+{
+  int const wb = push_win_bits(nv, tu);
+  if (wb < 14 || band_cut >= nv) band_cut = 0;
+  int64_t const nwin_real = std::max<int64_t>(1, (nv + (int64_t(1) << wb) - 1) >> wb);
+  int64_t const nwin      = band_cut > 0 ? 2 * nwin_real : nwin_real;
+  int const sbits = std::max(1, bits_for((unsigned long long)std::max<int64_t>(nv - 1, 1)));
+  int const vbits = std::max(1, bits_for((unsigned long long)std::max<int64_t>(nwin - 1, 1)));
+  int const shv   = wb + sbits;
+  if (shv + vbits > 64 || (uint64_t)ne >= (1ull << 32) || (uint64_t)nv >= (1ull << 32)) return false;
+  key_p const kc{shv, wb, (sbits >= 32 ? ~0ull : ((1ull << sbits) - 1ull))};
+  uint32_t const dmax = (1u << (16 - wb)) - 2, pmax = (1u << wb) - 1;
+  dbuf<uint64_t> kbuf(std::max<int64_t>(ne, 1), s);
+  {
+    dbuf<uint64_t> k2(std::max<int64_t>(ne, 1), s);
+    if (ne) {
+      hipLaunchKernelGGL(k_push_keys_p<E>, dim3((unsigned)std::min<int64_t>((ne + kRowsTile - 1) / kRowsTile, 65536)),
+                         dim3(256), 0, s, off, idx, nv, ne, wb, shv, (uint32_t)band_cut, nwin_real, kbuf.data());
+      CGX_LAUNCH_CHECK();
+      rocprim::double_buffer<uint64_t> db(kbuf.data(), k2.data());
+      size_t tmp = 0;
+      HIP_CHECK(rocprim::radix_sort_keys(nullptr, tmp, db, (size_t)ne, shv, shv + vbits, s));
+      buffer t(tmp, s);
+      HIP_CHECK(rocprim::radix_sort_keys(t.data(), tmp, db, (size_t)ne, shv, shv + vbits, s));
+      if (db.current() != kbuf.data()) std::swap(kbuf, k2);
+    }
+  }
+  uint64_t const* keys = kbuf.data();
+  dbuf<int64_t> ws(nwin + 1, s);
+  hipLaunchKernelGGL(k_win_starts<key_p>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys, ne, nwin,
+                     ws.data(), kc);
+  CGX_LAUNCH_CHECK();
+  dbuf<uint32_t> mj(ne + 1, s);
+  dbuf<CM> ex(ne + 1, s);
+  if (ne)
+    hipLaunchKernelGGL(k_jump_counts<key_p>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys, ne,
+                       ws.data(), dmax, pmax, mj.data(), kc);
+  CGX_LAUNCH_CHECK();
+  fill<uint32_t>(mj.data() + ne, 1, 0u, s);
+  exclusive_scan<uint32_t, CM>(mj.data(), ex.data(), ne + 1, s);
+  int64_t const total0 = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
+  CM const* cm         = ex.data() + 1;  // inclusive prefix
+  dbuf<unsigned long long> pad(nwin + 1, s), pb(nwin + 1, s);
+  hipLaunchKernelGGL(k_packed_pads<CM>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(), cm, nwin,
+                     total0, pad.data());
+  CGX_LAUNCH_CHECK();
+  exclusive_scan<unsigned long long, unsigned long long>(pad.data(), pb.data(), nwin + 1, s);
+  int64_t const total = total0 + (int64_t)to_host(pb.data() + nwin, 1, s)[0];
+  if (!(total <= ne + ne / 2 && (uint64_t)total < (1ull << 32))) return false;
+  pp.built     = true;
+  pp.ok        = true;
+  pp.win_bits  = wb;
+  pp.nwin      = nwin;
+  pp.bands     = band_cut > 0;
+  pp.nwin_real = nwin_real;
+  pp.nacc      = nwin << wb;
+  pp.acc.set_stream(s);
+  pp.acc.resize(pp.nacc * sizeof(unsigned long long));
+  HIP_CHECK(hipMemsetAsync(pp.acc.data(), 0, pp.nacc * sizeof(unsigned long long), s));
+  pp.tile_ctr.set_stream(s);
+  pp.tile_ctr.resize(2 * kQueues * kCtrStride * sizeof(unsigned int));
+  HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
+  pp.qoff.assign(kQueues + 1, 0);
+  pp.nitems = 0;
+  pp.packed = true;
+  uint16_t const pad_code = (uint16_t)(((1u << (16 - wb)) - 1) << wb);  // a jump of 0: no edge
+  pp.ent16.set_stream(s);
+  pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // + a unit: the kernel prefetches whole units
+  fill<uint16_t>(pp.ent16.data<uint16_t>(), (size_t)(total + kPushUnit), pad_code, s);
+  if (ne)
+    hipLaunchKernelGGL(k_pack16_p<CM>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys, ne, ws.data(),
+                       mj.data(), cm, pb.data(), kc, pmax, pp.ent16.data<uint16_t>());
+  CGX_LAUNCH_CHECK();
+  dbuf<int64_t> nws(nwin + 1, s);
+  hipLaunchKernelGGL(k_packed_win_starts<CM>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
+                     cm, pb.data(), nwin, total0, nws.data());
+  CGX_LAUNCH_CHECK();
+  dbuf<uint32_t> ucnt(nwin + 1, s), upos(nwin + 1, s);
+  hipLaunchKernelGGL(k_unit_counts, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, nws.data(), nwin,
+                     ucnt.data());
+  CGX_LAUNCH_CHECK();
+  exclusive_scan<uint32_t, uint32_t>(ucnt.data(), upos.data(), nwin + 1, s);
+  int64_t const nunits = (int64_t)to_host(upos.data() + nwin, 1, s)[0];
+  pp.units.set_stream(s);
+  pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
+  push_unit* units = pp.units.data<push_unit>();
+  hipLaunchKernelGGL(k_units_direct, dim3(grid_for(nwin, 64, 4096)), dim3(64), 0, s, nws.data(), nwin, upos.data(),
+                     units);
+  CGX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, total);
+  CGX_LAUNCH_CHECK();
+  pp.seg_base.set_stream(s);
+  pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
+  if (nunits)
+    hipLaunchKernelGGL((k_seg_bases<key_p, CM>), dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0,
+                       s, units, nunits, keys, ne, ws.data(), mj.data(), cm, pb.data(), dmax, pmax,
+                       pp.seg_base.data<uint32_t>(), kc);
+  CGX_LAUNCH_CHECK();
+  pp.ent.release();
+  pp.ew.release();
+  build_items(s, pp, units, nunits, wb >= 13, tu);
+  pp.nunits = nunits;
+  HIP_CHECK(hipStreamSynchronize(s));
+  return true;
+}
+
+template <typename E>
+bool build_push_packed_sym(hipStream_t s, E const* off, uint32_t const* idx, int64_t ne, int64_t nv, pr_push_t& pp,
+                           tuning_t const& tu, int64_t band_cut)
+{
+  if (ne < (int64_t(1) << 31)) return build_push_packed_sym_cm<E, uint32_t>(s, off, idx, ne, nv, pp, tu, band_cut);
+  return build_push_packed_sym_cm<E, unsigned long long>(s, off, idx, ne, nv, pp, tu, band_cut);
+}
+
 template <typename V, typename E, typename R>
 void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_weights)
 {
@@ -1732,13 +2181,27 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_
     adj.pr.ok    = false;
     return;
   }
+  if constexpr (sizeof(V) == 4) {
+    if (g.symmetric && !use_weights && h.tune.pr_packed && h.tune.pr_fast_build &&
+        build_push_packed_sym<E>(s, adj.offsets.data<E>(), reinterpret_cast<uint32_t const*>(adj.indices.data<V>()), ne,
+                                 nv, adj.pr, h.tune, push_band_cut(nv, h.tune)))
+      return;
+  }
   dbuf<uint32_t> rows(std::max<int64_t>(ne, 1), s);
   if (ne)
-    hipLaunchKernelGGL(k_edge_rows<E>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, adj.offsets.data<E>(),
-                       nv, ne, rows.data());
+    hipLaunchKernelGGL(k_edge_rows<E>, dim3((unsigned)std::min<int64_t>((ne + kRowsTile - 1) / kRowsTile, 65536)),
+                       dim3(256), 0, s, adj.offsets.data<E>(), nv, ne, rows.data());
   CGX_LAUNCH_CHECK();
+  if constexpr (sizeof(V) == 4) {
+    if (g.symmetric) {  // the same edges read as out-edges: (source = row, destination = index), source-sorted
+      build_push_from_coo<uint32_t, R>(s, reinterpret_cast<uint32_t const*>(adj.indices.data<V>()), rows.data(),
+                                       use_weights ? adj.weights.data<R>() : nullptr, ne, nv, nv, adj.pr, h.tune,
+                                       /*col_sorted=*/true, push_band_cut(nv, h.tune));
+      return;
+    }
+  }
   build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), use_weights ? adj.weights.data<R>() : nullptr, ne,
-                            nv, nv, adj.pr, h.tune);
+                            nv, nv, adj.pr, h.tune, false, push_band_cut(nv, h.tune));
 }
 
 template <typename V, typename R>
@@ -1793,15 +2256,20 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.tile_ctr = pp.tile_ctr.data<unsigned int>();
   sa.nwin     = pp.nwin;
   HIP_CHECK(hipMemsetAsync(sa.tile_ctr, 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
-  sa.fuse   = 0;  // the caller opts in (fuse_apply)
-  sa.parity = 0;
+  sa.fuse      = 0;  // the caller opts in (fuse_apply)
+  sa.parity    = 0;
+  sa.bands     = pp.bands ? 1 : 0;
+  sa.nwin_real = pp.nwin_real;
+  sa.win_pub   = pp.bands ? pp.win_pub.data<uint32_t>() : nullptr;
   if (!pp.win_items.empty()) {
     sa.win_items  = pp.win_items.data<uint32_t>();
     sa.win_left   = pp.win_left.data<uint32_t>();
     sa.empty_wins = pp.empty_wins.data<int64_t>();
     sa.nempty     = pp.nempty;
     sa.nwin_items = pp.nwin_items;
-    HIP_CHECK(hipMemcpyAsync(sa.win_left, sa.win_items, pp.nwin * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    int64_t const nreal = pp.bands ? pp.nwin_real : pp.nwin;
+    HIP_CHECK(hipMemcpyAsync(sa.win_left, sa.win_items, nreal * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    if (pp.bands) HIP_CHECK(hipMemsetAsync(sa.win_pub, 0, nreal * sizeof(uint32_t), s));
   }
 
 }
@@ -1810,6 +2278,7 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
 // block applies those alone); tuning_t::pr_fuse = 0 keeps the separate k_pr_apply (A/B)
 inline bool fuse_apply(pr_push_t const& pp, tuning_t const& tu)
 {
+  if (pp.bands) return pp.nitems > 0;  // (a banded schedule has no separate apply)
   return pp.win_bits >= 14 && pp.nitems > 0 && pp.nwin_items > 0 && pp.nempty <= 64 && !pp.win_items.empty() &&
          tu.pr_fuse;
 }
@@ -1819,6 +2288,7 @@ template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
   if (pp.win_bits == 14) {
+    if (pp.packed && pp.bands) return enc ? k_pr_push16_w14<V, E, R, true, true> : k_pr_push16_w14<V, E, R, false, true>;
     if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
     return weighted ? k_pr_push_q_w14<V, E, R, true> : k_pr_push_q_w14<V, E, R, false>;
   }
@@ -1856,7 +2326,6 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   if (nv == 0) return;
 
   adjacency_t& adj = ensure_adjacency(h, g, /*transposed=*/true);
-  ensure_schedule(h, g, adj);
   if (expensive && g.weighted) {
     CGX_INPUT(count_negative<R>(adj.weights.data<R>(), (size_t)g.num_edges, s) == 0,
               "Invalid input argument: input graph should have non-negative edge weights.");
@@ -1919,8 +2388,18 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     CGX_LAUNCH_CHECK();
   }
 
+  // windowed push (our own out-weight sums keep every fixed-point sum <= 1; user
+  // precomputed out-weights may not: generic pull kernel then)
+  bool push = pow_v == nullptr && max_iter > 0;
+  bool const push_w = g.weighted && !(push && unit_weights<R>(h, g, adj));  // entry weights in the push
+  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj, push_w);
+  push = push && adj.pr.ok;
+  // the degree-binned pull schedule only for the pull path (its host-built items were
+  // 7.4 ms of a first call at RMAT-24 that never used them)
+  if (!push) ensure_schedule(h, g, adj);
+
   // iteration state
-  int const nblk_iter = (int)adj.num_items;
+  int const nblk_iter = push ? 0 : (int)adj.num_items;
   int const nblk_init = (int)grid_for(nv, kBlock, 1024);
   dbuf<double> partials(2 * std::max<int64_t>({nblk_iter, nblk_init, 2048, (nv + 4095) / 4096}), s);
   dbuf<pr_state> st(1, s);
@@ -1931,8 +2410,8 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   a.off      = adj.offsets.data<E>();
   a.idx      = adj.indices.data<V>();
   a.wgt      = g.weighted ? adj.weights.data<R>() : nullptr;
-  a.order    = adj.degree_sorted ? nullptr : adj.order.data<V>();
-  a.items    = adj.items.data<work_item>();
+  a.order    = push || adj.degree_sorted ? nullptr : adj.order.data<V>();
+  a.items    = push ? nullptr : adj.items.data<work_item>();
   a.pr       = pr;
   a.outw     = outw;
   a.pers     = pers.data();
@@ -1946,12 +2425,6 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
   a.x_in     = nullptr;
   a.x_out    = xa.data();
 
-  // windowed push (our own out-weight sums keep every fixed-point sum <= 1; user
-  // precomputed out-weights may not: generic pull kernel then)
-  bool push = pow_v == nullptr && max_iter > 0;
-  bool const push_w = g.weighted && !(push && unit_weights<R>(h, g, adj));  // entry weights in the push
-  if (push && !adj.pr.built) build_pr_push_schedule<V, E, R>(h, g, adj, push_w);
-  push = push && adj.pr.ok;
   // fp32 packed push: x~ as enc_fixed words (tuning_t::pr_enc = 0: plain floats, A/B)
   a.enc  = push && adj.pr.packed && std::is_same<R, float>::value && h.tune.pr_enc;
   a.fp64 = push ? 0 : 1;

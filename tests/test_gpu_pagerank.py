@@ -378,6 +378,53 @@ def test_fused_apply_bitwise_equal(graph):
         assert (np.abs(got[:n] - ref) / ref).max() < REL
 
 
+@pytest.mark.parametrize("scale,wb", [(12, 14), (20, 14), (20, 0), (18, 12)])
+def test_fast_symmetric_build_bitwise_equal(scale, wb):
+    """The one-word-key schedule build of symmetric unweighted graphs (pagerank.hip
+    build_push_packed_sym: keys from the out-edge adjacency, a keys-only sort of the
+    window bits, units from the window starts) gives the same ranks and iteration
+    counts as the general build (option pr_fast_build = 0), with and without source
+    bands."""
+    s, d, _ = rmat_graph(scale, False, True)
+    out = []
+    for fast, cut in ((1, 0), (0, 0), (1, 4096), (0, 4096)):
+        h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True,
+                          options={"pr_win_bits": wb, "pr_fast_build": fast, "pr_band_cut": cut})
+        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        out.append((host(v), host(r), h.last_iterations()))
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+
+
+@pytest.mark.parametrize("graph", ["rmat20", "empty_windows", "star"])
+def test_banded_push_bitwise_equal(graph):
+    """Source bands (pagerank.hip banded_finish: every 16K window's entries split at a
+    source cut into two virtual windows, the stream and the queues band-major, a
+    window applied by the last of its items from its LDS and the other band's plane)
+    give the same bits and iteration count as the unbanded push, for cuts that put
+    most entries in either band, on the first (calibrating) and a later call."""
+    if graph == "rmat20":
+        s, d, _ = rmat_graph(20, False, True)
+        kw = dict(renumber=True, symmetric=True)
+    elif graph == "star":
+        s, d = _star_plus_ring(300_000)
+        kw = dict(renumber=True, symmetric=False)
+    else:
+        s, d, _ = _empty_window_graph()
+        kw = dict(renumber=False, symmetric=False)
+    out = []
+    for cut in (0, 64, 4096, 65536, 262144):
+        h, G = make_graph(s, d, None, transposed=True, **kw, options={"pr_win_bits": 14, "pr_band_cut": cut})
+        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        v2, r2 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert np.array_equal(host(r), host(r2)) and h.last_iterations() > 0
+        out.append((host(v), host(r), h.last_iterations()))
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+
+
 @pytest.mark.parametrize("graph", ["rmat12", "rmat20", "star"])
 def test_hub_lds_bitwise_equal(graph):
     """The 16K-window push that reads the hubs' x~ from LDS (pagerank.hip push_body16
