@@ -33,6 +33,8 @@
 #include "schedule.hpp"
 
 #include <rocprim/device/device_reduce_by_key.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -1501,6 +1503,25 @@ __global__ void k_jump_counts(uint64_t const* keys, int64_t ne, int64_t const* w
   }
 }
 
+// the same count as a scan input (k_jump_counts without the array: the scan reads the
+// keys and writes the prefix in one pass; position ne counts 0)
+struct jump_count_p {
+  uint64_t const* keys;
+  int64_t const* ws;
+  int64_t ne;
+  key_p kc;
+  uint32_t dmax, pmax;
+  __device__ __forceinline__ uint32_t operator()(int64_t k) const
+  {
+    if (k >= ne) return 0u;
+    uint64_t const key  = keys[k];
+    int64_t const w     = kc.win(key);
+    uint32_t const prev = k == ws[w] ? 0u : kc.src(keys[k - 1]);
+    uint32_t const D    = kc.src(key) - prev;
+    return D > dmax ? (D + pmax - 1) / pmax : 0u;
+  }
+};
+
 // real entry k at k + cm[k] (cm = inclusive prefix of the jump counts), its jumps
 // right before it
 __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t const* rows, int64_t ne,
@@ -1531,7 +1552,7 @@ __global__ void k_pack16(uint64_t const* keys, uint32_t const* vals, uint32_t co
 // the same from key_p keys (the slot in the key); cm a 32-bit prefix when the edges
 // are below 2^31 (no jump total can wrap it), else 64-bit
 template <typename CM>
-__global__ void k_pack16_p(uint64_t const* keys, int64_t ne, int64_t const* ws, uint32_t const* mj, CM const* cm,
+__global__ void k_pack16_p(uint64_t const* keys, int64_t ne, int64_t const* ws, CM const* cm,
                            unsigned long long const* pb, key_p kc, uint32_t pmax, uint16_t* ent16)
 {
   int const wb        = kc.wb;
@@ -1541,7 +1562,7 @@ __global__ void k_pack16_p(uint64_t const* keys, int64_t ne, int64_t const* ws, 
     int64_t const w     = kc.win(key);
     uint32_t const prev = k == ws[w] ? 0u : kc.src(keys[k - 1]);
     uint32_t const D    = kc.src(key) - prev;
-    uint32_t const m    = mj[k];
+    uint32_t const m    = (uint32_t)(cm[k] - cm[k - 1]);  // cm[-1] is the exclusive scan's 0
     int64_t const pos   = k + (int64_t)cm[k] + (int64_t)pb[w];
     uint32_t const slot = kc.slot(key);
     if (m == 0) {
@@ -1591,11 +1612,17 @@ __global__ void k_unit_counts(int64_t const* nws, int64_t nwin, uint32_t* cnt)
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w <= nwin; w += (int64_t)gridDim.x * blockDim.x)
     cnt[w] = w == nwin ? 0u : (uint32_t)((nws[w + 1] - nws[w] + kPushUnit - 1) / kPushUnit);
 }
-__global__ void k_units_direct(int64_t const* nws, int64_t nwin, uint32_t const* upos, push_unit* units)
+__global__ void k_units_direct(int64_t const* nws, int64_t nwin, uint32_t const* upos, int64_t nunits,
+                               push_unit* units)
 {
-  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwin; w += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t u = upos[w];
-    for (int64_t p = nws[w]; p < nws[w + 1]; p += kPushUnit) units[u++] = push_unit{p, 0, 0, w};
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < nunits; u += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nwin - 1;  // the last window whose units start at or before u
+    while (lo < hi) {
+      int64_t const mid = (lo + hi + 1) >> 1;
+      if ((int64_t)upos[mid] <= u) lo = mid;
+      else hi = mid - 1;
+    }
+    units[u] = push_unit{nws[lo] + (u - (int64_t)upos[lo]) * kPushUnit, 0, 0, lo};
   }
 }
 
@@ -1639,7 +1666,7 @@ __global__ void k_seg_bases(push_unit const* units, int64_t nunits, uint64_t con
         else hi = mid;
       }
       int64_t const k     = lo;
-      uint32_t const m    = mj[k];
+      uint32_t const m    = mj ? mj[k] : (uint32_t)(cm[k] - cm[k - 1]);  // no mj: cm[-1] is the scan's 0
       int64_t const w     = kc.win(keys[k]);
       int64_t const j     = p - (k + (int64_t)cm[k] + (int64_t)pb[w] - m);
       uint32_t const prev = k == ws[w] ? 0u : kc.src(keys[k - 1]);
@@ -2048,6 +2075,25 @@ bool unit_weights(handle_t& h, graph_t& g, adjacency_t& adj)
   return adj.unit_weights == 1;
 }
 
+// The window sort of the one-word keys: up to 10 window bits (RMAT-24 and below at
+// 16K windows) in ONE onesweep pass of 10 radix bits (1024-thread blocks, match
+// ranking, 8 keys a thread) -- 5.75 ms for 500M keys against 7.03 for the gfx950
+// default's two 8-bit passes (scripts/ubench/radix_bits.hip, profiles/r05/radix_bits.txt);
+// wider window fields keep the default (a 10-bit pass is slower there: 9.8 vs 7.1 ms
+// at 12 bits).
+using window_sort_10 = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+template <typename C>
+void sort_window_keys(rocprim::double_buffer<uint64_t>& db, int64_t ne, int shv, int vbits, hipStream_t s)
+{
+  size_t tmp = 0;
+  HIP_CHECK(rocprim::radix_sort_keys<C>(nullptr, tmp, db, (size_t)ne, shv, shv + vbits, s));
+  buffer t(tmp, s);
+  HIP_CHECK(rocprim::radix_sort_keys<C>(t.data(), tmp, db, (size_t)ne, shv, shv + vbits, s));
+}
+
 // The packed schedule of a symmetric unweighted graph straight from its adjacency
 // (build_push_from_coo's packed path with key_p keys; same stream, units, bases and
 // items bit for bit): one word per entry through a keys-only sort of the window bits,
@@ -2076,10 +2122,8 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
                          dim3(256), 0, s, off, idx, nv, ne, wb, shv, (uint32_t)band_cut, nwin_real, kbuf.data());
       CGX_LAUNCH_CHECK();
       rocprim::double_buffer<uint64_t> db(kbuf.data(), k2.data());
-      size_t tmp = 0;
-      HIP_CHECK(rocprim::radix_sort_keys(nullptr, tmp, db, (size_t)ne, shv, shv + vbits, s));
-      buffer t(tmp, s);
-      HIP_CHECK(rocprim::radix_sort_keys(t.data(), tmp, db, (size_t)ne, shv, shv + vbits, s));
+      if (vbits <= 10) sort_window_keys<window_sort_10>(db, ne, shv, vbits, s);
+      else sort_window_keys<rocprim::default_config>(db, ne, shv, vbits, s);
       if (db.current() != kbuf.data()) std::swap(kbuf, k2);
     }
   }
@@ -2088,14 +2132,15 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
   hipLaunchKernelGGL(k_win_starts<key_p>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, keys, ne, nwin,
                      ws.data(), kc);
   CGX_LAUNCH_CHECK();
-  dbuf<uint32_t> mj(ne + 1, s);
   dbuf<CM> ex(ne + 1, s);
-  if (ne)
-    hipLaunchKernelGGL(k_jump_counts<key_p>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys, ne,
-                       ws.data(), dmax, pmax, mj.data(), kc);
-  CGX_LAUNCH_CHECK();
-  fill<uint32_t>(mj.data() + ne, 1, 0u, s);
-  exclusive_scan<uint32_t, CM>(mj.data(), ex.data(), ne + 1, s);
+  {
+    auto jumps = rocprim::make_transform_iterator(rocprim::make_counting_iterator<int64_t>(0),
+                                                  jump_count_p{keys, ws.data(), ne, kc, dmax, pmax});
+    size_t tmp = 0;
+    HIP_CHECK(rocprim::exclusive_scan(nullptr, tmp, jumps, ex.data(), CM(0), (size_t)(ne + 1), rocprim::plus<CM>(), s));
+    buffer t(tmp, s);
+    HIP_CHECK(rocprim::exclusive_scan(t.data(), tmp, jumps, ex.data(), CM(0), (size_t)(ne + 1), rocprim::plus<CM>(), s));
+  }
   int64_t const total0 = ne + (int64_t)to_host(ex.data() + ne, 1, s)[0];
   CM const* cm         = ex.data() + 1;  // inclusive prefix
   dbuf<unsigned long long> pad(nwin + 1, s), pb(nwin + 1, s);
@@ -2127,7 +2172,7 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
   fill<uint16_t>(pp.ent16.data<uint16_t>(), (size_t)(total + kPushUnit), pad_code, s);
   if (ne)
     hipLaunchKernelGGL(k_pack16_p<CM>, dim3(grid_for(ne, kBlock, 16384)), dim3(kBlock), 0, s, keys, ne, ws.data(),
-                       mj.data(), cm, pb.data(), kc, pmax, pp.ent16.data<uint16_t>());
+                       cm, pb.data(), kc, pmax, pp.ent16.data<uint16_t>());
   CGX_LAUNCH_CHECK();
   dbuf<int64_t> nws(nwin + 1, s);
   hipLaunchKernelGGL(k_packed_win_starts<CM>, dim3(grid_for(nwin + 1, kBlock, 4096)), dim3(kBlock), 0, s, ws.data(),
@@ -2142,8 +2187,9 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
   pp.units.set_stream(s);
   pp.units.resize(std::max<int64_t>(nunits, 1) * sizeof(push_unit));
   push_unit* units = pp.units.data<push_unit>();
-  hipLaunchKernelGGL(k_units_direct, dim3(grid_for(nwin, 64, 4096)), dim3(64), 0, s, nws.data(), nwin, upos.data(),
-                     units);
+  if (nunits)
+    hipLaunchKernelGGL(k_units_direct, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, nws.data(), nwin,
+                       upos.data(), nunits, units);
   CGX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_unit_ends, dim3(grid_for(nunits, kBlock, 4096)), dim3(kBlock), 0, s, units, nunits, total);
   CGX_LAUNCH_CHECK();
@@ -2151,7 +2197,7 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
   pp.seg_base.resize(std::max<int64_t>(nunits * kSegsPerUnit, 1) * sizeof(uint32_t));
   if (nunits)
     hipLaunchKernelGGL((k_seg_bases<key_p, CM>), dim3(grid_for(nunits * kSegsPerUnit, kBlock, 16384)), dim3(kBlock), 0,
-                       s, units, nunits, keys, ne, ws.data(), mj.data(), cm, pb.data(), dmax, pmax,
+                       s, units, nunits, keys, ne, ws.data(), (uint32_t const*)nullptr, cm, pb.data(), dmax, pmax,
                        pp.seg_base.data<uint32_t>(), kc);
   CGX_LAUNCH_CHECK();
   pp.ent.release();
