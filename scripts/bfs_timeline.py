@@ -16,8 +16,9 @@ def short(n):
     return re.sub(r'<.*', '', n.split('(')[0].replace('void ', ''))[:32]
 
 
-f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
-rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+f = (glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True) + glob.glob(sys.argv[1] + "/**/*kernel_trace.csv.gz", recursive=True))[0]
+import gzip
+rows = sorted(csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)), key=lambda r: int(r["Start_Timestamp"]))
 ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Grid_Size_X"]) for r in rows]
 starts = [i for i, k in enumerate(ks) if k[2].startswith("k_bfs_setup")]
 n_last = int(sys.argv[2]) if len(sys.argv) > 2 else 3

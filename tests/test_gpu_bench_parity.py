@@ -355,15 +355,24 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
     * BFS from the largest hub: distances and predecessors equal.
     Results are kept on the host between the phases: RMAT-26 Louvain's level graphs
     take > 100 GB of the device."""
+    import time
     import torch
     bench, p = _bench()
     scale = 26
     n_ext = 1 << scale
+
+    def timed(f):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = f()
+        torch.cuda.synchronize()
+        return r, time.perf_counter() - t0
+
     print("device memory free/total GB at start", _free_device())
     # -- single GPU: Louvain on the weighted graph
     h = p.ResourceHandle()
     g, _, _ = bench.build_rmat_graph(p, h, scale, weighted=True, transposed=False)
-    v, c, q_sg = p.louvain(h, g, 100, 1.0, False)
+    (v, c, q_sg), t_lv_sg = timed(lambda: p.louvain(h, g, 100, 1.0, False))
     lv_sg = h.last_louvain_levels()
     sg_c = _by_ext(v, c, n_ext).cpu()
     del v, c
@@ -374,6 +383,7 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
     E = g.number_of_edges()
     v, x = p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False)
     it_sg = h.last_iterations()
+    _, t_pr_sg = timed(lambda: p.pagerank(h, g, None, None, None, None, 0.85, 1e-6, 500, False))  # steady call
     sg_x = _by_ext(v, x.view(torch.int32), n_ext).cpu()
     root = int(v[0])  # internal id 0: the largest degree
     d, pr, vb = p.bfs(h, g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
@@ -386,7 +396,7 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
     with _OneRankRccl() as rc:
         hm = p.ResourceHandle(rc.ctx.ptr)
         gm, _, _ = bench.build_rmat_graph(p, hm, scale, weighted=True, transposed=False, mg=(0, 1))
-        vm, cm, q_mg = p.louvain(hm, gm, 100, 1.0, False)
+        (vm, cm, q_mg), t_lv_mg = timed(lambda: p.louvain(hm, gm, 100, 1.0, False))
         assert hm.last_louvain_levels() == lv_sg
         assert q_mg == q_sg, (q_mg, q_sg)
         ids = vm.cpu().to(torch.int64)
@@ -400,12 +410,16 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
         assert hm.last_iterations() == it_sg
         assert torch.equal(xm.view(torch.int32).cpu().to(torch.int64), sg_x[vm.cpu().to(torch.int64)]), \
             "MG PageRank differs from SG at RMAT-26"
+        _, t_pr_mg = timed(lambda: p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False))
         dm, pm, vmb = p.bfs(hm, gm, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
         ids = vmb.cpu().to(torch.int64)
         assert torch.equal(dm.cpu().to(torch.int64), sg_d[ids]), "MG BFS distances differ from SG at RMAT-26"
         assert torch.equal(pm.cpu().to(torch.int64), sg_p[ids]), "MG BFS predecessors differ from SG at RMAT-26"
         print(f"RMAT-26 one-rank RCCL MG == SG: PageRank {it_sg} iterations, BFS from {root}, "
               f"Louvain Q {q_sg:.9f} in {lv_sg} levels")
+        # the one-rank MG path's cost over SG (steady PageRank call; Louvain end to end)
+        print(f"RMAT-26 MG/SG time: PageRank {t_pr_mg / t_pr_sg:.3f} ({1e3 * t_pr_mg:.2f} / {1e3 * t_pr_sg:.2f} ms), "
+              f"Louvain {t_lv_mg / t_lv_sg:.3f} ({t_lv_mg:.2f} / {t_lv_sg:.2f} s)")
         del vm, xm, dm, pm, vmb
         gm = None
         hm = None
