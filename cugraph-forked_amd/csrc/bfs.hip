@@ -151,6 +151,12 @@ __global__ void k_publish_seq(bfs_ctr* ctr, bfs_ctr_hdr* host, unsigned long lon
   // reads is in it; the next kernels are stream-ordered behind this one anyway).  A
   // system-scope release there (its L2 write-back) measured 0.674-0.675 against
   // 0.667-0.669 ms per RMAT-24 traversal, same box.
+  // (gfx9 family only: there vmcnt counts stores as well as loads; gfx10+ counts
+  // stores in vscnt, and this wait would not order them -- the build rejects it below.
+  // It also relies on handle_t::polled_as staying fine-grained coherent memory.)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "k_publish_seq orders its stores with s_waitcnt vmcnt(0): gfx9-family (gfx950) targets only"
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (i != 0) return;
   __hip_atomic_store(&host->pad[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -795,6 +801,7 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
 #define CGX_BFS_RES_W 16
 #endif
   constexpr int w = CGX_BFS_RES_W;
+  static_assert(w >= 2 && w <= 32 && (w & (w - 1)) == 0, "residual group width: a power of two in [2, 32]");
   V const nd       = (V)(a.depth + 1);
   int const tid    = threadIdx.x;
   int const lane   = tid & (w - 1);
@@ -1085,12 +1092,20 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
     // (40, 64) 226K; (80, 64) 223K; (80, 128) 225K; (150, 64) 209K.
     // tuning_t overrides are measurement only.
     double const beta_do  = tu.bfs_beta;
+    // The switch rule, in one place: the direction of the level whose frontier has n_f
+    // vertices and m_f edges (m_u unexplored edges) after a level run bottom-up (cur_bu)
+    // or top-down.  Also the "next level is bottom-up" test after a top-down level,
+    // which decides which kernel turns that level's predecessors into external ids
+    // (k_mark_queues now, or k_frontier_from_dist / k_mark_queues at the next level's
+    // conversion) -- so both uses must agree, and they do by calling this.
+    auto next_dir_bu = [&](bool cur_bu, unsigned long long nf, unsigned long long mf, unsigned long long mu) {
+      if (!dir_opt) return false;
+      if (!cur_bu) return (double)mf > (double)mu / alpha_do;
+      return !((double)nf < (double)nv / beta_do);
+    };
     while (n_f > 0 && depth < limit) {
       auto tl = std::chrono::steady_clock::now();
-      if (dir_opt) {
-        if (!bottom_up && (double)m_f > (double)m_u / alpha_do) bottom_up = true;
-        else if (bottom_up && (double)n_f < (double)nv / beta_do) bottom_up = false;
-      }
+      bottom_up = next_dir_bu(bottom_up, n_f, m_f, m_u);
       a.depth = depth;  // (k_publish_seq zeroed the counters it read)
       if (bottom_up) {
         if (!have_bitmap) {  // queues -> frontier bitmap (fr is all zero here)
@@ -1265,7 +1280,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
             break;
           }
           unsigned long long const m_u_next = m_u > m_f ? m_u - m_f : 0;
-          bool const next_bu = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
+          bool const next_bu = next_dir_bu(false, n_f, m_f, m_u_next);
           bool const last    = n_f == 0 || depth + 1 >= limit;
           if (!last && !next_bu) {
             hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s,
@@ -1296,7 +1311,7 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
         // next bottom-up level marks them with its frontier bitmap (queues -> bitmap
         // above), and after the last level nothing reads them
         unsigned long long const m_u_next = m_u > m_f ? m_u - m_f : 0;
-        bool const next_bu   = dir_opt && (double)m_f > (double)m_u_next / alpha_do;
+        bool const next_bu   = next_dir_bu(false, n_f, m_f, m_u_next);
         bool const last      = n_f == 0 || depth + 1 >= limit;
         if (!last && !next_bu) {
           hipLaunchKernelGGL(k_mark_queues<V>, dim3(grid_for(n_f, kBlock, 4096)), dim3(kBlock), 0, s, qb[0].data(),

@@ -85,6 +85,8 @@ struct handle_t {
   }
   // Coherent (fine-grained) pinned block the host polls while the stream runs on:
   // a kernel publishes values and then a sequence number with system-scope stores.
+  // It must stay hipHostMallocCoherent (uncached): bfs.hip k_publish_seq orders the
+  // words before the sequence number with a vmcnt wait only, no release.
   void* polled = nullptr;
   template <typename T>
   T* polled_as()
@@ -201,7 +203,10 @@ struct adjacency_t {
   std::vector<int64_t> bin_begin;       // positions (in processing order) where each bin starts
   buffer items;                         // work items for the SpMV-like kernels
   int64_t num_items = 0;
-  buffer bfs_head;  // BFS bottom-up probe: 32 B per vertex (bfs.hip k_bfs_head), built on first use
+  // BFS bottom-up probe's head table: 16 B per vertex (16 * kHeadQ, bfs.hip k_bfs_head; RMAT-24 142 MB),
+  // built on the first direction-optimising BFS and kept for the adjacency's lifetime like pr and
+  // items (freed with the graph; trim_device_cache returns only the allocator's free blocks)
+  buffer bfs_head;
   pr_push_t pr;  // PageRank windowed-push schedule (pagerank.hip), built on first use
 };
 

@@ -40,6 +40,13 @@
 #include <cmath>
 #include <cstdlib>
 
+// Stores and atomics are ordered before hand-offs (the iteration state's host words,
+// the fused finish's counters) by s_waitcnt vmcnt(0) alone: vmcnt counts stores only on
+// the gfx9 family (gfx10+ counts them in vscnt), so the build is gfx9-only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "s_waitcnt vmcnt(0) orders stores on gfx9-family (gfx950) targets only"
+#endif
+
 namespace cgx {
 
 struct pr_state {
