@@ -29,7 +29,8 @@ struct mg_context;  // comm.hpp (multi-GPU); nullptr for single GPU
 // Schedule-time switches (pr_win_bits, pr_packed, pr_whole) apply to schedules built
 // after they are set: the push schedule is cached on the graph.
 struct tuning_t {
-  int pr_win_bits      = 0;     // 0: by size (push_win_bits); 12 / 13 / 14 force 4K / 8K / 16K windows
+  int pr_win_bits      = 0;     // 0: by size (push_win_bits); 12 / 13 / 14 / 15 force 4K / 8K / 16K / 32K windows
+                                // (15: single-GPU symmetric unweighted schedules only, else 14)
   bool pr_packed       = true;  // 16-bit entries for unweighted graphs (else 32-bit)
   bool pr_whole        = true;  // windows summed by one item are stored, not added
   bool pr_calib        = true;  // measured-cost queues after the first launch
@@ -39,6 +40,8 @@ struct tuning_t {
   bool pr_enc          = true;  // x~ as fixed-point words (fp32 single GPU)
   bool pr_hub          = true;  // hub x~ staged in LDS (16K windows)
   int64_t pr_band_cut  = -1;    // banded push source cut (-1: by size, 0: no bands)
+  int pr_share_div     = 0;     // items per push block on average (0: kShareDiv); windows above 1.5x are shared
+  bool pr_carry_check  = true;  // 32K push: returning LDS adds + carries (0: measurement only, wrong sums)
   bool pr_fast_build   = true;  // symmetric unweighted schedules through one-word keys (else the general build)
   int mg_chunks        = 0;     // MG overlap chunks (0: by size)
   double bfs_alpha     = 40.0;  // direction switch (Beamer's alpha / beta)
@@ -184,6 +187,7 @@ struct pr_push_t {
   bool bands = false;
   int64_t nwin_real = 0;  // real windows (nwin counts the virtual ones)
   buffer win_pub;         // uint32[nwin_real]: items of the window that published this iteration
+  buffer carry;           // uint32[nacc]: 32K windows' carry words (push_args::carry), zero between iterations
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).

@@ -516,8 +516,8 @@ extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t
     auto b   = [&](bool& f) { f = value != 0.0; };
     auto i32 = [&](int& f) { f = (int)value; };
     if (n == "pr_win_bits") {
-      CGX_INPUT(value == 0 || value == 12 || value == 13 || value == 14,
-                "Invalid input argument: pr_win_bits must be 0, 12, 13 or 14");
+      CGX_INPUT(value == 0 || value == 12 || value == 13 || value == 14 || value == 15,
+                "Invalid input argument: pr_win_bits must be 0, 12, 13, 14 or 15");
       i32(t.pr_win_bits);
     } else if (n == "pr_packed") b(t.pr_packed);
     else if (n == "pr_whole") b(t.pr_whole);
@@ -529,6 +529,8 @@ extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t
     else if (n == "pr_hub") b(t.pr_hub);
     else if (n == "pr_band_cut") t.pr_band_cut = (int64_t)value;
     else if (n == "pr_fast_build") b(t.pr_fast_build);
+    else if (n == "pr_carry_check") b(t.pr_carry_check);
+    else if (n == "pr_share_div") i32(t.pr_share_div);
     else if (n == "mg_chunks") i32(t.mg_chunks);
     else if (n == "bfs_alpha") t.bfs_alpha = value;
     else if (n == "bfs_beta") t.bfs_beta = value;

@@ -25,8 +25,9 @@
 //     path sweep_sorted -- key = row << cb | cluster(destination), radix sort,
 //     reduce_by_key to (row, cluster, sum), gains, reduce_by_key over the row
 //     (also the A/B switch CGX_LOUVAIN_HASH=0).
-// Ties go to the smaller cluster id in every path.  Cluster weights are a
-// reduce_by_key over vertices sorted by cluster; the modularity's internal weight
+// Ties go to the smaller cluster id in every path.  Cluster weights are 64-bit
+// fixed-point totals updated by each sweep's moves (as the multi-GPU owners keep
+// them); the modularity's internal weight
 // comes from the sweep's own-cluster sums.  The run is deterministic.
 #include "capi.hpp"
 #include "comm.hpp"
@@ -187,19 +188,6 @@ __global__ void k_move(uint32_t const* uu, gain_t const* best, int64_t n, uint32
     gain_t b   = best[i];
     if (b.dq > 0.0 && ((b.c > c[u + base]) == up_down)) next[u] = b.c;
   }
-}
-
-__global__ void k_scatter_cluster_weights(uint32_t const* ck, double const* cw, int64_t n, double* a)
-{
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    a[ck[i]] = cw[i];
-}
-
-// rows v with edges mark their cluster c[v] (c points at the rows' clusters)
-__global__ void k_mark_present(uint32_t const* c, uint8_t const* has_edges, int64_t nv, uint8_t* present)
-{
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x)
-    if (has_edges[v]) present[c[v]] = 1;
 }
 
 struct sumsq_f {
@@ -1318,36 +1306,6 @@ double modularity_own(louvain_state& S, level_graph const& g, double const* own,
   return hv[0] / S.m - (S.gamma * hv[1]) / (S.m * S.m);
 }
 
-// cluster weights a[c] = sum of k[v] over v in c; present[c] = some v in c has
-// edges.  a and present are indexed by cluster id (all nv ids); k and has_edges by
-// row.  Multi-GPU: per-rank partial sums, then a SUM / MAX allreduce.
-void cluster_weights(louvain_state& S, level_graph const& g, uint32_t const* c, double const* k,
-                     uint8_t const* has_edges, double* a, uint8_t* present)
-{
-  hipStream_t s = S.s;
-  int64_t nv = g.nv, nr = g.nrows;
-  fill<double>(a, nv, 0.0, s);
-  fill<uint8_t>(present, nv, 0, s);
-  if (nr > 0) {
-    dbuf<uint32_t> ck(nr, s), ck2(nr, s);
-    dbuf<double> kv2(nr, s);
-    HIP_CHECK(hipMemcpyAsync(ck.data(), c + g.base, nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    radix_sort_pairs<uint32_t, double>(ck.data(), ck2.data(), k, kv2.data(), (size_t)nr, 0, bits_for(nv - 1), s);
-    dbuf<uint32_t> uk(nr, s);
-    dbuf<double> uw(nr, s);
-    int64_t nu = reduce_by_key(ck2.data(), kv2.data(), (size_t)nr, uk.data(), uw.data(), rocprim::plus<double>(),
-                               rocprim::equal_to<uint32_t>(), s);
-    hipLaunchKernelGGL(k_scatter_cluster_weights, dim3(blocks(nu)), dim3(kBlock), 0, s, uk.data(), uw.data(), nu, a);
-    CGX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_mark_present, dim3(blocks(nr)), dim3(kBlock), 0, s, c + g.base, has_edges, nr, present);
-    CGX_LAUNCH_CHECK();
-  }
-  if (S.comm) {
-    S.comm->allreduce<double>(a, a, (size_t)nv, CGX_COMM_SUM, s);
-    S.comm->allreduce<uint8_t>(present, present, (size_t)nv, CGX_COMM_MAX, s);
-  }
-}
-
 // the sort-based local move over the edges (src, dst, w)[0, ne) of some of the
 // rows (whole rows only): next[row] is written for the rows that move
 void sweep_sorted(louvain_state& S, level_graph const& g, uint32_t const* src, uint32_t const* dst, double const* w,
@@ -1696,6 +1654,42 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
   }
 }
 
+// fixed-point vertex weights of the rows: K = rint(k * scale)
+__global__ void k_to_fixed(double const* k, int64_t n, double scale, long long* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = __double2ll_rn(k[i] * scale);
+}
+
+// the sweep's cluster weights and present flags from the owners' answers
+__global__ void k_cluster_vals(long long const* afix, int const* pcnt, int64_t n, double inv, int all_present,
+                               double* a, uint8_t* present)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    a[i]       = (double)afix[i] * inv;
+    present[i] = (all_present || pcnt[i] > 0) ? 1 : 0;
+  }
+}
+
+// single GPU: the moves' fixed-point weight deltas (every moved vertex takes its K
+// and its has-edges count from the old cluster to the new one; integer adds, so the
+// totals do not depend on the order of the atomics)
+__global__ void k_apply_moves(uint32_t const* old_c, uint32_t const* new_c, int64_t n, long long const* kfix,
+                              uint8_t const* has_edges, long long* afix, int* pcnt)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const o = old_c[v], c = new_c[v];
+    if (o == c) continue;
+    unsigned long long const kv = (unsigned long long)kfix[v];
+    atomicAdd(reinterpret_cast<unsigned long long*>(afix + o), 0ull - kv);
+    atomicAdd(reinterpret_cast<unsigned long long*>(afix + c), kv);
+    if (has_edges[v]) {
+      atomicSub(pcnt + o, 1);
+      atomicAdd(pcnt + c, 1);
+    }
+  }
+}
+
 // contract the level graph by `labels` (graph_contraction / coarsen_graph): sum
 // parallel edges, renumber the used labels by descending coarse out-degree
 // (stable: ties by ascending label), relabel the dendrogram level in place
@@ -1815,8 +1809,23 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     dbuf<uint8_t> has_edges(nv, s), present(nv, s);
     dbuf<u64> vstats(2, s);
     vertex_weights(S, cur, off.data(), k.data(), self.data(), has_edges.data(), vstats.data());
-    HIP_CHECK(hipMemcpyAsync(a.data(), k.data(), nv * sizeof(double), hipMemcpyDeviceToDevice, s));
-    fill<uint8_t>(present.data(), nv, 1, s);
+    // Cluster weights in 64-bit fixed point, as the multi-GPU owners keep them (scale
+    // 2^(60 - e), the total weight < 2^e): every move adds its vertex's K to the new
+    // cluster and takes it from the old one (k_apply_moves), integer adds that give
+    // the same totals in any order -- one pass over the vertices per sweep where the
+    // re-summation sorted every vertex by cluster (~0.3 ms a sweep at RMAT-23).  a and
+    // present are read off them; the first sweep sees every vertex present.
+    int const ea        = S.m > 0 ? std::ilogb(S.m) + 1 : 0;
+    double const ascale = std::ldexp(1.0, 60 - ea), ainv = std::ldexp(1.0, ea - 60);
+    dbuf<long long> kfix(nv, s), afix(nv, s);
+    dbuf<int> pcnt(nv, s);
+    hipLaunchKernelGGL(k_to_fixed, dim3(blocks(nv)), dim3(kBlock), 0, s, k.data(), nv, ascale, kfix.data());
+    CGX_LAUNCH_CHECK();
+    HIP_CHECK(hipMemcpyAsync(afix.data(), kfix.data(), nv * sizeof(long long), hipMemcpyDeviceToDevice, s));
+    convert<int, uint8_t>(pcnt.data(), has_edges.data(), nv, s);
+    hipLaunchKernelGGL(k_cluster_vals, dim3(blocks(nv)), dim3(kBlock), 0, s, afix.data(), pcnt.data(), nv, ainv, 1,
+                       a.data(), present.data());
+    CGX_LAUNCH_CHECK();
     dbuf<uint32_t> clusters(nv, s), next(nv, s);
     iota<uint32_t>(clusters.data(), nv, 0u, s);
     sweep_plan plan;
@@ -1832,8 +1841,13 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     double cur_q = new_q - 1.0;
     while (new_q > cur_q + 0.0001) {
       cur_q = new_q;
+      hipLaunchKernelGGL(k_apply_moves, dim3(blocks(nv)), dim3(kBlock), 0, s, clusters.data(), next.data(), nv,
+                         kfix.data(), has_edges.data(), afix.data(), pcnt.data());
+      CGX_LAUNCH_CHECK();
       std::swap(clusters, next);
-      cluster_weights(S, cur, clusters.data(), k.data(), has_edges.data(), a.data(), present.data());
+      hipLaunchKernelGGL(k_cluster_vals, dim3(blocks(nv)), dim3(kBlock), 0, s, afix.data(), pcnt.data(), nv, ainv, 0,
+                         a.data(), present.data());
+      CGX_LAUNCH_CHECK();
       up_down = !up_down;
       sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down,
             own.data());
@@ -1847,6 +1861,9 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     // the level's sweep state goes before the contraction's sort buffers are allocated
     plan = sweep_plan{};
     for (auto* b : {&own, &k, &self, &a}) b->free();
+    kfix.free();
+    afix.free();
+    pcnt.free();
     for (auto* b : {&clusters, &next}) b->free();
     has_edges.free();
     present.free();
@@ -2137,23 +2154,6 @@ __global__ void k_sub_u32(uint32_t* x, int64_t n, uint32_t lo)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     x[i] -= lo;
-}
-
-// fixed-point vertex weights of the rows: K = rint(k * scale)
-__global__ void k_to_fixed(double const* k, int64_t n, double scale, long long* out)
-{
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = __double2ll_rn(k[i] * scale);
-}
-
-// the sweep's cluster weights and present flags from the owners' answers
-__global__ void k_cluster_vals(long long const* afix, int const* pcnt, int64_t n, double inv, int all_present,
-                               double* a, uint8_t* present)
-{
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    a[i]       = (double)afix[i] * inv;
-    present[i] = (all_present || pcnt[i] > 0) ? 1 : 0;
-  }
 }
 
 // sum over the owned cluster ids of a_c^2 (present clusters only)

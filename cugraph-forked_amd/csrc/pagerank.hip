@@ -99,10 +99,10 @@ struct pr_args {
   int fp64;         // (diff, dangling) summed in fp64 (the pull path: user out-weights bound no sum)
 };
 
-// x~ as the push consumes it: the 64-bit fixed-point value RNE(x * 2^62) of an fp32
+// x~ as the push consumes it: the 64-bit fixed-point value RNE(x * 2^52) of an fp32
 // x in [0, 1] written as one 32-bit word, significand M (24 bits) | shift s << 24,
-// value = M << s.  x = M * 2^(eb - 150) for the biased exponent eb, so s = eb - 88
-// for x >= 2^-39 (exact); smaller x are rounded to nearest-even here, once per
+// value = M << s.  x = M * 2^(eb - 150) for the biased exponent eb, so s = eb - 98
+// for x >= 2^-29 (exact); smaller x are rounded to nearest-even here, once per
 // vertex, and stored with s = 0.  The push then converts with an and, a shift and
 // a 64-bit shift instead of the 7-op fp32 sequence per entry (to_fixed_f32), with
 // the same bits.
@@ -111,9 +111,9 @@ __device__ __forceinline__ uint32_t enc_fixed(float x)
   uint32_t const b  = __float_as_uint(x);
   uint32_t const eb = b >> 23;  // x >= 0
   uint32_t const m  = (b & 0x7fffffu) | 0x800000u;
-  if (eb >= 88u) return ((eb - 88u) << 24) | m;
+  if (eb >= 98u) return ((eb - 98u) << 24) | m;
   if (eb == 0u) return 0u;  // denormal or zero: below 2^-126, rounds to 0
-  uint32_t const k = 88u - eb;
+  uint32_t const k = 98u - eb;
   if (k > 24u) return 0u;  // m / 2^k < 1/2
   uint32_t const q    = m >> k;
   uint32_t const r    = m & ((1u << k) - 1u);
@@ -438,10 +438,13 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 //    x~ lines one gathers are in that XCD's L2 for the others: an offline LRU
 //    model of the 8 L2s (RMAT-24) gives 12.9M x~ misses per iteration against
 //    22.4M for one queue of 8-unit tiles;
-//  * sums are 64-bit fixed point (scale 2^62; every destination's sum is at most
+//  * sums are 64-bit fixed point (scale 2^52; every destination's sum is at most
 //    the total rank mass 1 since x~[u] w(u, v) summed over v is pr[u]).  Integer
 //    addition is associative: the result is bitwise deterministic whatever the
-//    order of the atomics.
+//    order of the atomics.  2^52 (2^62 until round 5) keeps a typical contribution
+//    (x~ ~ 2^-27 at RMAT-24) well below 2^32, so the 32K-destination windows can sum
+//    in 32-bit LDS words with rare carries (push_body16, WB = 15); the resolution
+//    2^-52 is about half an fp32 ulp of the smallest rank, (1 - alpha) / V, at RMAT-26.
 //
 // Ids descend by degree, so a window of low-degree destinations draws its sources
 // mostly from the hubs (few x~ lines); measured alternative: windows dealt runs of
@@ -468,8 +471,8 @@ constexpr int kHubBytes = 32768 - 512;
 #ifndef CGX_APPLY_BATCH
 #define CGX_APPLY_BATCH 4
 #endif
-constexpr double kFixScale    = 4611686018427387904.0;  // 2^62
-constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
+constexpr double kFixScale    = 4503599627370496.0;  // 2^52
+constexpr double kFixScaleInv = 1.0 / 4503599627370496.0;
 
 // Window bits: about 500-600 windows measured best -- fewer x~ line visits per
 // entry as windows grow, against the load balance of few windows.  14 (16K
@@ -478,9 +481,17 @@ constexpr double kFixScaleInv = 1.0 / 4611686018427387904.0;
 // 13 (8K, 64 KB, two blocks per CU) from 2^22, 12 below (RMAT-22, 586 windows:
 // 0.181 ms against 0.199 with 13 and 0.219 with 14).  tuning_t::pr_win_bits
 // overrides (12, 13 or 14).
-inline int push_win_bits(int64_t n_rows, tuning_t const& tu)
+// wide: the caller's schedule can take 32K windows (15: single GPU, packed entries --
+// the symmetric unweighted build), else 15 falls back to 14.  32K windows from 2^24
+// rows: RMAT-26 2.84 vs 2.98 ms/iteration, but RMAT-24 0.70 vs 0.58 (same box,
+// gpurun_out/r05q): 21 % fewer L1->L2 requests, yet as many L2 misses (fewer windows
+// in flight per XCD share fewer lines) and the carry check's returning LDS adds cost
+// 0.085 ms (0.619 without them, wrong sums).
+inline int push_win_bits(int64_t n_rows, tuning_t const& tu, bool wide = false)
 {
   if (tu.pr_win_bits == 12 || tu.pr_win_bits == 13 || tu.pr_win_bits == 14) return tu.pr_win_bits;
+  if (tu.pr_win_bits == 15) return wide ? 15 : 14;
+  if (n_rows >= (int64_t(1) << 24)) return wide ? 15 : 14;
   return n_rows >= (int64_t(1) << 23) ? 14 : n_rows >= (int64_t(1) << 22) ? 13 : 12;
 }
 
@@ -518,6 +529,11 @@ struct push_args {
   push_unit const* units;
   int64_t nunits;
   unsigned long long* acc;  // [n_rows] fixed-point sums, zero between iterations
+  int acc32_nocheck;        // measurement only (tuning_t::pr_carry_check = 0): the 32K push's LDS adds
+                            // without returns -- wrong sums once a word wraps; timing A/B
+  uint32_t* carry;          // 32K windows (WB = 15): per destination, 2^32 units of its sum that the
+                            // 32-bit LDS words carried out (and high words of large terms); zero
+                            // between iterations, read and cleared with the sums; else nullptr
   int64_t const* items;     // first unit of every item, nitems + 1 entries
   int64_t const* queue;     // item ids, queue by queue
   int64_t qoff[kQueues + 1];
@@ -560,15 +576,15 @@ __device__ __forceinline__ unsigned long long to_fixed(double v)
   return (unsigned long long)__double2ll_rn(v * kFixScale);
 }
 
-// The same value, round-to-nearest-even(x * 2^62), for an fp32 x in [0, 1) in fp32
+// The same value, round-to-nearest-even(x * 2^52), for an fp32 x in [0, 1) in fp32
 // arithmetic only: the fp64 sequence (cvt, 2 ldexp, rndne, floor, fma, 2 cvt) was
 // most of the push's VALU issue time (SQ_ACTIVE_INST_ANY at ~75 % of the waves'
-// cycles, RMAT-24).  y = x * 2^30 and its fraction are exact in fp32; the fraction's
-// significant bits then sit at 2^-32 .. 2^-62 of x, so rint(frac * 2^32) rounds
-// exactly where __double2ll_rn does and never reaches 2^32 (24-bit significands).
+// cycles, RMAT-24).  y = x * 2^20 and its fraction are exact in fp32; the fraction
+// times 2^32 is the fixed-point value's low word before rounding, so rint(frac * 2^32)
+// rounds exactly where __double2ll_rn does and never reaches 2^32 (24-bit significands).
 __device__ __forceinline__ unsigned long long to_fixed_f32(float x)
 {
-  float const y     = x * 1073741824.0f;  // 2^30
+  float const y     = x * 1048576.0f;  // 2^20
   uint32_t const hi = (uint32_t)y;
   float const fr    = y - (float)hi;
   uint32_t const lo = (uint32_t)__builtin_rintf(fr * 4294967296.0f);  // 2^32
@@ -590,22 +606,22 @@ constexpr int64_t kWinMask   = kWholeItem - 1;
 
 // add the LDS window to the global accumulators (or store it: the item is the
 // whole window) and clear it
-template <int WB, typename V, typename E, typename R>
-__device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
+template <int WB, typename V, typename E, typename R, typename A>
+__device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, A* acc, int64_t win_w)
 {
   __syncthreads();
   unsigned long long* g = sa.acc + ((win_w & kWinMask) << WB);
   if (win_w & kWholeItem) {
     for (int i = threadIdx.x; i < (1 << WB); i += kPushThreads) {
-      g[i]   = acc[i];
-      acc[i] = 0ull;
+      g[i]   = (unsigned long long)acc[i];
+      acc[i] = 0;
     }
   } else {
     for (int i = threadIdx.x; i < (1 << WB); i += kPushThreads) {
-      unsigned long long v = acc[i];
+      unsigned long long v = (unsigned long long)acc[i];
       if (v) {
         atomicAdd(g + i, v);
-        acc[i] = 0ull;
+        acc[i] = 0;
       }
     }
   }
@@ -634,8 +650,8 @@ __device__ __forceinline__ void flush_window(push_args<V, E, R> const& sa, unsig
 // (pr / x~' / the queue heads of the other parity are read by the next launch).
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <int WB, typename V, typename E, typename R>
-__device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64_t w, unsigned long long* lds,
+template <int WB, typename V, typename E, typename R, typename A>
+__device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64_t w, A* lds,
                                              unsigned long long& my_diff, unsigned long long& my_dang)
 {
   auto const& a     = sa.a;
@@ -654,11 +670,14 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
       int const i = i0 + j * kPushThreads;
       if (i < n) {
         if (lds) {
-          f[j]   = lds[i];
-          lds[i] = 0ull;
+          f[j]   = (unsigned long long)lds[i];
+          lds[i] = 0;
         } else {  // read and zero for the next iteration, at the coherence point
           f[j] = __hip_atomic_exchange(sa.acc + v0 + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if constexpr (WB == 15)  // the 32-bit LDS words' carries (push_body16)
+          f[j] += (unsigned long long)__hip_atomic_exchange(sa.carry + v0 + i, 0u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT) << 32;
         old[j] = a.pr[v0 + i];
         ow[j]  = a.outw[v0 + i];
       }
@@ -787,8 +806,8 @@ __device__ __forceinline__ bool banded_finish(push_args<V, E, R> const& sa, unsi
   return true;
 }
 
-template <int WB, typename V, typename E, typename R, bool BANDS = false>
-__device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
+template <int WB, typename V, typename E, typename R, bool BANDS = false, typename A>
+__device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, A* acc, int64_t win_w)
 {
   __shared__ unsigned long long s_red[kPushThreads / 64];
   __shared__ int s_flag;
@@ -803,10 +822,10 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
   if (!whole) {
     unsigned long long* g = sa.acc + (w << WB);
     for (int i = tid; i < (1 << WB); i += kPushThreads) {
-      unsigned long long const v = acc[i];
+      unsigned long long const v = (unsigned long long)acc[i];
       if (v) {
         __hip_atomic_fetch_add(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[i] = 0ull;
+        acc[i] = 0;
       }
     }
     wait_vmem();  // this thread's adds are performed before the item is counted off
@@ -834,7 +853,7 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
   my_diff = my_dang = 0;
   for (int64_t k = 0; k < sa.nempty; ++k) {
     if constexpr (BANDS) apply_window_banded<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, -1, my_diff, my_dang);
-    else apply_window<WB, V, E, R>(sa, sa.empty_wins[k], nullptr, my_diff, my_dang);
+    else apply_window<WB, V, E, R>(sa, sa.empty_wins[k], (A*)nullptr, my_diff, my_dang);
   }
   unsigned long long const ed = block_sum_u64<kPushThreads>(my_diff, s_red);
   unsigned long long const eg = block_sum_u64<kPushThreads>(my_dang, s_red);
@@ -859,8 +878,8 @@ __device__ __forceinline__ void fused_finish(push_args<V, E, R> const& sa, unsig
 // kernel has the fused finish (16K windows only, decided at run time by sa.fuse).  In
 // the 64-VGPR kernels of 4K / 8K windows its code costs 140-156 B of scratch per lane:
 // measured on RMAT-22, 0.274 against 0.176 ms/iteration unfused (same box)
-template <int WB, typename V, typename E, typename R, bool FUSE, bool BANDS = false>
-__device__ __forceinline__ void end_item(push_args<V, E, R> const& sa, unsigned long long* acc, int64_t win_w)
+template <int WB, typename V, typename E, typename R, bool FUSE, bool BANDS = false, typename A>
+__device__ __forceinline__ void end_item(push_args<V, E, R> const& sa, A* acc, int64_t win_w)
 {
   if constexpr (BANDS) {  // (a banded schedule is always fused)
     fused_finish<WB, V, E, R, true>(sa, acc, win_w);
@@ -1055,7 +1074,11 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   constexpr uint32_t kLow   = (1u << WB) - 1;
   constexpr int kRows       = kSegEntries / 64;
   static_assert(kRows == kPerThread, "a wave segment is one unit row per thread");
-  __shared__ unsigned long long acc[kWin];
+  // 32K-destination windows (WB = 15) sum in 32-bit LDS words: 128 KB like the 16K
+  // windows' 64-bit words, so the 16K-source hub table still fits beside them
+  constexpr bool kAcc32 = WB == 15;
+  using acc_t           = typename std::conditional<kAcc32, uint32_t, unsigned long long>::type;
+  __shared__ acc_t acc[kWin];
   constexpr int kHub = HUB ? kHubBytes / (int)sizeof(xw_t) : 1;
   __shared__ xw_t hub[kHub];
   __shared__ int64_t s_item;
@@ -1064,7 +1087,7 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
   int const tid  = threadIdx.x;
   int const lane = tid & 63;
   int const wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0ull;
+  for (int i = tid; i < kWin; i += kPushThreads) acc[i] = 0;
   using cunit_t        = __attribute__((address_space(4))) push_unit const;
   cunit_t* const units = (cunit_t*)sa.units;
   xw_t const* const x  = reinterpret_cast<xw_t const*>(sa.a.x_in);
@@ -1141,14 +1164,53 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
       }
     };
     auto sum = [&](u32x4_t const& w, xw_t const (&xv)[kRows]) {
+      if constexpr (kAcc32) {
+        // A term's low word goes into the 32-bit LDS sum; the old value the add returns
+        // says whether it carried out, and a carry (or a term of 2^32 or more: x~ above
+        // 2^-20) is counted in the destination's global carry word -- rare (about
+        // sum / 2^32 per destination and iteration), and integer like the rest, so the
+        // sums stay exact and order-free.  All 8 adds are issued before the first
+        // return is waited for.
+        uint32_t lo[kRows], old[kRows];
+        uint32_t* const cw = sa.carry + ((win & kWinMask) << WB);
+        if (sa.acc32_nocheck) {  // measurement only (pr_carry_check = 0): no returns, carries lost
 #pragma unroll
-      for (int j = 0; j < kRows; ++j) {
-        uint32_t const e = entry(w, j);
-        xw_t const v     = xv[j];
-        unsigned long long fix;
-        if constexpr (ENC) fix = dec_fixed(v);
-        else fix = fixed_of(v);
-        if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
+          for (int j = 0; j < kRows; ++j) {
+            uint32_t const e = entry(w, j);
+            unsigned long long fix;
+            if constexpr (ENC) fix = dec_fixed(xv[j]);
+            else fix = fixed_of(xv[j]);
+            if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], (uint32_t)fix);
+          }
+          return;
+        }
+#pragma unroll
+        for (int j = 0; j < kRows; ++j) {
+          uint32_t const e = entry(w, j);
+          unsigned long long fix;
+          if constexpr (ENC) fix = dec_fixed(xv[j]);
+          else fix = fixed_of(xv[j]);
+          lo[j] = (e >> WB) != kJump ? (uint32_t)fix : 0u;
+          if ((e >> WB) != kJump) {
+            old[j] = atomicAdd(&acc[e & kLow], lo[j]);
+            if (fix >> 32) atomicAdd(cw + (e & kLow), (uint32_t)(fix >> 32));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kRows; ++j) {
+          uint32_t const e = entry(w, j);
+          if ((e >> WB) != kJump && old[j] > ~lo[j]) atomicAdd(cw + (e & kLow), 1u);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kRows; ++j) {
+          uint32_t const e = entry(w, j);
+          xw_t const v     = xv[j];
+          unsigned long long fix;
+          if constexpr (ENC) fix = dec_fixed(v);
+          else fix = fixed_of(v);
+          if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], fix);
+        }
       }
     };
     // Software pipeline: the next unit's gathers are issued before this unit is
@@ -1216,6 +1278,15 @@ __global__ __launch_bounds__(kPushThreads) void k_pr_push16_w14(push_args<V, E, 
   push_body16<14, V, E, R, ENC, true, true, BANDS>(sa);
 }
 
+// 32K-destination windows in 32-bit LDS words (fewer (window, x~ line) pairs than 16K
+// windows: RMAT-22 0.41 -> 0.26 GB of line fills for 1.053E -> 1.115E entries,
+// scripts/l2model pairs model); single GPU, packed entries, fused apply
+template <typename V, typename E, typename R, bool ENC>
+__global__ __launch_bounds__(kPushThreads) void k_pr_push16_w15(push_args<V, E, R> sa)
+{
+  push_body16<15, V, E, R, ENC, true, true, false>(sa);
+}
+
 template <typename V, typename E, typename R, bool WEIGHTED>
 __global__ __launch_bounds__(kPushThreads) void k_pr_push_q_w14(push_args<V, E, R> sa)
 {
@@ -1234,6 +1305,13 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
   unsigned long long my_diff = 0, my_dang = 0;
   int64_t const stride = (int64_t)gridDim.x * blockDim.x;
   int64_t v            = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // a 32K-window schedule's carries (sa.carry): the sums' high parts, read and cleared here
+  auto take_carry = [&](int64_t vv) -> unsigned long long {
+    if (!sa.carry) return 0ull;
+    uint32_t const c = sa.carry[vv];
+    if (c) sa.carry[vv] = 0u;
+    return (unsigned long long)c << 32;
+  };
   if constexpr (std::is_same<R, float>::value) {
     // fp32: four consecutive vertices per lane through 16-byte loads and stores (pr,
     // outw, x~) and two 16-byte loads of the sums -- a quarter of the memory
@@ -1242,7 +1320,8 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
     typedef unsigned u4_t __attribute__((ext_vector_type(4)));
     typedef unsigned long long u2_t __attribute__((ext_vector_type(2)));
     bool const aligned = ((reinterpret_cast<uintptr_t>(a.pr) | reinterpret_cast<uintptr_t>(a.outw) |
-                           reinterpret_cast<uintptr_t>(a.x_out) | reinterpret_cast<uintptr_t>(sa.acc)) & 15) == 0;
+                           reinterpret_cast<uintptr_t>(a.x_out) | reinterpret_cast<uintptr_t>(sa.acc)) & 15) == 0 &&
+                         !sa.carry;
     if (aligned) {
       int64_t const nq = a.nv / 4;
       for (int64_t q = v; q < nq; q += stride) {
@@ -1290,13 +1369,15 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
     for (int j = 0; j < kApplyBatch; ++j) {
       int64_t const vj = v + j * stride;
       if (!sa.keep_acc && f[j] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
+      f[j] += take_carry(vj);
       vertex_update_from<V, E, R>(a, (V)vj, (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf, my_diff,
                                   my_dang);
     }
   }
   for (; v < a.nv; v += stride) {
-    unsigned long long const f = sa.acc[v];
+    unsigned long long f = sa.acc[v];
     if (!sa.keep_acc && f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
+    f += take_carry(v);
     vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
@@ -1766,7 +1847,8 @@ inline void build_items(hipStream_t s, pr_push_t& pp, push_unit* units, int64_t 
   // Below: one queue of tiles of <= 8 units of a window (RMAT-22: the XCD queues
   // measured 0.199 -> 0.216, the last groups' imbalance outweighing the L2 hits).
   auto hu = to_host(units, nunits, s);
-  int64_t const tg = std::max<int64_t>(kPushUnit, ne / (push_blocks(pp.win_bits) * kShareDiv));
+  int64_t const div = tu.pr_share_div > 0 ? tu.pr_share_div : kShareDiv;
+  int64_t const tg  = std::max<int64_t>(kPushUnit, ne / (push_blocks(pp.win_bits) * div));
   std::vector<int64_t> item_u, item_e;
   for (int64_t u0 = 0; u0 < nunits;) {
     int64_t u1 = u0;
@@ -2111,8 +2193,8 @@ template <typename E, typename CM>
 bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, int64_t ne, int64_t nv, pr_push_t& pp,
                               tuning_t const& tu, int64_t band_cut)
 {
-  int const wb = push_win_bits(nv, tu);
-  if (wb < 14 || band_cut >= nv) band_cut = 0;
+  int const wb = push_win_bits(nv, tu, true);
+  if (wb != 14 || band_cut >= nv) band_cut = 0;
   int64_t const nwin_real = std::max<int64_t>(1, (nv + (int64_t(1) << wb) - 1) >> wb);
   int64_t const nwin      = band_cut > 0 ? 2 * nwin_real : nwin_real;
   int const sbits = std::max(1, bits_for((unsigned long long)std::max<int64_t>(nv - 1, 1)));
@@ -2170,6 +2252,12 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
   pp.tile_ctr.set_stream(s);
   pp.tile_ctr.resize(2 * kQueues * kCtrStride * sizeof(unsigned int));
   HIP_CHECK(hipMemsetAsync(pp.tile_ctr.data(), 0, 2 * kQueues * kCtrStride * sizeof(unsigned int), s));
+  pp.carry.release();
+  if (wb == 15) {
+    pp.carry.set_stream(s);
+    pp.carry.resize(pp.nacc * sizeof(uint32_t));
+    HIP_CHECK(hipMemsetAsync(pp.carry.data(), 0, pp.nacc * sizeof(uint32_t), s));
+  }
   pp.qoff.assign(kQueues + 1, 0);
   pp.nitems = 0;
   pp.packed = true;
@@ -2302,6 +2390,7 @@ void set_queue_args(push_args<V, E, R>& sa, pr_push_t& pp, hipStream_t s)
   sa.units    = pp.units.data<push_unit>();
   sa.nunits   = pp.nunits;
   sa.acc      = pp.acc.data<unsigned long long>();
+  sa.carry    = pp.win_bits == 15 ? pp.carry.data<uint32_t>() : nullptr;
   sa.items    = pp.items.data<int64_t>();
   sa.queue    = pp.queue.data<int64_t>();
   sa.nitems   = pp.nitems;
@@ -2340,6 +2429,7 @@ inline bool fuse_apply(pr_push_t const& pp, tuning_t const& tu)
 template <typename V, typename E, typename R>
 auto push_kernel(pr_push_t const& pp, bool weighted, bool enc = false)
 {
+  if (pp.win_bits == 15) return enc ? k_pr_push16_w15<V, E, R, true> : k_pr_push16_w15<V, E, R, false>;
   if (pp.win_bits == 14) {
     if (pp.packed && pp.bands) return enc ? k_pr_push16_w14<V, E, R, true, true> : k_pr_push16_w14<V, E, R, false, true>;
     if (pp.packed) return enc ? k_pr_push16_w14<V, E, R, true> : k_pr_push16_w14<V, E, R, false>;
@@ -2498,6 +2588,7 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
     sa.fuse    = fuse ? 1 : 0;
     sa.nhub    = h.tune.pr_hub ? nv : 0;  // hub x~ staged in LDS (16K windows; A/B switch)
+    sa.acc32_nocheck = h.tune.pr_carry_check ? 0 : 1;
   }
   // measured-cost queues: the first launch on this schedule records item durations
   bool calibrating = push && calibration_wanted(adj.pr, h.tune);

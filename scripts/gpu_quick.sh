@@ -10,7 +10,7 @@ if [ -n "${PRE:-}" ]; then
   timeout -k 10 300 bash -c "$PRE" > $OUT/pre.log 2>&1; rc=$?; tail -30 $OUT/pre.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "${TESTS:-}" ]; then
-  CGX_TEST_CLOCK=1 timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -m gpu -v -rf --timeout 400 --timeout-method thread --durations=20 > $OUT/pytest.log 2>&1
+  CGX_TEST_CLOCK=1 timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest $TESTS -m gpu -v -rf ${PYTEST_EXTRA:-} --timeout 400 --timeout-method thread --durations=20 > $OUT/pytest.log 2>&1
   rc=$?; tail -25 $OUT/pytest.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi
 if [ -n "${BENCH:-}" ]; then

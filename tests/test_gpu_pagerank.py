@@ -316,11 +316,12 @@ def test_unit_weights_take_unweighted_push(scale):
 
 @pytest.mark.parametrize("scale", [12, 20])
 def test_window_bits_bitwise_equal(scale):
-    """4K, 8K and 16K-destination windows (pr_win_bits 12 / 13 / 14; 14 runs one
-    128 KB-LDS block per CU) sum the same fixed-point terms: the same bits."""
+    """4K, 8K, 16K and 32K-destination windows (pr_win_bits 12 / 13 / 14 / 15; 14 and
+    15 run one 128 KB-LDS block per CU, 15 in 32-bit words with carries) sum the same
+    fixed-point terms: the same bits.  (15 with 32-bit entries is built as 14.)"""
     s, d, _ = rmat_graph(scale, False, True)
     out = []
-    for wb in (12, 13, 14):
+    for wb in (12, 13, 14, 15):
         for packed in (1, 0):
             h, G = make_graph(s, d, None, transposed=True, symmetric=True,
                               options={"pr_win_bits": wb, "pr_packed": packed})
@@ -345,8 +346,8 @@ def _empty_window_graph():
     return (pairs // n).astype(np.int32), (pairs % n).astype(np.int32), n
 
 
-@pytest.mark.parametrize("graph", ["rmat20", "empty_windows"])
-def test_fused_apply_bitwise_equal(graph):
+@pytest.mark.parametrize("graph,wb", [("rmat20", 14), ("rmat20", 15), ("empty_windows", 14)])
+def test_fused_apply_bitwise_equal(graph, wb):
     """The push with the apply fused in (pagerank.hip fused_finish: the block that
     finishes a window applies it, from LDS for whole-window items; the last one
     applies the windows without items and updates the state) gives the same bits
@@ -362,7 +363,7 @@ def test_fused_apply_bitwise_equal(graph):
     out = []
     for fuse, whole in ((1, 1), (0, 1), (1, 0)):
         h, G = make_graph(s, d, None, transposed=True, **kw,
-                          options={"pr_win_bits": 14, "pr_fuse": fuse, "pr_whole": whole})
+                          options={"pr_win_bits": wb, "pr_fuse": fuse, "pr_whole": whole})
         v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
         # a second call on the same schedule: queue heads and window counts were reset
         _, r2 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
@@ -378,7 +379,7 @@ def test_fused_apply_bitwise_equal(graph):
         assert (np.abs(got[:n] - ref) / ref).max() < REL
 
 
-@pytest.mark.parametrize("scale,wb", [(12, 14), (20, 14), (20, 0), (18, 12)])
+@pytest.mark.parametrize("scale,wb", [(12, 14), (20, 14), (20, 0), (18, 12), (20, 15)])
 def test_fast_symmetric_build_bitwise_equal(scale, wb):
     """The one-word-key schedule build of symmetric unweighted graphs (pagerank.hip
     build_push_packed_sym: keys from the out-edge adjacency, a keys-only sort of the
@@ -519,3 +520,37 @@ def test_out_weight_sums_tiled(case):
         assert rel.max() <= 1.2e-7 and (got == want).mean() > 0.9999
     else:
         assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n", [4000, 200_000])
+def test_wide_window_carries_bitwise_equal(n):
+    """32K windows sum in 32-bit LDS words (push_body16, WB = 15): a small graph has
+    large x~ terms (1 / V, above 2^-20: high words counted in the carry array) and
+    destinations whose sums wrap the 32-bit word many times per window (every carry
+    counted).  Same bits and iterations as the 64-bit-word 16K windows, fused and
+    separate apply, and a second call on the cached schedule (carries cleared)."""
+    rng = np.random.default_rng(11)
+    m = 40 * n
+    s = rng.integers(0, n, m).astype(np.int32)
+    d = (rng.integers(0, n, m) // rng.integers(1, 50, m)).astype(np.int32)  # skewed to low ids
+    pairs = np.unique(np.concatenate([s.astype(np.int64) * n + d, d.astype(np.int64) * n + s]))
+    pairs = pairs[pairs // n != pairs % n]
+    s, d = (pairs // n).astype(np.int32), (pairs % n).astype(np.int32)
+    out = []
+    for wb, fuse in ((14, 1), (15, 1), (15, 0)):
+        h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True,
+                          options={"pr_win_bits": wb, "pr_fuse": fuse})
+        v, r = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        _, r2 = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-6, 500, False)
+        assert np.array_equal(host(r), host(r2))
+        out.append((host(v), host(r), h.last_iterations()))
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+    og_g = og.create_graph(s, d, None, store_transposed=True, renumber=True)
+    ref = np.zeros(n)
+    ref[og_g.number_map] = opr.pagerank_from_graph(og_g, alpha=0.85, epsilon=1e-6, max_iterations=500)
+    vv = out[0][0]
+    got = np.zeros(n)
+    got[vv] = out[0][1]
+    assert (np.abs(got[vv] - ref[vv]) / ref[vv]).max() < REL
