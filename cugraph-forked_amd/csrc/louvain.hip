@@ -24,7 +24,7 @@
 //   * a row the tables cannot hold (or a level with negative weights): the sort
 //     path sweep_sorted -- key = row << cb | cluster(destination), radix sort,
 //     reduce_by_key to (row, cluster, sum), gains, reduce_by_key over the row
-//     (also the A/B switch CGX_LOUVAIN_HASH=0).
+//     (also the A/B option louvain_hash = 0).
 // Ties go to the smaller cluster id in every path.  Cluster weights are 64-bit
 // fixed-point totals updated by each sweep's moves (as the multi-GPU owners keep
 // them); the modularity's internal weight
