@@ -188,6 +188,10 @@ struct pr_push_t {
   int64_t nwin_real = 0;  // real windows (nwin counts the virtual ones)
   buffer win_pub;         // uint32[nwin_real]: items of the window that published this iteration
   buffer carry;           // uint32[nacc]: 32K windows' carry words (push_args::carry), zero between iterations
+  // the last call's iteration count (plain calls: no guess, no personalization) with
+  // its alpha and epsilon: the first chunk of the next such call (pagerank.hip)
+  int last_iters = 0;
+  double last_alpha = -1.0, last_eps = -1.0;
 };
 
 // One orientation of the adjacency: majors (rows) -> minors (indices).
