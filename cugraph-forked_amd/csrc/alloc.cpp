@@ -10,6 +10,7 @@
 // returned, and the allocation is retried once.
 #include "common.hpp"
 
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -23,6 +24,10 @@ struct cache_t {
   std::unordered_map<hipStream_t, std::multimap<size_t, void*>> free_blocks;
   std::unordered_map<void*, size_t> live;  // block -> class size
   size_t cached = 0;
+  // statistics (cugraph_amd_allocator_stats): driver allocations, their bytes and
+  // seconds, and out-of-memory trims (every cached block returned, then a retry)
+  size_t n_malloc = 0, malloc_bytes = 0, n_oom = 0;
+  double malloc_s = 0.0;
 };
 
 cache_t& cache()
@@ -86,14 +91,19 @@ void* device_alloc_raw(size_t bytes, hipStream_t s)
     }
   }
   void* p = nullptr;
+  auto const t0 = std::chrono::steady_clock::now();
   if (hipMalloc(&p, cls) != hipSuccess) {
     (void)hipGetLastError();
+    ++c.n_oom;
     trim_locked(c);
     if (hipMalloc(&p, cls) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
   }
+  c.malloc_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  ++c.n_malloc;
+  c.malloc_bytes += cls;
   c.live[p] = cls;
   return p;
 }
@@ -128,6 +138,17 @@ void* device_forget(void* p, hipStream_t s)
   // pending work on the block's stream finishes before the caller may hipFree it
   if (hipStreamSynchronize(s) != hipSuccess) (void)hipGetLastError();
   return p;
+}
+
+void device_alloc_stats(double* out)
+{
+  cache_t& c = cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  out[0] = (double)c.n_malloc;
+  out[1] = (double)c.malloc_bytes;
+  out[2] = c.malloc_s;
+  out[3] = (double)c.n_oom;
+  out[4] = (double)c.cached;
 }
 
 size_t device_cache_trim()

@@ -583,4 +583,5 @@ extern "C" void cugraph_amd_last_louvain_partition(const cugraph_resource_handle
   *ghosts      = H(handle)->last_louvain_ghosts;
 }
 extern "C" size_t cugraph_amd_trim_device_cache(void) { return cgx::device_cache_trim(); }
+extern "C" void cugraph_amd_allocator_stats(double* out) { cgx::device_alloc_stats(out); }
 extern "C" const char* cugraph_amd_version(void) { return "cugraph-forked_amd libcugraph_c gfx950 " __DATE__; }

@@ -74,6 +74,7 @@ constexpr data_type_id_t dtype_of()
 void* device_alloc(size_t bytes, hipStream_t s);
 void device_free(void* p, hipStream_t s);
 size_t device_cache_trim();  // returns the cached bytes released
+void device_alloc_stats(double* out);  // [5]: driver allocations, their bytes and seconds, OOM trims, cached bytes
 // Hand a live block to the caller: the allocator stops tracking it (it is never
 // cached or reused) and the stream is synchronised; the caller frees it with hipFree.
 void* device_forget(void* p, hipStream_t s);

@@ -25,6 +25,15 @@ __all__ = ["trim_device_cache", "ResourceHandle", "GraphProperties", "SGGraph", 
            "louvain", "version"]
 
 
+def allocator_stats():
+    """libcugraph_c's caching allocator counters: dict of driver allocations, their
+    bytes and seconds, out-of-memory trims and the bytes cached now."""
+    out = (ctypes.c_double * 5)()
+    _lib.lib.cugraph_amd_allocator_stats(out)
+    return {"mallocs": int(out[0]), "malloc_bytes": int(out[1]), "malloc_s": out[2], "oom_trims": int(out[3]),
+            "cached_bytes": int(out[4])}
+
+
 def trim_device_cache():
     """Return libcugraph_c's cached HBM blocks to the driver (ext.h
     cugraph_amd_trim_device_cache); call it beside torch.cuda.empty_cache().

@@ -144,6 +144,7 @@ _proto("cugraph_amd_last_louvain_levels", c_size_t, P)
 _proto("cugraph_amd_last_louvain_sweep_bytes", c_double, P)
 _proto("cugraph_amd_last_louvain_partition", None, P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64))
 _proto("cugraph_amd_trim_device_cache", c_size_t)
+_proto("cugraph_amd_allocator_stats", None, ctypes.POINTER(c_double))
 _proto("cugraph_amd_version", ctypes.c_char_p)
 _proto("cugraph_amd_measure_copy_bandwidth", c_double, P, c_size_t, c_int)
 _proto("cugraph_type_erased_device_array_release", P, P)

@@ -149,6 +149,12 @@ cugraph_type_erased_device_array_view_t* cugraph_amd_heirarchical_clustering_res
  * equivalent is releasing its RMM pool. */
 size_t cugraph_amd_trim_device_cache(void);
 
+/* The caching allocator's counters since the process started: out[0] driver
+ * allocations (hipMalloc), out[1] their bytes, out[2] the seconds spent in them,
+ * out[3] out-of-memory trims (every cached block released, then one retry),
+ * out[4] bytes cached now.  Measurement aid. */
+void cugraph_amd_allocator_stats(double* out);
+
 /* Measured HBM ceiling: a 16-B-per-lane grid-stride copy of `bytes` (nontemporal
  * loads and stores), `reps` launches timed with HIP events on the handle's stream.
  * Returns (read + write bytes) / time in GB/s, or a negative value on error. */
