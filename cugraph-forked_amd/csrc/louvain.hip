@@ -1103,6 +1103,7 @@ struct louvain_state {
   dbuf<double> scal;       // 2 scalars
   size_t bytes = 0;        // multi-GPU: bytes this rank sent in the exchanges being counted
   tuning_t tune;           // the handle's A/B switches (louvain_*)
+  bool trace = false;      // CGX_LOUVAIN_TRACE: per-level plan statistics on stderr (measurement only)
   louvain_state(hipStream_t st, tuning_t const& t) : s(st), scratch(1024, st), scal(2, st), tune(t) {}
 };
 
@@ -1599,6 +1600,28 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, u64
   }
   HIP_CHECK(hipStreamSynchronize(s));  // the walk's scratch goes out of scope
   P.hash = true;
+  if (S.trace && tb > 0) {  // heavy rows by degree (measurement only)
+    dbuf<int64_t> first(tb, s), deg(tb, s);
+    hipLaunchKernelGGL(k_big_info, dim3(grid_for(tb, kBlock, 16384)), dim3(kBlock), 0, s, P.bigd.data(), P.off, tb,
+                       first.data(), deg.data());
+    CGX_LAUNCH_CHECK();
+    auto const hd = to_host(deg.data(), (size_t)tb, s);
+    int64_t const lim[6] = {2048, 4096, 8192, 32768, 262144, INT64_MAX};
+    int64_t rows[6] = {}, edges[6] = {};
+    for (int64_t d : hd) {
+      int b = 0;
+      while (d > lim[b]) ++b;
+      ++rows[b];
+      edges[b] += d;
+    }
+    std::fprintf(stderr, "[louvain] plan: %lld hash chunks, %lld heavy rows (%lld segments, %lld bucket blocks); "
+                         "heavy rows / edges by degree <=2K %lld/%lld <=4K %lld/%lld <=8K %lld/%lld <=32K %lld/%lld "
+                         "<=256K %lld/%lld more %lld/%lld\n",
+                 (long long)P.nchunks, (long long)tb, (long long)P.nsegs, (long long)P.nbblocks, (long long)rows[0],
+                 (long long)edges[0], (long long)rows[1], (long long)edges[1], (long long)rows[2], (long long)edges[2],
+                 (long long)rows[3], (long long)edges[3], (long long)rows[4], (long long)edges[4], (long long)rows[5],
+                 (long long)edges[5]);
+  }
 }
 
 // one synchronous local-move sweep (update_clustering_by_delta_modularity) over
@@ -1787,6 +1810,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
   std::vector<dbuf<uint32_t>> dendrogram;
   double best_q = -1.0;
   bool const trace = std::getenv("CGX_LOUVAIN_TRACE") != nullptr;  // measurement only
+  S.trace          = trace;
   auto t_last      = std::chrono::steady_clock::now();
   auto lap         = [&](char const* what, int64_t nv, int64_t ne, double q) {
     if (!trace) return;
