@@ -396,9 +396,17 @@ def networkx_cpu_legs(args):
 
 
 # ----------------------------------------------------------------------------- BFS
+def ab_options(h, args):
+    """--options name=value,...: handle options for A/B runs (include/cugraph_amd/ext.h)."""
+    for kv in filter(None, (getattr(args, "options", "") or "").split(",")):
+        k, v = kv.split("=")
+        h.set_option(k, float(v))
+
+
 def bfs_leg(p, args, child=False):
     import torch
     h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
+    ab_options(h, args)
     scale = args.bfs_scale
     g, roots, deg = build_rmat_graph(p, h, scale, transposed=False, want_roots=args.bfs_roots, mg=args.mg)
     V, E = g.number_of_vertices(), g.number_of_edges()
@@ -516,6 +524,7 @@ def louvain_leg(p, args, scale=None):
     resolution 1.0.  SG at N=1, the MG path (rows by source owner, RCCL) at N>1."""
     import torch
     h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
+    ab_options(h, args)
     small, _, _ = build_rmat_graph(p, h, 10, weighted=True, transposed=False, mg=args.mg)
     p.louvain(h, small, 100, 1.0, False)  # module load + allocator warm-up off the clock
     del small
@@ -616,6 +625,7 @@ def main():
     ap.add_argument("--traffic-child", choices=["pagerank", "bfs"], default=None, help=argparse.SUPPRESS)
     ap.add_argument("--bfs-only", action="store_true", help="A/B aid: only the BFS leg, its dict on stdout")
     ap.add_argument("--louvain-only", action="store_true", help="A/B aid: only the Louvain leg, its dict on stdout")
+    ap.add_argument("--options", default="", help="A/B aid: handle options name=value,... for the BFS / Louvain legs")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -849,16 +849,18 @@ __global__ __launch_bounds__(256) void k_bu_residual(bfs_args<V, E> a, V const* 
   flush_counts(a.ctr, my_n, my_m);
 }
 
-// dist = INF, pred = -1 and the three bitmaps cleared in one launch (was 2 fills + 3 memsets)
+// dist = INF, pred = -1, the result's vertex ids (the number map) and the three
+// bitmaps cleared in one launch (was 2 fills + 3 memsets + a copy)
 template <typename V>
 __global__ void k_bfs_setup(V* dist, V* pred, int64_t nv, V inf, uint32_t* vis, uint32_t* fr, uint32_t* nxt,
-                            int64_t nwords, int* bad)
+                            int64_t nwords, int* bad, V const* nmap, V* vout)
 {
   int64_t const stride = (int64_t)gridDim.x * blockDim.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *bad = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += stride) {
     dist[v] = inf;
     if (pred) pred[v] = (V)-1;
+    vout[v] = nmap[v];
   }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords; i += stride) {
     vis[i] = 0u;
@@ -924,7 +926,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   // (no host round trip here)
   if (g.renumbered) renumber_ext_to_int_unchecked(h, g, sources->data, sources->size);
   V const INF = std::numeric_limits<V>::max();
-  res.vertices  = number_map_copy(h, g);
+  // the result's vertex ids: the number map, copied by k_bfs_setup (one pass with the initialisation)
+  res.vertices  = std::make_unique<device_array_t>((size_t)nv, g.vertex_type, s);
   res.distances = std::make_unique<device_array_t>((size_t)nv, dtype_of<V>(), s);
   res.predecessors = std::make_unique<device_array_t>(want_pred ? (size_t)nv : 0, dtype_of<V>(), s);
   V* dist = res.distances->buf.data<V>();
@@ -940,7 +943,8 @@ void bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, size
   dbuf<uint32_t> vis(nwords, s), fr(nwords, s), nxt(nwords, s);
   dbuf<int> bad(1, s);
   hipLaunchKernelGGL(k_bfs_setup<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, dist, pred, nv, INF,
-                     vis.data(), fr.data(), nxt.data(), nwords, bad.data());
+                     vis.data(), fr.data(), nxt.data(), nwords, bad.data(), g.number_map.data<V>(),
+                     res.vertices->buf.data<V>());
   CGX_LAUNCH_CHECK();
   dbuf<V> qa[3], qb[3];
   for (int c = 0; c < 3; ++c) {

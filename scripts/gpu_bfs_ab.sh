@@ -1,5 +1,7 @@
-# BFS A/B: optional tests, then bench.py --bfs-only under each MODES entry
-# (env assignments joined by ',', "-" = defaults)
+#!/bin/bash
+# BFS A/B: optional tests, then bench.py --bfs-only under each MODES entry (handle
+# options name=value joined by ',', "-" = defaults), the modes interleaved ROUNDS times
+# usage: TAG=r05ab MODES="- bfs_prefetch_off=0" ROUNDS=2 bash scripts/gpu_bfs_ab.sh
 set -o pipefail
 OUT=gpurun_out/${TAG:-bfsab}; mkdir -p $OUT
 if [ -n "$TESTS" ]; then
@@ -7,8 +9,10 @@ if [ -n "$TESTS" ]; then
   rc=$?; tail -3 $OUT/pytest.log; grep -E "FAILED" $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
 i=0
-for m in ${MODES:-- -}; do
-  i=$((i+1)); envs=""; [ "$m" = "-" ] || envs="${m//,/ }"
-  env $envs timeout -k 10 300 python -u bench.py --bfs-only ${BENCH_ARGS:-} > $OUT/b_$i.json 2> $OUT/b_$i.err
-  rc=$?; echo "== $m: $(grep '\[bench\]' $OUT/b_$i.err)"; [ $rc -eq 0 ] || { tail $OUT/b_$i.err; exit $rc; }
+for r in $(seq ${ROUNDS:-1}); do
+  for m in ${MODES:-- -}; do
+    i=$((i+1)); opts=""; [ "$m" = "-" ] || opts="$m"
+    timeout -k 10 300 python -u bench.py --bfs-only --options "$opts" ${BENCH_ARGS:-} > $OUT/b_$i.json 2> $OUT/b_$i.err
+    rc=$?; echo "== $m: $(grep '\[bench\]' $OUT/b_$i.err)" | tee -a $OUT/ab.log; [ $rc -eq 0 ] || { tail $OUT/b_$i.err; exit $rc; }
+  done
 done
