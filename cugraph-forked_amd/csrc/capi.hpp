@@ -46,6 +46,8 @@ struct tuning_t {
   int mg_chunks        = 0;     // MG overlap chunks (0: by size)
   double bfs_alpha     = 40.0;  // direction switch (Beamer's alpha / beta)
   double bfs_beta      = 64.0;
+  double mg_bfs_alpha  = 40.0;  // multi-GPU BFS direction switch (mg_bfs.hip; one-rank RMAT-24: 40 / 64
+  double mg_bfs_beta   = 64.0;  // 2.92 vs Beamer's 14 / 24 3.20 ms per traversal)
   bool bfs_probe_vec   = true;  // bottom-up probe by 16-byte loads
   bool bfs_head        = true;  // bottom-up probe's head table
   int bfs_res_grid     = 1024;  // residual scan blocks

@@ -29,10 +29,14 @@
 //    frontier bits as whole words.  Level counts go to 16 partial counters.
 //
 // Both pick the frontier neighbour with the smallest global id, so distances and
-// predecessors do not depend on the direction schedule.  The direction switch keeps
-// Beamer's alpha 14 / beta 24 on global counts: a bottom-up level here also pays a
-// V/8-byte bitmap allgather, so the single-GPU tuning (40 / 64, bfs.hip) does not
-// carry over unmeasured.  Predecessors are returned as external ids.
+// predecessors do not depend on the direction schedule.  The direction switch on
+// global counts is the handle's mg_bfs_alpha / mg_bfs_beta, 40 / 64 like the single
+// GPU's: through a one-rank RCCL communicator (no exchange cost) RMAT-24 takes 2.92
+// ms per traversal with them against 3.20 with Beamer's 14 / 24
+// (scripts/mg_bfs_ab.py); with several ranks a bottom-up level adds a V/8-byte
+// bitmap allgather (1.1 MB at RMAT-24) and a top-down level its candidates'
+// all-to-all, so the measured kernel trade stands until a multi-rank run says
+// otherwise.  Predecessors are returned as external ids.
 #include "capi.hpp"
 #include "comm.hpp"
 #include "mg_graph.hpp"
@@ -701,8 +705,8 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   to_device(colvoff_d.data(), colvoff.data(), colvoff.size(), s);
   while (nf > 0 && depth < limit) {
     if (dir_opt) {
-      if (!bottom_up && m_f > m_u / 14.0) bottom_up = true;
-      else if (bottom_up && (double)nf < (double)g.num_vertices / 24.0) bottom_up = false;
+      if (!bottom_up && m_f > m_u / h.tune.mg_bfs_alpha) bottom_up = true;
+      else if (bottom_up && (double)nf < (double)g.num_vertices / h.tune.mg_bfs_beta) bottom_up = false;
     }
     HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
     V const depth1 = depth + 1;

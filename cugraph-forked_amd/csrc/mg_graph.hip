@@ -83,10 +83,26 @@ __global__ void k_owner_global(V const* x, size_t n, int64_t const* voff, int P,
   }
 }
 
-__global__ void k_histogram(int const* dest_sorted, size_t n, int P, int64_t* cnt)
+// per-rank counts of a destination-sorted array: two binary searches per rank (a
+// per-element atomicAdd onto the P counters serialised at the memory side: 14 ms for
+// 2.4M elements on one rank, RMAT-22's predecessor routing in the MG BFS)
+__global__ void k_rank_counts(int const* dest_sorted, int64_t n, int P, int64_t* cnt)
 {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    atomicAdd((unsigned long long*)(cnt + dest_sorted[i]), 1ull);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P; q += gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = n;  // first position with dest >= q
+    while (lo < hi) {
+      int64_t const mid = (lo + hi) >> 1;
+      if (dest_sorted[mid] < q) lo = mid + 1;
+      else hi = mid;
+    }
+    int64_t a = lo, b = n;  // first position with dest >= q + 1
+    while (a < b) {
+      int64_t const mid = (a + b) >> 1;
+      if (dest_sorted[mid] < q + 1) a = mid + 1;
+      else b = mid;
+    }
+    cnt[q] = a - lo;
+  }
 }
 
 template <typename T, typename I>
@@ -120,8 +136,7 @@ routing route_by(int const* dest, size_t n, int P, hipStream_t s)
   iota<int64_t>(iv.data(), n, 0, s);
   radix_sort_pairs<int, int64_t>(dest, d2.data(), iv.data(), rt.perm.data(), n, 0, bits_for(P), s);
   dbuf<int64_t> cnt(P, s);
-  fill<int64_t>(cnt.data(), P, 0, s);
-  hipLaunchKernelGGL(k_histogram, dim3(blocks(n)), dim3(kBlock), 0, s, d2.data(), n, P, cnt.data());
+  hipLaunchKernelGGL(k_rank_counts, dim3(1), dim3(64), 0, s, d2.data(), (int64_t)n, P, cnt.data());
   CGX_LAUNCH_CHECK();
   auto h = to_host(cnt.data(), P, s);
   for (int q = 0; q < P; ++q) rt.counts[q] = (size_t)h[q];
