@@ -346,10 +346,12 @@ __global__ void k_frontier_degrees(uint32_t const* frontier, int64_t nf, int64_t
 }
 
 // first position with key >= voff[q] << 32, for q in [0, P]
-__global__ void k_split_points(unsigned long long const* keys, int64_t n, int64_t const* voff, int P, int64_t* pos)
+__global__ void k_split_points(unsigned long long const* keys, size_t const* count, int64_t const* voff, int P,
+                               int64_t* pos)
 {
   int q = threadIdx.x;
   if (q > P) return;
+  int64_t const n = (int64_t)*count;  // the unique run count, left on the device
   unsigned long long bound = q == P ? ~0ull : ((unsigned long long)voff[q] << 32);
   int64_t lo = 0, hi = n;
   while (lo < hi) {
@@ -366,9 +368,10 @@ struct same_v {
 };
 
 // compact candidate keys -> v << 32 | parent (the sentinel ~0 stays ~0)
-__global__ void k_expand_cand(unsigned long long* k, int64_t n, int gb)
+__global__ void k_expand_cand(unsigned long long* k, size_t const* count, int gb)
 {
   unsigned long long const mask = (1ull << gb) - 1;
+  int64_t const n                = (int64_t)*count;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     unsigned long long const x = k[i];
     if (x != ~0ull) k[i] = ((x >> gb) << 32) | (x & mask);
@@ -394,9 +397,10 @@ __global__ void k_td_claim(unsigned long long const* cand, int64_t n, int64_t lo
 }
 
 template <typename V>
-__global__ void k_td_finalize(uint32_t const* next, int64_t n, V depth1, V* dist, V* pred, long long* best,
-                              int64_t const* off, level_ctr* ctr)
+__global__ void k_td_finalize(uint32_t const* next, V depth1, V* dist, V* pred, long long* best, int64_t const* off,
+                              level_ctr* ctr)
 {
+  int64_t const n      = (int64_t)ctr->next_n;  // the claims of k_td_claim (launched before, same stream)
   unsigned long long m = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t v = next[i];
@@ -406,6 +410,28 @@ __global__ void k_td_finalize(uint32_t const* next, int64_t n, V depth1, V* dist
     m += (unsigned long long)(off[v + 1] - off[v]);
   }
   block_add(&ctr->next_m, m);
+}
+
+// total candidate count: the exclusive scan's last entry plus the last degree
+__global__ void k_scan_total(unsigned long long const* pre, unsigned long long const* dg, int64_t n,
+                             unsigned long long* out)
+{
+  if (threadIdx.x == 0) *out = pre[n - 1] + dg[n - 1];
+}
+
+// a level's (vertices, edges) folded on the device: red[0..1] are then summed over the
+// ranks, red[2] keeps this rank's vertex count (one read-back per level)
+__global__ void k_level_fold(level_ctr const* c, double* red)
+{
+  if (threadIdx.x) return;
+  unsigned long long n = c->next_n, m = c->next_m;
+  for (int p = 0; p < kParts; ++p) {
+    n += c->part[p][0];
+    m += c->part[p][1];
+  }
+  red[0] = (double)n;
+  red[1] = (double)m;
+  red[2] = (double)n;
 }
 
 __global__ void k_mark_bits(uint32_t const* q, int64_t n, uint32_t* bits)
@@ -745,6 +771,7 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       for (auto x : row_counts) mx = std::max(mx, x);
       int64_t const nfg = mx * (int64_t)rowc.size;
       int64_t mcand     = 0;
+      dbuf<unsigned long long> tot(1, s);
       dbuf<uint32_t> fsend(std::max<int64_t>(mx, 1), s), fgath(std::max<int64_t>(nfg, 1), s);
       dbuf<unsigned long long> dg(std::max<int64_t>(nfg, 1), s), pre(std::max<int64_t>(nfg, 1), s);
       if (mx) {
@@ -756,35 +783,34 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
                            blk.off.data<int64_t>(), dg.data());
         CGX_LAUNCH_CHECK();
         exclusive_scan<unsigned long long, unsigned long long>(dg.data(), pre.data(), nfg, s);
-        mcand = (int64_t)(to_host(pre.data() + nfg - 1, 1, s)[0] + to_host(dg.data() + nfg - 1, 1, s)[0]);
+        hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(64), 0, s, pre.data(), dg.data(), nfg, tot.data());
+        CGX_LAUNCH_CHECK();
+        mcand = (int64_t)to_host_scalar(tot.data(), s);
       }
       // candidates over the block, smallest parent per destination
       dbuf<unsigned long long> cand(std::max<int64_t>(mcand, 1), s), cs(std::max<int64_t>(mcand, 1), s),
         cu(std::max<int64_t>(mcand, 1), s);
-      int64_t nu = 0;
+      dbuf<size_t> cnt(1, s);
       if (mcand) {
         hipLaunchKernelGGL(k_block_candidates<V>, dim3(blocks(mcand)), dim3(kBlock), 0, s, fgath.data(), nfg,
                            pre.data(), mcand, blk.off.data<int64_t>(), blk.idx.data<uint32_t>(), blk.row_lo, lo, hi,
                            dist, gb, cand.data());
         CGX_LAUNCH_CHECK();
         radix_sort_keys<unsigned long long>(cand.data(), cs.data(), mcand, 0, 2 * gb, s);
-        dbuf<size_t> cnt(1, s);
         size_t tmp = 0;
         HIP_CHECK(rocprim::unique(nullptr, tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v{gb}, s));
         buffer t(tmp, s);
         HIP_CHECK(rocprim::unique(t.data(), tmp, cs.data(), cu.data(), cnt.data(), (size_t)mcand, same_v{gb}, s));
-        nu = (int64_t)to_host_scalar(cnt.data(), s);
-        if (nu) {
-          hipLaunchKernelGGL(k_expand_cand, dim3(blocks(nu)), dim3(kBlock), 0, s, cu.data(), nu, gb);
-          CGX_LAUNCH_CHECK();
-        }
+        // the run count stays on the device: unique leaves at least one run of mcand >= 1 keys
+        hipLaunchKernelGGL(k_expand_cand, dim3(capped(mcand)), dim3(kBlock), 0, s, cu.data(), cnt.data(), gb);
+        CGX_LAUNCH_CHECK();
       }
       // to the destinations' owners: the R ranks of column c (the sentinel run, if
       // any, sorts last and is dropped)
       std::vector<size_t> counts(colc.size, 0);
-      if (nu) {
+      if (mcand) {
         dbuf<int64_t> pos(colc.size + 1, s);
-        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), nu, colvoff_d.data(), colc.size,
+        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), cnt.data(), colvoff_d.data(), colc.size,
                            pos.data());
         CGX_LAUNCH_CHECK();
         auto hp = to_host(pos.data(), colc.size + 1, s);
@@ -797,22 +823,21 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
                            reinterpret_cast<unsigned long long const*>(got.data()), (int64_t)got.n, lo, dist,
                            best.data(), flag.data(), qb.data(), ctr.data());
       CGX_LAUNCH_CHECK();
-      auto hn = to_host(ctr.data(), 1, s)[0];
-      if (hn.next_n)
-        hipLaunchKernelGGL(k_td_finalize<V>, dim3(capped(hn.next_n)), dim3(kBlock), 0, s, qb.data(),
-                           (int64_t)hn.next_n, depth1, dist, pred, best.data(), rows.off.data<int64_t>(), ctr.data());
+      // the claim count stays on the device (at most got.n)
+      if (got.n)
+        hipLaunchKernelGGL(k_td_finalize<V>, dim3(capped(got.n)), dim3(kBlock), 0, s, qb.data(), depth1, dist, pred,
+                           best.data(), rows.off.data<int64_t>(), ctr.data());
       CGX_LAUNCH_CHECK();
       std::swap(qa, qb);
     }
-    auto const cnt = level_counts(to_host(ctr.data(), 1, s)[0]);
-    nf_own         = (int64_t)cnt.first;
-    dbuf<double> red(2, s);
-    double loc[2] = {(double)cnt.first, (double)cnt.second};
-    HIP_CHECK(hipMemcpyAsync(red.data(), loc, sizeof(loc), hipMemcpyHostToDevice, s));
+    dbuf<double> red(3, s);
+    hipLaunchKernelGGL(k_level_fold, dim3(1), dim3(64), 0, s, ctr.data(), red.data());
+    CGX_LAUNCH_CHECK();
     comm.allreduce<double>(red.data(), red.data(), 2, CGX_COMM_SUM, s);
-    auto gr = to_host(red.data(), 2, s);
+    auto gr = to_host(red.data(), 3, s);
     nf      = (int64_t)gr[0];
     m_f     = gr[1];
+    nf_own  = (int64_t)gr[2];
     m_u     = m_u > m_f ? m_u - m_f : 0;
     ++depth;
     ++levels;
