@@ -561,6 +561,7 @@ constexpr int kBigThreads    = 512;
 constexpr int kBigMaxBuckets = 1024;  // LDS of pass A: 52 KB -> 3 blocks per CU
 constexpr int kBigPerBucket  = 2048;
 constexpr int kBigMaxSegs    = 2048;  // rows of <= 4M edges (heavier: sort path)
+constexpr int kBktSegGroup   = 512;   // pass B stages a row's segment runs 512 at a time (LDS: 3 blocks per CU)
 constexpr int kBktSlots      = 4096;
 constexpr int kBktThreads    = 512;
 constexpr int kBktCap        = 3072;  // < kBktSlots - kBktThreads: probing always ends
@@ -580,6 +581,15 @@ struct big_row {
   uint32_t single;      // one segment: pass A moves the row itself
 };
 
+// one pass-B block: bucket b of heavy row j (row id u), the row's first bucket-offset
+// slot ob and first partial slot pb (segment q's offsets are ob + q (2^logb + 1), its
+// partials start at pb + q kBigSeg), so the block reads its runs without the row and
+// segment records in between
+struct big_bblk {
+  int64_t ob, pb;
+  uint32_t j, u, b, ns, logb, pad;
+};
+
 struct big_args {
   uint32_t const* dst;
   double const* w;
@@ -592,7 +602,7 @@ struct big_args {
   u64* pval;
   int32_t* boffs;
   u64* own;
-  u64 const* bblocks;
+  big_bblk const* bblk;
   double const* self;
   double const* a;
   uint8_t const* present;
@@ -667,6 +677,7 @@ __device__ void gains_one_row(big_args const& p, uint32_t const* key, u64* val, 
   int const tid      = threadIdx.x;
   double an[kSPT];
   uint8_t pr[kSPT];
+  u64 tmax = 0;
 #pragma unroll
   for (int q = 0; q < kSPT; ++q) {
     int const h       = tid + q * T;
@@ -687,20 +698,27 @@ __device__ void gains_one_row(big_args const& p, uint32_t const* key, u64* val, 
     double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
     u64 const o  = order_bits(dq);
     val[h]       = o;
-    atomicMax(&bq, o);
+    tmax         = o > tmax ? o : tmax;
   }
+  // the wave's maximum first: one LDS atomic per wave instead of one per slot (a row's
+  // thousands of slots all hit the one word)
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    u64 const y = __shfl_xor(tmax, d, 64);
+    tmax        = y > tmax ? y : tmax;
+  }
+  if ((tid & 63) == 0 && tmax != 0) atomicMax(&bq, tmax);
 }
 
 // the block's LDS table holds every neighbour cluster of row rw.row: gains, best,
 // move (k_gain + best_gain_op + k_move for one row); bq / bc: LDS scratch
 __device__ void move_whole_row(big_args const& p, big_row const& rw, uint32_t const* key, u64* val, int nslot,
-                               unsigned bits, u64& bq, uint32_t& bc, double& old_sh)
+                               unsigned bits, u64& bq, uint32_t& bc, double& old_sh, uint32_t cu, double self,
+                               double kv, double a_old)
 {
 #pragma clang fp contract(off)
   int const tid      = threadIdx.x;
   uint32_t const u   = rw.row;
-  uint32_t const cu  = p.c[u + p.base];
-  double const self  = p.self[u];
   if (tid == 0) {
     double own     = 0.0;
     unsigned h     = slot32(cu, (int)bits);
@@ -717,7 +735,7 @@ __device__ void move_whole_row(big_args const& p, big_row const& rw, uint32_t co
     bc     = kEmpty32;
   }
   __syncthreads();
-  double const kv = p.k[u], a_old = p.a[cu], old_s = old_sh;
+  double const old_s = old_sh;
   gains_one_row<kBigThreads, kBigSlots>(p, key, val, nslot, cu, old_s, kv, a_old, bq);
   __syncthreads();
   for (int h = tid; h < nslot; h += blockDim.x)
@@ -741,6 +759,14 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
   int const tid     = threadIdx.x;
   big_seg const sg  = p.segs[blockIdx.x];
   big_row const rw  = p.rows[sg.j];
+  // the row's values are loaded here, in flight under the edge loads and gathers
+  uint32_t const cu = p.c[rw.row + p.base];
+  double kv = 0.0, self = 0.0, a_old = 0.0;
+  if (rw.single) {
+    kv    = p.k[rw.row];
+    self  = p.self[rw.row];
+    a_old = p.a[cu];
+  }
   int const nbk     = 1 << rw.logb;
   int bits          = 6;  // 2^bits >= 2 * edges slots
   while ((1 << bits) < 2 * (int)(sg.e1 - sg.e0)) ++bits;
@@ -785,7 +811,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
   }
   __syncthreads();
   if (rw.single) {
-    move_whole_row(p, rw, key, val, nslot, (unsigned)bits, bq, bc, old_sh);
+    move_whole_row(p, rw, key, val, nslot, (unsigned)bits, bq, bc, old_sh, cu, self, kv, a_old);
     return;
   }
   // The segment's distinct (cluster, partial) pairs, grouped by bucket: each thread
@@ -794,7 +820,6 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
   // contiguous run -- coalesced, where a store per pair at its bucket's position wrote
   // one partial line per 4- and 8-byte value
   constexpr int kSPT = kBigSlots / kBigThreads;
-  uint32_t const cu  = p.c[rw.row + p.base];
   uint32_t ck[kSPT], cpos[kSPT];
   u64 cv[kSPT];
 #pragma unroll
@@ -834,90 +859,102 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
 #pragma clang fp contract(off)
   __shared__ uint32_t key[kBktSlots];
   __shared__ u64 val[kBktSlots];
-  __shared__ uint32_t pre[kBigMaxSegs];
-  __shared__ int64_t start[kBigMaxSegs];
+  __shared__ uint32_t pre[kBktSegGroup];
+  __shared__ uint32_t start[kBktSegGroup];  // from the row's first partial slot (< 4M)
   __shared__ uint32_t wsum[kBktThreads / 64 + 1];
   __shared__ uint32_t distinct, bc;
   __shared__ int over;
   __shared__ u64 bq;
-  int const tid  = threadIdx.x;
-  u64 const jb   = p.bblocks[blockIdx.x];
-  uint32_t const j = (uint32_t)(jb >> 32), b = (uint32_t)jb;
-  big_row const rw = p.rows[j];
-  int const nbk    = 1 << rw.logb;
-  int const ns     = (int)(rw.send - rw.sbeg);
+  int const tid      = threadIdx.x;
+  big_bblk const bk  = p.bblk[blockIdx.x];
+  int const nbk      = 1 << bk.logb;
+  int const ns       = (int)bk.ns;
+  uint32_t const b   = bk.b;
   // row data first: independent of the partials, in flight meanwhile
-  uint32_t const u  = rw.row;
-  uint32_t const cu = p.c[u + p.base];
-  double const kv   = p.k[u], a_old = p.a[cu], self = p.self[u];
-  double const old_s = (double)(long long)p.own[j] * p.inv_scale - self;
-  for (int i = tid; i < ns; i += kBktThreads) {
-    big_seg const sg = p.segs[rw.sbeg + i];
-    int32_t const lo = p.boffs[sg.boff + b], hi = p.boffs[sg.boff + b + 1];
-    pre[i]           = (uint32_t)(hi - lo);
-    start[i]         = sg.pbase + lo;
-  }
+  uint32_t const u   = bk.u;
+  uint32_t const cu  = p.c[u + p.base];
+  double const kv    = p.k[u], self = p.self[u];
+  u64 const ownj     = p.own[bk.j];
+  double const a_old = p.a[cu];
   if (tid == 0) {
     distinct = 0;
     over     = 0;
     bq       = 0;
     bc       = kEmpty32;
   }
-  __syncthreads();
-  uint32_t const total = block_excl_scan<kBktThreads, kBigMaxSegs / kBktThreads>(pre, ns, wsum);
-  int bits             = 6;  // 2^bits >= 2 * partials slots, at most kBktSlots (then the cap guards)
-  while ((1 << bits) < kBktSlots && (1u << bits) < 2 * total) ++bits;
-  int const nslot     = 1 << bits;
-  unsigned const mask = (unsigned)nslot - 1;
+  // the segments' runs of bucket b, kBktSegGroup segments at a time (one group below
+  // 1M-edge rows, so the table is sized by its partials)
+  int bits            = 6;  // 2^bits >= 2 * partials slots, at most kBktSlots (then the cap guards)
+  int nslot           = 0;
+  unsigned mask       = 0;
   int const cap       = p.cap;  // below kBktSlots slots total <= nslot / 2: never full
-  for (int i = tid; i < nslot; i += kBktThreads) {
-    key[i] = kEmpty32;
-    val[i] = 0;
-  }
-  __syncthreads();
-  constexpr int kPPT = 4;  // partials per thread per batch, loaded before their inserts
-  bool stop          = false;
-  for (uint32_t f0 = 0; f0 < total && !stop; f0 += kPPT * kBktThreads) {
-    uint32_t kq[kPPT];
-    u64 vq[kPPT];
-#pragma unroll
-    for (int q = 0; q < kPPT; ++q) {
-      uint32_t const f = f0 + tid + q * kBktThreads;
-      if (f >= total) break;
-      int lo = 0, hi = ns - 1;  // last segment with pre <= f
-      while (lo < hi) {
-        int const mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= f) lo = mid;
-        else hi = mid - 1;
-      }
-      int64_t const x = start[lo] + (f - pre[lo]);
-      kq[q]           = p.pkey[x];
-      vq[q]           = p.pval[x];
+  bool stop           = false;
+  for (int g0 = 0; g0 < ns; g0 += kBktSegGroup) {
+    int const gn = ns - g0 < kBktSegGroup ? ns - g0 : kBktSegGroup;
+    for (int i = tid; i < gn; i += kBktThreads) {
+      int64_t const o  = bk.ob + (int64_t)(g0 + i) * (nbk + 1) + b;
+      int32_t const lo = p.boffs[o], hi = p.boffs[o + 1];
+      pre[i]           = (uint32_t)(hi - lo);
+      start[i]         = (uint32_t)((g0 + i) * kBigSeg + lo);
     }
+    __syncthreads();
+    uint32_t const total = block_excl_scan<kBktThreads, kBktSegGroup / kBktThreads>(pre, gn, wsum);
+    if (g0 == 0) {
+      if (ns > kBktSegGroup) bits = 12;
+      while ((1 << bits) < kBktSlots && (1u << bits) < 2 * total) ++bits;
+      nslot = 1 << bits;
+      mask  = (unsigned)nslot - 1;
+      for (int i = tid; i < nslot; i += kBktThreads) {
+        key[i] = kEmpty32;
+        val[i] = 0;
+      }
+      __syncthreads();
+    }
+    constexpr int kPPT = 4;  // partials per thread per batch, loaded before their inserts
+    for (uint32_t f0 = 0; f0 < total && !stop; f0 += kPPT * kBktThreads) {
+      uint32_t kq[kPPT];
+      u64 vq[kPPT];
 #pragma unroll
-    for (int q = 0; q < kPPT; ++q) {
-      if (stop || f0 + tid + q * kBktThreads >= total) break;
-      uint32_t const cc = kq[q];
-      unsigned h        = slot32(cc, bits);
-      while (true) {
-        uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
-        if (prev == kEmpty32 || prev == cc) {
-          atomicAdd(&val[h], vq[q]);
-          if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= cap) {
-            over = 1;
-            stop = true;
-          }
-          break;
+      for (int q = 0; q < kPPT; ++q) {
+        uint32_t const f = f0 + tid + q * kBktThreads;
+        if (f >= total) break;
+        int lo = 0, hi = gn - 1;  // last segment with pre <= f
+        while (lo < hi) {
+          int const mid = (lo + hi + 1) >> 1;
+          if (pre[mid] <= f) lo = mid;
+          else hi = mid - 1;
         }
-        h = (h + 1) & mask;
+        int64_t const x = bk.pb + start[lo] + (f - pre[lo]);
+        kq[q]           = p.pkey[x];
+        vq[q]           = p.pval[x];
+      }
+#pragma unroll
+      for (int q = 0; q < kPPT; ++q) {
+        if (stop || f0 + tid + q * kBktThreads >= total) break;
+        uint32_t const cc = kq[q];
+        unsigned h        = slot32(cc, bits);
+        while (true) {
+          uint32_t const prev = atomicCAS(&key[h], kEmpty32, cc);
+          if (prev == kEmpty32 || prev == cc) {
+            atomicAdd(&val[h], vq[q]);
+            if (prev == kEmpty32 && (int)atomicAdd(&distinct, 1u) >= cap) {
+              over = 1;
+              stop = true;
+            }
+            break;
+          }
+          h = (h + 1) & mask;
+        }
       }
     }
+    __syncthreads();  // pre / start are rewritten by the next group
+    if (over) break;
   }
-  __syncthreads();
   if (over) {
     if (tid == 0) atomicOr(p.overflow, 1);
     return;
   }
+  double const old_s = (double)(long long)ownj * p.inv_scale - self;
   gains_one_row<kBktThreads, kBktSlots>(p, key, val, nslot, cu, old_s, kv, a_old, bq);
   __syncthreads();
   for (int h = tid; h < nslot; h += kBktThreads)
@@ -927,11 +964,11 @@ __global__ __launch_bounds__(kBktThreads) void k_big_buckets(big_args p)
     p.best_q[blockIdx.x] = bq;
     p.best_c[blockIdx.x] = bc;
   }
-  (void)nbk;
 }
 
 __global__ void k_big_move(big_args p)
 {
+  if (*p.overflow) return;  // pass B gave up: the sweep is redone on the sort path
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < p.nrows; j += (int64_t)gridDim.x * blockDim.x) {
     big_row const rw = p.rows[j];
     if (rw.single) continue;
@@ -1033,7 +1070,7 @@ __device__ __forceinline__ int ceil_log2_dev(int64_t x)
 }
 
 __global__ void k_big_plan(int64_t const* rows, int64_t const* off, int64_t n, int64_t maxdeg, int pass,
-                           u64* cnt, u64 const* pos, big_row* brows, big_seg* bsegs, u64* bblocks, int* rest)
+                           u64* cnt, u64 const* pos, big_row* brows, big_seg* bsegs, big_bblk* bblk, int* rest)
 {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     int64_t const r = rows[j], first = off[r], d = off[r + 1] - first;
@@ -1073,7 +1110,18 @@ __global__ void k_big_plan(int64_t const* rows, int64_t const* off, int64_t n, i
       sg.pad   = 0;
       bsegs[sb + q] = sg;
     }
-    for (int64_t b = 0; b < nbk; ++b) bblocks[bb + b] = ((u64)j << 32) | (u64)b;
+    for (int64_t b = 0; b < nbk; ++b) {
+      big_bblk k;
+      k.ob         = ob;
+      k.pb         = pb;
+      k.j          = (uint32_t)j;
+      k.u          = (uint32_t)r;
+      k.b          = (uint32_t)b;
+      k.ns         = (uint32_t)nseg;
+      k.logb       = (uint32_t)logb;
+      k.pad        = 0;
+      bblk[bb + b] = k;
+    }
   }
 }
 
@@ -1368,7 +1416,8 @@ struct sweep_plan {
   int64_t nbig = 0, nsegs = 0, nbblocks = 0;
   dbuf<big_row> brows;
   dbuf<big_seg> bsegs;
-  dbuf<u64> bblocks, own, best_q;
+  dbuf<big_bblk> bblocks;
+  dbuf<u64> own, best_q;
   dbuf<uint32_t> best_c, pkey;
   dbuf<u64> pval;
   dbuf<int32_t> boffs;
@@ -1413,7 +1462,7 @@ std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P, tuning_t const&
   std::vector<int64_t> rest;
   std::vector<big_row> rows;
   std::vector<big_seg> segs;
-  std::vector<u64> bb;
+  std::vector<big_bblk> bb;
   int64_t pstart = 0, boff = 0;
   int64_t const md     = tu.louvain_big_maxdeg;  // tests: a lower limit
   int64_t const maxdeg = std::min<int64_t>(md > 0 ? md : INT64_MAX, (int64_t)kBigMaxBuckets * kBktCap * 4 / 5);
@@ -1448,7 +1497,9 @@ std::vector<int64_t> plan_big_rows(hipStream_t s, sweep_plan& P, tuning_t const&
     rw.send   = (uint32_t)segs.size();
     rw.single = single ? 1u : 0u;
     if (!single)
-      for (int b = 0; b < (1 << logb); ++b) bb.push_back(((u64)j << 32) | (u64)b);
+      for (int b = 0; b < (1 << logb); ++b)
+        bb.push_back(big_bblk{segs[rw.sbeg].boff, segs[rw.sbeg].pbase, (uint32_t)j, (uint32_t)r, (uint32_t)b,
+                              (uint32_t)nseg, (uint32_t)logb, 0u});
     pstart += d;
   }
   int64_t const nb = (int64_t)rows.size();
@@ -1487,7 +1538,7 @@ bool plan_big_rows_device(hipStream_t s, sweep_plan& P, tuning_t const& tu)
   fill<int>(rest.data(), 1, 0, s);
   unsigned const g = grid_for(n, kBlock, 16384);
   hipLaunchKernelGGL(k_big_plan, dim3(g), dim3(kBlock), 0, s, P.bigd.data(), P.off, n, maxdeg, 0, cnt.data(),
-                     (u64 const*)nullptr, (big_row*)nullptr, (big_seg*)nullptr, (u64*)nullptr, rest.data());
+                     (u64 const*)nullptr, (big_row*)nullptr, (big_seg*)nullptr, (big_bblk*)nullptr, rest.data());
   CGX_LAUNCH_CHECK();
   for (int q = 0; q < 4; ++q)
     exclusive_scan<u64, u64>(cnt.data() + q * (n + 1), pos.data() + q * (n + 1), (size_t)(n + 1), s);
@@ -1639,7 +1690,6 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     sweep_sorted(S, g, g.src.data(), g.dst.data(), g.w.data(), g.ne, c, next, k, self, a, present, up_down, own);
     return;
   }
-  bool sorted_all = false;
   if (P.big_hash) {
     big_args ba{g.dst.data(), g.w.data(), c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
                 P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, present, k, S.m, S.gamma,
@@ -1651,19 +1701,12 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     CGX_LAUNCH_CHECK();
     if (P.nbblocks) hipLaunchKernelGGL(k_big_buckets, dim3((unsigned)P.nbblocks), dim3(kBktThreads), 0, s, ba);
     CGX_LAUNCH_CHECK();
-    if (to_host_scalar(P.overflow.data(), s) == 0) {
-      hipLaunchKernelGGL(k_big_move, dim3(blocks(P.nbig)), dim3(kBlock), 0, s, ba);
-      CGX_LAUNCH_CHECK();
-    } else {
-      P.big_hash = false;  // a bucket outgrew its table: this level's heavy rows use the sort path
-      HIP_CHECK(hipMemcpyAsync(next, c + g.base, g.nrows * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-      big_rows_to_host(s, P);
-      build_sort_coo(s, g, P, P.big);
-      sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down, own);
-      sorted_all = true;
-    }
+    // moves nothing when a bucket outgrew its table (the flag is read after the sweep:
+    // no host round trip between the heavy and the light rows)
+    hipLaunchKernelGGL(k_big_move, dim3(blocks(P.nbig)), dim3(kBlock), 0, s, ba);
+    CGX_LAUNCH_CHECK();
   }
-  if (P.e_big && !sorted_all)
+  if (P.e_big)
     sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down, own);
   if (P.nchunks) {
     hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), c, (uint32_t)g.base, self, a,
@@ -1674,6 +1717,14 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     else
       hipLaunchKernelGGL(k_sweep_hash<u64>, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
     CGX_LAUNCH_CHECK();
+  }
+  if (P.big_hash && to_host_scalar(P.overflow.data(), s) != 0) {
+    // a bucket outgrew its table: this level's heavy rows take the sort path, and the
+    // sweep runs again from the start (never seen on R-MAT)
+    P.big_hash = false;
+    big_rows_to_host(s, P);
+    build_sort_coo(s, g, P, P.big);
+    sweep(S, g, P, c, next, k, self, a, present, up_down, own);
   }
 }
 
