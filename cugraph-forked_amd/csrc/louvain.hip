@@ -300,10 +300,14 @@ __global__ void k_to_vertex(uint32_t const* x, int64_t n, V* out)
 // order-independent, and exact for integer weights, so the gains are the same IEEE
 // values as the sort path's and the oracle's.  Replaces key build + radix sort +
 // two reduce_by_key passes (~20 B of HBM traffic per edge per pass) by one pass
-// over the edges.  Small blocks (256 threads, ~34 KB of LDS with 32-bit pair keys:
-// 4 per CU) so that one block's gathers overlap another's LDS phases.
+// over the edges.  Small blocks (256 threads, 30 KB of LDS with 32-bit pair keys: 5
+// per CU) so that one block's gathers overlap another's LDS phases; the grid is
+// persistent, each block loading its next chunk's edges while it works on the current
+// one (RMAT-23 level 0: a chunk holds ~36 rows, so 128 rows per chunk rarely binds).
 constexpr int kHashEdges   = 1024;
-constexpr int kHashRows    = 256;
+constexpr int kHashRows    = 128;  // row arrays 5 KB: 5 blocks per CU
+constexpr int kHashResident = 5;    // resident blocks per CU (the persistent grid)
+constexpr int kCUs          = 256;  // MI355X
 constexpr int kHashSlots   = 2048;
 constexpr int kHashThreads = 256;
 
@@ -312,12 +316,13 @@ struct hash_sweep_args {
   uint32_t const* dst;
   double const* w;
   int64_t const* off;
-  int64_t const* chunks;  // 2 per chunk: first row, end row
+  int64_t const* chunks;  // 4 per chunk: first row, end row, first edge, end edge
+  int64_t nchunks;
   uint32_t const* c;
   uint32_t base;
   double const* self;
   double const* a;
-  uint8_t const* present;
+  double const* ag;  // gain weights: a[c] for a present cluster, FLT_MAX otherwise (one gather)
   double const* k;
   double m, gamma, scale, inv_scale;
   uint32_t* next;
@@ -358,61 +363,97 @@ __device__ inline double unorder_bits(u64 o)
 }
 
 template <typename K>
-__global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
+__global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_sweep_hash(
+  hash_sweep_args p)
 {
 #pragma clang fp contract(off)
   using PK = pair_key<K>;
+  constexpr int kEPT = kHashEdges / kHashThreads;
   __shared__ K key[kHashSlots];
   __shared__ u64 val[kHashSlots];
   __shared__ uint32_t r_cu[kHashRows], r_bc[kHashRows];
   __shared__ double r_k[kHashRows], r_aold[kHashRows], r_old[kHashRows];
   __shared__ u64 r_best[kHashRows];
-  int const tid    = threadIdx.x;
-  int64_t const r0 = p.chunks[2 * blockIdx.x], r1 = p.chunks[2 * blockIdx.x + 1];
-  int const nrow   = (int)(r1 - r0);
-  int64_t const e0 = p.off[r0], e1 = p.off[r1];
-  int bits         = 6;  // table of 2^bits >= 2 * edges slots
-  while ((1 << bits) < 2 * (int)(e1 - e0)) ++bits;
-  int const nslot     = 1 << bits;
-  unsigned const mask = (unsigned)nslot - 1;
-  for (int i = tid; i < nslot; i += kHashThreads) {
-    key[i] = PK::empty;
-    val[i] = 0;
-  }
-  // thread t owns row t of the chunk
-  bool const has_row = tid < nrow;
-  int64_t const u    = r0 + tid;
-  uint32_t cu        = 0;
-  double self        = 0.0;
-  if (has_row) {
-    cu           = p.c[u + p.base];
-    self         = p.self[u];
-    r_cu[tid]    = cu;
-    r_k[tid]     = p.k[u];
-    r_aold[tid]  = p.a[cu];
-    r_old[tid]   = 0.0;
-    r_best[tid]  = 0;
-    r_bc[tid]    = 0xffffffffu;
-  }
-  __syncthreads();
-  {
-    // all of this thread's edges (<= kEPT) loaded, then their clusters, then the
-    // inserts: the gathers overlap instead of waiting behind each CAS loop
-    constexpr int kEPT = kHashEdges / kHashThreads;
-    uint32_t ri[kEPT], dv[kEPT];
-    double wv[kEPT];
+  int const tid = threadIdx.x;
+  // Persistent blocks: chunk ch is processed while the edges of the block's next chunk
+  // (and the record of the one after) are in flight, so a chunk waits on its cluster
+  // and gain gathers only, not on its edge loads.
+  int64_t ch = blockIdx.x;
+  if (ch >= p.nchunks) return;
+  int64_t const* rc = p.chunks + 4 * ch;
+  int64_t r0 = rc[0], r1 = rc[1], e0 = rc[2], e1 = rc[3];
+  uint32_t ri[kEPT], dv[kEPT];
+  double wv[kEPT];
 #pragma unroll
-    for (int q = 0; q < kEPT; ++q) {
-      int64_t const e = e0 + tid + q * kHashThreads;
-      if (e < e1) {
-        ri[q] = p.src[e] - (uint32_t)r0;
-        dv[q] = p.dst[e];
-        wv[q] = p.w[e];
-      }
+  for (int q = 0; q < kEPT; ++q) {
+    int64_t const e = e0 + tid + q * kHashThreads;
+    if (e < e1) {
+      ri[q] = p.src[e] - (uint32_t)r0;
+      dv[q] = p.dst[e];
+      wv[q] = p.w[e];
     }
+  }
+  int64_t nch = ch + gridDim.x;
+  int64_t n0 = 0, n1 = 0, ne0 = 0, ne1 = 0;  // the next chunk's record
+  if (nch < p.nchunks) {
+    rc  = p.chunks + 4 * nch;
+    n0  = rc[0];
+    n1  = rc[1];
+    ne0 = rc[2];
+    ne1 = rc[3];
+  }
+  while (true) {
+    int const nrow = (int)(r1 - r0);
+    int bits       = 6;  // table of 2^bits >= 2 * edges slots
+    while ((1 << bits) < 2 * (int)(e1 - e0)) ++bits;
+    int const nslot     = 1 << bits;
+    unsigned const mask = (unsigned)nslot - 1;
+    // this chunk's clusters, then the next chunk's edges and the record after it
 #pragma unroll
     for (int q = 0; q < kEPT; ++q)
       if (e0 + tid + q * kHashThreads < e1) dv[q] = p.c[dv[q]];
+    uint32_t nri[kEPT], ndv[kEPT];
+    double nwv[kEPT];
+    if (nch < p.nchunks) {
+#pragma unroll
+      for (int q = 0; q < kEPT; ++q) {
+        int64_t const e = ne0 + tid + q * kHashThreads;
+        if (e < ne1) {
+          nri[q] = p.src[e] - (uint32_t)n0;
+          ndv[q] = p.dst[e];
+          nwv[q] = p.w[e];
+        }
+      }
+    }
+    int64_t const nnch = nch + gridDim.x;
+    int64_t m0 = 0, m1 = 0, me0 = 0, me1 = 0;
+    if (nnch < p.nchunks) {
+      rc  = p.chunks + 4 * nnch;
+      m0  = rc[0];
+      m1  = rc[1];
+      me0 = rc[2];
+      me1 = rc[3];
+    }
+    for (int i = tid; i < nslot; i += kHashThreads) {
+      key[i] = PK::empty;
+      val[i] = 0;
+    }
+    // thread t owns row t of the chunk
+    bool const has_row = tid < nrow;
+    int64_t const u    = r0 + tid;
+    uint32_t cu        = 0;
+    double self        = 0.0;
+    if (has_row) {
+      cu          = p.c[u + p.base];
+      self        = p.self[u];
+      r_cu[tid]   = cu;
+      r_k[tid]    = p.k[u];
+      r_aold[tid] = p.a[cu];
+      r_old[tid]  = 0.0;
+      r_best[tid] = 0;
+      r_bc[tid]   = 0xffffffffu;
+    }
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
       if (e0 + tid + q * kHashThreads >= e1) break;
@@ -428,71 +469,87 @@ __global__ __launch_bounds__(kHashThreads) void k_sweep_hash(hash_sweep_args p)
         h = (h + 1) & mask;
       }
     }
-  }
-  __syncthreads();
-  // weight into the own cluster, self loop excluded (k_old_sum)
-  if (has_row) {
-    K const kk = PK::make(tid, cu);
-    unsigned h = PK::slot(kk, bits);
-    double own = 0.0;
-    while (key[h] != PK::empty) {
-      if (key[h] == kk) {
-        own        = (double)(long long)val[h] * p.inv_scale;
-        r_old[tid] = own - self;
-        break;
+    __syncthreads();
+    // weight into the own cluster, self loop excluded (k_old_sum)
+    if (has_row) {
+      K const kk = PK::make(tid, cu);
+      unsigned h = PK::slot(kk, bits);
+      double own = 0.0;
+      while (key[h] != PK::empty) {
+        if (key[h] == kk) {
+          own        = (double)(long long)val[h] * p.inv_scale;
+          r_old[tid] = own - self;
+          break;
+        }
+        h = (h + 1) & mask;
       }
-      h = (h + 1) & mask;
+      p.own[u] = own;
     }
-    p.own[u] = own;
-  }
-  __syncthreads();
-  // gains (k_gain), per-row maximum.  For the own cluster s = sum - self = old_s,
-  // the same IEEE value as k_gain's.
-  {
-    constexpr int kSPT = kHashSlots / kHashThreads;
-    double an[kSPT];
-    uint8_t pr[kSPT];
+    __syncthreads();
+    // gains (k_gain), per-row maximum.  For the own cluster s = sum - self = old_s,
+    // the same IEEE value as k_gain's.
+    {
+      constexpr int kSPT = kHashSlots / kHashThreads;
+      double an[kSPT];
 #pragma unroll
-    for (int q = 0; q < kSPT; ++q) {  // the neighbour clusters' weights, all in flight
-      int const h = tid + q * kHashThreads;
-      K const kk  = h < nslot ? key[h] : PK::empty;
-      if (kk != PK::empty) {
+      for (int q = 0; q < kSPT; ++q) {  // the neighbour clusters' gain weights, all in flight
+        int const h = tid + q * kHashThreads;
+        K const kk  = h < nslot ? key[h] : PK::empty;
+        if (kk != PK::empty) {
+          uint32_t const cc = PK::cluster(kk);
+          an[q]             = p.ag[cc];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kSPT; ++q) {
+        int const h = tid + q * kHashThreads;
+        if (h >= nslot) break;
+        K const kk = key[h];
+        if (kk == PK::empty) continue;
+        int const i       = PK::row(kk);
         uint32_t const cc = PK::cluster(kk);
-        pr[q]             = p.present[cc];
-        an[q]             = p.a[cc];
+        double s          = cc == r_cu[i] ? r_old[i] : (double)(long long)val[h] * p.inv_scale;
+        double a_new      = an[q];
+        double a_old      = r_aold[i];
+        double kv         = r_k[i];
+        double dq = 2.0 * (((s - r_old[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
+        u64 const o = order_bits(dq);
+        val[h]      = o;
+        atomicMax(&r_best[i], o);
       }
     }
-#pragma unroll
-    for (int q = 0; q < kSPT; ++q) {
-      int const h = tid + q * kHashThreads;
-      if (h >= nslot) break;
+    __syncthreads();
+    // ties: the smaller cluster (best_gain_op)
+    for (int h = tid; h < nslot; h += kHashThreads) {
       K const kk = key[h];
       if (kk == PK::empty) continue;
-      int const i       = PK::row(kk);
-      uint32_t const cc = PK::cluster(kk);
-      double s          = cc == r_cu[i] ? r_old[i] : (double)(long long)val[h] * p.inv_scale;
-      double a_new      = pr[q] ? an[q] : (double)FLT_MAX;
-      double a_old      = r_aold[i];
-      double kv         = r_k[i];
-      double dq = 2.0 * (((s - r_old[i]) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
-      u64 const o = order_bits(dq);
-      val[h]      = o;
-      atomicMax(&r_best[i], o);
+      int const i = PK::row(kk);
+      if (val[h] == r_best[i]) atomicMin(&r_bc[i], PK::cluster(kk));
     }
-  }
-  __syncthreads();
-  // ties: the smaller cluster (best_gain_op)
-  for (int h = tid; h < nslot; h += kHashThreads) {
-    K const kk = key[h];
-    if (kk == PK::empty) continue;
-    int const i = PK::row(kk);
-    if (val[h] == r_best[i]) atomicMin(&r_bc[i], PK::cluster(kk));
-  }
-  __syncthreads();
-  if (has_row && r_best[tid] != 0) {
-    double const dq  = unorder_bits(r_best[tid]);
-    uint32_t const b = r_bc[tid];
-    if (dq > 0.0 && ((b > cu) == p.up_down)) p.next[u] = b;
+    __syncthreads();
+    if (has_row && r_best[tid] != 0) {
+      double const dq  = unorder_bits(r_best[tid]);
+      uint32_t const b = r_bc[tid];
+      if (dq > 0.0 && ((b > cu) == p.up_down)) p.next[u] = b;
+    }
+    if (nch >= p.nchunks) break;
+    __syncthreads();  // the table and the row arrays are cleared for the next chunk
+    ch = nch;
+    r0 = n0;
+    r1 = n1;
+    e0 = ne0;
+    e1 = ne1;
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      ri[q] = nri[q];
+      dv[q] = ndv[q];
+      wv[q] = nwv[q];
+    }
+    nch = nnch;
+    n0  = m0;
+    n1  = m1;
+    ne0 = me0;
+    ne1 = me1;
   }
 }
 
@@ -605,7 +662,7 @@ struct big_args {
   big_bblk const* bblk;
   double const* self;
   double const* a;
-  uint8_t const* present;
+  double const* ag;  // gain weights (hash_sweep_args::ag)
   double const* k;
   double m, gamma, scale, inv_scale;
   u64* best_q;
@@ -676,16 +733,12 @@ __device__ void gains_one_row(big_args const& p, uint32_t const* key, u64* val, 
   constexpr int kSPT = S / T;
   int const tid      = threadIdx.x;
   double an[kSPT];
-  uint8_t pr[kSPT];
   u64 tmax = 0;
 #pragma unroll
   for (int q = 0; q < kSPT; ++q) {
     int const h       = tid + q * T;
     uint32_t const cc = h < nslot ? key[h] : kEmpty32;
-    if (cc != kEmpty32) {
-      pr[q] = p.present[cc];
-      an[q] = p.a[cc];
-    }
+    if (cc != kEmpty32) an[q] = p.ag[cc];
   }
 #pragma unroll
   for (int q = 0; q < kSPT; ++q) {
@@ -694,7 +747,7 @@ __device__ void gains_one_row(big_args const& p, uint32_t const* key, u64* val, 
     uint32_t const cc = key[h];
     if (cc == kEmpty32) continue;
     double s     = cc == cu ? old_s : (double)(long long)val[h] * p.inv_scale;
-    double a_new = pr[q] ? an[q] : (double)FLT_MAX;
+    double a_new = an[q];
     double dq    = 2.0 * (((s - old_s) / p.m) - p.gamma * (a_new * kv - a_old * kv + kv * kv) / (p.m * p.m));
     u64 const o  = order_bits(dq);
     val[h]       = o;
@@ -1002,44 +1055,38 @@ __global__ void k_chunk_walk(int64_t const* off, int64_t nr, int pass, uint32_t*
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nblk; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t const rb = t * kHashRows, re = rb + kHashRows < nr ? rb + kHashRows : nr;
     int64_t nc = 0, nb = 0, r0 = rb, ce = 0;
-    int64_t* co = pass ? chunks + 2 * cpos[t] : nullptr;
+    int64_t* co = pass ? chunks + 4 * cpos[t] : nullptr;
     int64_t* bo = pass ? bigrows + bpos[t] : nullptr;
-    int64_t lo = off[rb];
+    int64_t lo  = off[rb];
+    auto emit   = [&](int64_t a, int64_t b, int64_t eb) {  // rows [a, b), edges [eb - ce, eb)
+      if (pass) {
+        co[4 * nc]     = a;
+        co[4 * nc + 1] = b;
+        co[4 * nc + 2] = eb - ce;
+        co[4 * nc + 3] = eb;
+      }
+      ++nc;
+    };
     for (int64_t r = rb; r < re; ++r) {
       int64_t const hi = off[r + 1], d = hi - lo;
-      lo               = hi;
       if (d > kHashEdges) {
-        if (ce > 0) {
-          if (pass) {
-            co[2 * nc]     = r0;
-            co[2 * nc + 1] = r;
-          }
-          ++nc;
-        }
+        if (ce > 0) emit(r0, r, lo);
         if (pass) bo[nb] = r;
         ++nb;
         ce = 0;
         r0 = r + 1;
+        lo = hi;
         continue;
       }
       if (ce + d > kHashEdges) {
-        if (pass) {
-          co[2 * nc]     = r0;
-          co[2 * nc + 1] = r;
-        }
-        ++nc;
+        emit(r0, r, lo);
         ce = 0;
         r0 = r;
       }
       ce += d;
+      lo = hi;
     }
-    if (ce > 0) {
-      if (pass) {
-        co[2 * nc]     = r0;
-        co[2 * nc + 1] = re;
-      }
-      ++nc;
-    }
+    if (ce > 0) emit(r0, re, lo);
     if (!pass) {
       ccount[t] = (uint32_t)nc;
       bcount[t] = (uint32_t)nb;
@@ -1424,6 +1471,7 @@ struct sweep_plan {
   dbuf<int> overflow;
   std::vector<int64_t> big, big_first, big_deg;  // every heavy row (host; filled when a host plan needs them)
   dbuf<int64_t> bigd;                            // the heavy rows, ascending (device)
+  dbuf<double> ag;                               // the sweep's gain weights (k_gain_weights)
   int64_t tb = 0;
 };
 
@@ -1637,7 +1685,7 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, u64
   auto const th    = to_host(tot.data(), 2, s);
   int64_t const tc = th[0], tb = th[1];
   P.nchunks        = tc;
-  P.chunks.resize(std::max<int64_t>(2 * tc, 1), s);
+  P.chunks.resize(std::max<int64_t>(4 * tc, 1), s);
   P.bigd.resize(std::max<int64_t>(tb, 1), s);
   P.tb = tb;
   hipLaunchKernelGGL(k_chunk_walk, dim3(wg), dim3(kBlock), 0, s, off, nr, 1, cc.data(), bc.data(), cp.data(), bp.data(),
@@ -1675,10 +1723,17 @@ void plan_sweeps(louvain_state& S, level_graph const& g, int64_t const* off, u64
   }
 }
 
+__global__ void k_gain_weights(double const* a, uint8_t const* present, int64_t n, double* ag)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ag[i] = present[i] ? a[i] : (double)FLT_MAX;
+}
+
 // one synchronous local-move sweep (update_clustering_by_delta_modularity) over
 // this rank's rows; next[row] = the row's cluster after the sweep
 void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const* c, uint32_t* next,
-           double const* k, double const* self, double const* a, uint8_t const* present, bool up_down, double* own)
+           double const* k, double const* self, double const* a, uint8_t const* present, int64_t na, bool up_down,
+           double* own)
 {
   hipStream_t s = S.s;
   if (g.nrows) {
@@ -1690,9 +1745,14 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     sweep_sorted(S, g, g.src.data(), g.dst.data(), g.w.data(), g.ne, c, next, k, self, a, present, up_down, own);
     return;
   }
+  // the gain weights of this sweep's clusters: one 8-byte gather per (row, cluster)
+  // pair where a and present took two
+  if (P.ag.n < (size_t)std::max<int64_t>(na, 1)) P.ag.resize(std::max<int64_t>(na, 1), s);
+  if (na) hipLaunchKernelGGL(k_gain_weights, dim3(blocks(na)), dim3(kBlock), 0, s, a, present, na, P.ag.data());
+  CGX_LAUNCH_CHECK();
   if (P.big_hash) {
     big_args ba{g.dst.data(), g.w.data(), c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
-                P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, present, k, S.m, S.gamma,
+                P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, P.ag.data(), k, S.m, S.gamma,
                 P.scale, P.inv_scale, P.best_q.data(), P.best_c.data(), P.overflow.data(), big_bucket_cap(S.tune), next,
                 up_down, own};
     fill<u64>(P.own.data(), P.nbig, 0ull, s);
@@ -1709,13 +1769,16 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
   if (P.e_big)
     sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down, own);
   if (P.nchunks) {
-    hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), c, (uint32_t)g.base, self, a,
-                       present, k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down, own};
+    hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), P.nchunks, c, (uint32_t)g.base,
+                       self, a, P.ag.data(), k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down, own};
+    // persistent blocks: the resident count (5 per CU at 30 KB of LDS)
+    unsigned const hg  = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)kHashResident * kCUs);
+    unsigned const hgw = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(kHashResident - 1) * kCUs);  // 38 KB
     bool const wide = S.tune.louvain_wide_keys;  // tests of the 64-bit keys
     if (g.nv < (1 << 24) - 1 && !wide)
-      hipLaunchKernelGGL(k_sweep_hash<uint32_t>, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
+      hipLaunchKernelGGL(k_sweep_hash<uint32_t>, dim3(hg), dim3(kHashThreads), 0, s, ha);
     else
-      hipLaunchKernelGGL(k_sweep_hash<u64>, dim3((unsigned)P.nchunks), dim3(kHashThreads), 0, s, ha);
+      hipLaunchKernelGGL(k_sweep_hash<u64>, dim3(hgw), dim3(kHashThreads), 0, s, ha);
     CGX_LAUNCH_CHECK();
   }
   if (P.big_hash && to_host_scalar(P.overflow.data(), s) != 0) {
@@ -1724,7 +1787,7 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
     P.big_hash = false;
     big_rows_to_host(s, P);
     build_sort_coo(s, g, P, P.big);
-    sweep(S, g, P, c, next, k, self, a, present, up_down, own);
+    sweep(S, g, P, c, next, k, self, a, present, na, up_down, own);
   }
 }
 
@@ -1909,7 +1972,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
     // every sweep also returns the internal weight of the clustering it started from
     // (modularity_own): sweep k + 1 runs before the loop decides on clustering k
     bool up_down = true;
-    sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down,
+    sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), nv, up_down,
           own.data());
     double new_q = modularity_own(S, cur, own.data(), a.data(), present.data());
     lap("setup", nv, cur.ne, new_q);
@@ -1924,7 +1987,7 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
                          a.data(), present.data());
       CGX_LAUNCH_CHECK();
       up_down = !up_down;
-      sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), up_down,
+      sweep(S, cur, plan, clusters.data(), next.data(), k.data(), self.data(), a.data(), present.data(), nv, up_down,
             own.data());
       new_q = modularity_own(S, cur, own.data(), a.data(), present.data());
       if (new_q > cur_q)
@@ -2835,7 +2898,7 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
     S.bytes          = 0;
     mg_view(S, L, all_present, W);
     phase("view", sweeps);
-    sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), up_down,
+    sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), W.ncl, up_down,
           own.data());
     phase("sweep", sweeps);
     double new_q = mg_modularity(S, L, own.data(), all_present);
@@ -2854,7 +2917,8 @@ void mg_louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolutio
       up_down     = !up_down;
       mg_view(S, L, all_present, W);
       phase("view", sweeps);
-      sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), up_down,
+      sweep(S, cur, plan, W.c_loc.data(), next.data(), k.data(), self.data(), W.a.data(), W.present.data(), W.ncl,
+            up_down,
             own.data());
       phase("sweep", sweeps);
       new_q = mg_modularity(S, L, own.data(), all_present);
