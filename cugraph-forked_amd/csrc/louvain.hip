@@ -61,6 +61,7 @@ struct level_graph {
   int64_t base = 0, nrows = 0;
   dbuf<uint32_t> src, dst;  // sorted by (src, dst)
   dbuf<double> w;
+  float const* wf = nullptr;  // level 0 of fp32 input: the same weights as fp32 (the graph's own array)
 };
 
 struct gain_t {
@@ -312,9 +313,9 @@ constexpr int kHashSlots   = 2048;
 constexpr int kHashThreads = 256;
 
 struct hash_sweep_args {
-  uint32_t const* src;
   uint32_t const* dst;
   double const* w;
+  float const* wf;  // when set, the weights as read (fp32 input at level 0: 4 bytes an edge fewer)
   int64_t const* off;
   int64_t const* chunks;  // 4 per chunk: first row, end row, first edge, end edge
   int64_t nchunks;
@@ -362,8 +363,24 @@ __device__ inline double unorder_bits(u64 o)
   return __longlong_as_double((long long)((o >> 63) ? (o & 0x7fffffffffffffffull) : ~o));
 }
 
-template <typename K>
-__global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5, 5))) void k_sweep_hash(
+// WT: the weight type read (float: hash_sweep_args::wf, double: w)
+template <typename WT>
+__device__ __forceinline__ WT const* sweep_weights(hash_sweep_args const& p);
+template <>
+__device__ __forceinline__ float const* sweep_weights<float>(hash_sweep_args const& p)
+{
+  return p.wf;
+}
+template <>
+__device__ __forceinline__ double const* sweep_weights<double>(hash_sweep_args const& p)
+{
+  return p.w;
+}
+
+// (5 waves per SIMD: 5 blocks per CU at 30 KB; the fp64-weight form spills at 5)
+template <typename K, typename WT>
+__global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(sizeof(WT) == 4 ? 5 : 4, 5))) void
+k_sweep_hash(
   hash_sweep_args p)
 {
 #pragma clang fp contract(off)
@@ -374,6 +391,7 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5,
   __shared__ uint32_t r_cu[kHashRows], r_bc[kHashRows];
   __shared__ double r_k[kHashRows], r_aold[kHashRows], r_old[kHashRows];
   __shared__ u64 r_best[kHashRows];
+  __shared__ uint32_t r_off[kHashRows + 1];  // the rows' first edges, from the chunk's first
   int const tid = threadIdx.x;
   // Persistent blocks: chunk ch is processed while the edges of the block's next chunk
   // (and the record of the one after) are in flight, so a chunk waits on its cluster
@@ -382,15 +400,18 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5,
   if (ch >= p.nchunks) return;
   int64_t const* rc = p.chunks + 4 * ch;
   int64_t r0 = rc[0], r1 = rc[1], e0 = rc[2], e1 = rc[3];
-  uint32_t ri[kEPT], dv[kEPT];
-  double wv[kEPT];
+  WT const* const wp = sweep_weights<WT>(p);
+  uint32_t dv[kEPT];
+  WT wv[kEPT];
+  // thread t <= rows holds row t's first edge (an edge's row is found in r_off: no
+  // per-edge row array is read)
+  int64_t ro = tid <= (int)(r1 - r0) ? p.off[r0 + tid] : 0;
 #pragma unroll
   for (int q = 0; q < kEPT; ++q) {
     int64_t const e = e0 + tid + q * kHashThreads;
     if (e < e1) {
-      ri[q] = p.src[e] - (uint32_t)r0;
       dv[q] = p.dst[e];
-      wv[q] = p.w[e];
+      wv[q] = wp[e];
     }
   }
   int64_t nch = ch + gridDim.x;
@@ -412,16 +433,17 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5,
 #pragma unroll
     for (int q = 0; q < kEPT; ++q)
       if (e0 + tid + q * kHashThreads < e1) dv[q] = p.c[dv[q]];
-    uint32_t nri[kEPT], ndv[kEPT];
-    double nwv[kEPT];
+    uint32_t ndv[kEPT];
+    WT nwv[kEPT];
+    int64_t nro = 0;
     if (nch < p.nchunks) {
+      if (tid <= (int)(n1 - n0)) nro = p.off[n0 + tid];
 #pragma unroll
       for (int q = 0; q < kEPT; ++q) {
         int64_t const e = ne0 + tid + q * kHashThreads;
         if (e < ne1) {
-          nri[q] = p.src[e] - (uint32_t)n0;
           ndv[q] = p.dst[e];
-          nwv[q] = p.w[e];
+          nwv[q] = wp[e];
         }
       }
     }
@@ -453,12 +475,20 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5,
       r_best[tid] = 0;
       r_bc[tid]   = 0xffffffffu;
     }
+    if (tid <= nrow) r_off[tid] = (uint32_t)(ro - e0);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
-      if (e0 + tid + q * kHashThreads >= e1) break;
-      K const kk  = PK::make((int)ri[q], dv[q]);
-      u64 const v = (u64)__double2ll_rn(wv[q] * p.scale);
+      int const j = tid + q * kHashThreads;
+      if (e0 + j >= e1) break;
+      int lo = 0, hi = nrow - 1;  // the edge's row: the last with r_off <= j (empty rows share starts)
+      while (lo < hi) {
+        int const mid = (lo + hi + 1) >> 1;
+        if ((int)r_off[mid] <= j) lo = mid;
+        else hi = mid - 1;
+      }
+      K const kk  = PK::make(lo, dv[q]);
+      u64 const v = (u64)__double2ll_rn((double)wv[q] * p.scale);
       unsigned h  = PK::slot(kk, bits);
       while (true) {
         K const prev = atomicCAS(&key[h], PK::empty, kk);
@@ -539,9 +569,9 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(5,
     r1 = n1;
     e0 = ne0;
     e1 = ne1;
+    ro = nro;
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
-      ri[q] = nri[q];
       dv[q] = ndv[q];
       wv[q] = nwv[q];
     }
@@ -650,6 +680,7 @@ struct big_bblk {
 struct big_args {
   uint32_t const* dst;
   double const* w;
+  float const* wf;  // hash_sweep_args::wf
   uint32_t const* c;
   uint32_t base;
   big_seg const* segs;
@@ -840,7 +871,7 @@ __global__ __launch_bounds__(kBigThreads) void k_big_partials(big_args p)
       int64_t const e = sg.e0 + tid + q * kBigThreads;
       if (e < sg.e1) {
         dv[q] = p.dst[e];
-        wv[q] = p.w[e];
+        wv[q] = p.wf ? (double)p.wf[e] : p.w[e];
       }
     }
 #pragma unroll
@@ -1751,7 +1782,7 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
   if (na) hipLaunchKernelGGL(k_gain_weights, dim3(blocks(na)), dim3(kBlock), 0, s, a, present, na, P.ag.data());
   CGX_LAUNCH_CHECK();
   if (P.big_hash) {
-    big_args ba{g.dst.data(), g.w.data(), c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
+    big_args ba{g.dst.data(), g.w.data(), g.wf, c, (uint32_t)g.base, P.bsegs.data(), P.brows.data(), P.nbig, P.pkey.data(),
                 P.pval.data(), P.boffs.data(), P.own.data(), P.bblocks.data(), self, a, P.ag.data(), k, S.m, S.gamma,
                 P.scale, P.inv_scale, P.best_q.data(), P.best_c.data(), P.overflow.data(), big_bucket_cap(S.tune), next,
                 up_down, own};
@@ -1769,16 +1800,20 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
   if (P.e_big)
     sweep_sorted(S, g, P.bsrc, P.bdst, P.bw, P.e_big, c, next, k, self, a, present, up_down, own);
   if (P.nchunks) {
-    hash_sweep_args ha{g.src.data(), g.dst.data(), g.w.data(), P.off, P.chunks.data(), P.nchunks, c, (uint32_t)g.base,
+    hash_sweep_args ha{g.dst.data(), g.w.data(), g.wf, P.off, P.chunks.data(), P.nchunks, c, (uint32_t)g.base,
                        self, a, P.ag.data(), k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down, own};
-    // persistent blocks: the resident count (5 per CU at 30 KB of LDS)
-    unsigned const hg  = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)kHashResident * kCUs);
+    // persistent blocks: the resident count (5 per CU at 30 KB of LDS with fp32 weights,
+    // 4 with fp64 weights (registers) or 64-bit keys (38 KB of LDS))
+    unsigned const hg  = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(g.wf ? kHashResident : kHashResident - 1) * kCUs);
     unsigned const hgw = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(kHashResident - 1) * kCUs);  // 38 KB
     bool const wide = S.tune.louvain_wide_keys;  // tests of the 64-bit keys
-    if (g.nv < (1 << 24) - 1 && !wide)
-      hipLaunchKernelGGL(k_sweep_hash<uint32_t>, dim3(hg), dim3(kHashThreads), 0, s, ha);
-    else
-      hipLaunchKernelGGL(k_sweep_hash<u64>, dim3(hgw), dim3(kHashThreads), 0, s, ha);
+    if (g.nv < (1 << 24) - 1 && !wide) {
+      if (g.wf) hipLaunchKernelGGL((k_sweep_hash<uint32_t, float>), dim3(hg), dim3(kHashThreads), 0, s, ha);
+      else hipLaunchKernelGGL((k_sweep_hash<uint32_t, double>), dim3(hg), dim3(kHashThreads), 0, s, ha);
+    } else {
+      if (g.wf) hipLaunchKernelGGL((k_sweep_hash<u64, float>), dim3(hgw), dim3(kHashThreads), 0, s, ha);
+      else hipLaunchKernelGGL((k_sweep_hash<u64, double>), dim3(hgw), dim3(kHashThreads), 0, s, ha);
+    }
     CGX_LAUNCH_CHECK();
   }
   if (P.big_hash && to_host_scalar(P.overflow.data(), s) != 0) {
@@ -1918,6 +1953,9 @@ void louvain_impl(handle_t& h, graph_t& g, size_t max_level, double resolution, 
                        adj.indices.data<V>(), adj.weights.data<R>(), nv0, cur.ne, cur.src.data(), cur.dst.data(),
                        cur.w.data());
   CGX_LAUNCH_CHECK();
+  // fp32 input: level 0's hash sweeps read the adjacency's own fp32 weights (edge order
+  // is the adjacency's; the fp64 values are the same numbers)
+  if constexpr (std::is_same_v<R, float>) cur.wf = cur.ne ? adj.weights.data<float>() : nullptr;
   device_sum(plain_f{cur.w.data()}, (size_t)cur.ne, S.scal.data(), S.scratch.data(), s);
   S.m = to_host_scalar(S.scal.data(), s);  // total edge weight (constant over levels)
 
