@@ -1985,17 +1985,23 @@ inline void calibrate_queues(hipStream_t s, pr_push_t& pp, tuning_t const& tu)
 // split at the source cut into two virtual windows, vw = band * nwin_real + window, so
 // the stream, the items and the queues run every window's low-source entries first
 // and the whole grid gathers one band of x~ at a time (push_body16 BANDS)
+//
+// wide: 32K windows from 2^24 rows as the symmetric builder takes them (packed
+// entries only; their carries are folded by the fused apply or k_pr_apply, so a
+// caller whose sums leave through a collective -- MG with several grid rows -- passes
+// false)
 template <typename C, typename R>
 void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R const* w, int64_t ne, int64_t n_rows,
                          int64_t n_cols, pr_push_t& pp, tuning_t const& tu, bool col_sorted = false,
-                         int64_t band_cut = 0)
+                         int64_t band_cut = 0, bool wide = false)
 {
   pp.built = true;
   pp.ok    = (uint64_t)n_rows < (1ull << 32) && (uint64_t)n_cols < (1ull << 32) && (uint64_t)ne < (1ull << 32);
   if (!pp.ok) return;
-  int const wb = push_win_bits(n_rows, tu);
+  int const wb = push_win_bits(n_rows, tu, wide && !w && tu.pr_packed);
   int const sb = 32 - wb;
-  if (wb < 14 || w || !tu.pr_packed || band_cut >= n_cols) band_cut = 0;
+  if (wb != 14 || w || !tu.pr_packed || band_cut >= n_cols) band_cut = 0;
+  pp.carry.release();
   int64_t const nwin_real = std::max<int64_t>(1, (n_rows + (int64_t(1) << wb) - 1) >> wb);
   int64_t const nwin      = band_cut > 0 ? 2 * nwin_real : nwin_real;
   pp.win_bits        = wb;
@@ -2055,6 +2061,11 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
     if (total <= ne + ne / 2 && (uint64_t)total < (1ull << 32)) {
       uint16_t const pad_code = (uint16_t)(((1u << (16 - wb)) - 1) << wb);  // a jump of 0: no edge
       pp.packed = true;
+      if (wb == 15) {  // the 32K push's per-destination carry words
+        pp.carry.set_stream(s);
+        pp.carry.resize(pp.nacc * sizeof(uint32_t));
+        HIP_CHECK(hipMemsetAsync(pp.carry.data(), 0, pp.nacc * sizeof(uint32_t), s));
+      }
       pp.ent16.set_stream(s);
       pp.ent16.resize((total + kPushUnit) * sizeof(uint16_t));  // + a unit: the kernel prefetches whole units
       fill<uint16_t>(pp.ent16.data<uint16_t>(), (size_t)(total + kPushUnit), pad_code, s);
@@ -2094,11 +2105,11 @@ void build_push_from_coo(hipStream_t s, uint32_t const* rows, C const* cols, R c
       return;
     }
   }
-  if (band_cut > 0) {  // bands need the packed format: the same schedule without them
+  if (band_cut > 0 || wb == 15) {  // bands and 32K windows need the packed format: the schedule without them
     keys_out.free();
     vals_out.free();
     ws.free();
-    build_push_from_coo<C, R>(s, rows, cols, w, ne, n_rows, n_cols, pp, tu, col_sorted, 0);
+    build_push_from_coo<C, R>(s, rows, cols, w, ne, n_rows, n_cols, pp, tu, col_sorted, 0, false);
     return;
   }
   dbuf<uint32_t> flag(ne + 1, s), uid(ne + 1, s);
@@ -2841,7 +2852,9 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
   R const* const w_in    = g.weighted ? mg.w.data<R>() : nullptr;
   (void)n_rows;
   if (K == 1) {  // (cs = nmax_col: the rows are already owner * cs + owner-local row)
-    build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), w_in, ne, n_rows_k, n_cols, blk->ch[0].pp, h.tune);
+    // one grid row: the sums stay on this rank, so 32K windows as on one GPU
+    build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), w_in, ne, n_rows_k, n_cols, blk->ch[0].pp, h.tune,
+                                     false, 0, R_ == 1);
   } else {
     dbuf<uint32_t> chunk(ne, s), chunk_s(ne, s), iv(ne, s), perm(ne, s), rows_s(ne, s), cols_s(ne, s);
     dbuf<R> w_s(w_in ? ne : 1, s);
@@ -3138,7 +3151,8 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
     pr_push_t& pp = blk.ch[k].pp;
     spk[k].a      = a;
     set_queue_args(spk[k], pp, s);
-    spk[k].win_bits = pp.win_bits;
+    spk[k].win_bits      = pp.win_bits;
+    spk[k].acc32_nocheck = h.tune.pr_carry_check ? 0 : 1;
     nblk_push[k]    = spk[k].nitems && pp.nunits ? push_blocks(pp.win_bits) : 0;
     // the push's persistent blocks fill every CU (LDS or registers), so an RCCL
     // kernel launched beside it would wait for the push to end: with overlapped

@@ -372,6 +372,7 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
     # -- single GPU: Louvain on the weighted graph
     h = p.ResourceHandle()
     g, _, _ = bench.build_rmat_graph(p, h, scale, weighted=True, transposed=False)
+    p.louvain(h, g, 100, 1.0, False)  # (first call: allocator warm-up, as the MG call below is not)
     (v, c, q_sg), t_lv_sg = timed(lambda: p.louvain(h, g, 100, 1.0, False))
     lv_sg = h.last_louvain_levels()
     sg_c = _by_ext(v, c, n_ext).cpu()
@@ -387,6 +388,8 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
     sg_x = _by_ext(v, x.view(torch.int32), n_ext).cpu()
     root = int(v[0])  # internal id 0: the largest degree
     d, pr, vb = p.bfs(h, g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+    _, t_bfs_sg = timed(lambda: p.bfs(h, g, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True,
+                                      False))
     sg_d, sg_p = _by_ext(vb, d, n_ext).cpu(), _by_ext(vb, pr, n_ext).cpu()
     del v, x, d, pr, vb
     g = None
@@ -412,13 +415,17 @@ def test_mg_one_rank_rccl_rmat26_equals_sg():
             "MG PageRank differs from SG at RMAT-26"
         _, t_pr_mg = timed(lambda: p.pagerank(hm, gm, None, None, None, None, 0.85, 1e-6, 500, False))
         dm, pm, vmb = p.bfs(hm, gm, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+        _, t_bfs_mg = timed(lambda: p.bfs(hm, gm, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0,
+                                          True, False))
         ids = vmb.cpu().to(torch.int64)
         assert torch.equal(dm.cpu().to(torch.int64), sg_d[ids]), "MG BFS distances differ from SG at RMAT-26"
         assert torch.equal(pm.cpu().to(torch.int64), sg_p[ids]), "MG BFS predecessors differ from SG at RMAT-26"
         print(f"RMAT-26 one-rank RCCL MG == SG: PageRank {it_sg} iterations, BFS from {root}, "
               f"Louvain Q {q_sg:.9f} in {lv_sg} levels")
-        # the one-rank MG path's cost over SG (steady PageRank call; Louvain end to end)
+        # the one-rank MG path's cost over SG (steady PageRank and BFS calls; Louvain end
+        # to end, the SG time from its second call)
         print(f"RMAT-26 MG/SG time: PageRank {t_pr_mg / t_pr_sg:.3f} ({1e3 * t_pr_mg:.2f} / {1e3 * t_pr_sg:.2f} ms), "
+              f"BFS {t_bfs_mg / t_bfs_sg:.3f} ({1e3 * t_bfs_mg:.2f} / {1e3 * t_bfs_sg:.2f} ms), "
               f"Louvain {t_lv_mg / t_lv_sg:.3f} ({t_lv_mg:.2f} / {t_lv_sg:.2f} s)")
         del vm, xm, dm, pm, vmb
         gm = None
