@@ -2325,13 +2325,6 @@ __global__ void k_localize(uint32_t* dst, int64_t ne, uint32_t lo, uint32_t nr, 
   }
 }
 
-// out[i] = position of x[i] in the sorted key list
-__global__ void k_rank_in(uint32_t const* x, int64_t n, uint32_t const* keys, int64_t nk, uint32_t* out)
-{
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = (uint32_t)lower_bound_u32(keys, nk, x[i]);
-}
-
 // owner side of a lookup: out[i] = table[key[i] - lo]
 template <typename T>
 __global__ void k_owner_gather(uint32_t const* key, int64_t n, uint32_t lo, T const* table, T* out)
@@ -2481,6 +2474,59 @@ int64_t sort_unique_u32(uint32_t const* in, int64_t n, dbuf<uint32_t>& out, int 
   return (int64_t)to_host_scalar(cnt.data(), s);
 }
 
+// distinct ids through a bitmap of the id range (ids < nv): nv / 8 bytes, where a sort
+// of n keys reads and writes them once per radix pass
+__global__ void k_set_bits(uint32_t const* in, int64_t n, uint32_t* bm)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicOr(bm + (in[i] >> 5), 1u << (in[i] & 31u));
+}
+__global__ void k_word_popc(uint32_t const* bm, int64_t nw, uint32_t* wc)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= nw; i += (int64_t)gridDim.x * blockDim.x)
+    wc[i] = i < nw ? (uint32_t)__popc(bm[i]) : 0u;
+}
+__global__ void k_emit_bits(uint32_t const* bm, uint32_t const* wp, int64_t nw, uint32_t* out)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t b = bm[i], o = wp[i];
+    while (b) {
+      int const t = __ffs(b) - 1;
+      out[o++]    = (uint32_t)(i * 32 + t);
+      b &= b - 1;
+    }
+  }
+}
+__global__ void k_rank_bits(uint32_t const* in, int64_t n, uint32_t const* bm, uint32_t const* wp, uint32_t* rank)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t const x = in[i], w = x >> 5;
+    rank[i]          = wp[w] + (uint32_t)__popc(bm[w] & ((1u << (x & 31u)) - 1u));
+  }
+}
+
+// the sorted distinct ids of in[0, n) (ids < nv) into out, and each input's position
+// among them into rank (sort_unique_u32 and a lower bound per id, through a bitmap)
+int64_t unique_ranks_bitmap(uint32_t const* in, int64_t n, int64_t nv, dbuf<uint32_t>& out, uint32_t* rank,
+                            hipStream_t s)
+{
+  int64_t const nw = (nv + 31) / 32;
+  dbuf<uint32_t> bm(std::max<int64_t>(nw, 1), s), wc(nw + 1, s), wp(nw + 1, s);
+  fill<uint32_t>(bm.data(), nw, 0u, s);
+  if (n) hipLaunchKernelGGL(k_set_bits, dim3(blocks(n)), dim3(kBlock), 0, s, in, n, bm.data());
+  CGX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_word_popc, dim3(blocks(nw + 1)), dim3(kBlock), 0, s, bm.data(), nw, wc.data());
+  CGX_LAUNCH_CHECK();
+  exclusive_scan<uint32_t, uint32_t>(wc.data(), wp.data(), (size_t)(nw + 1), s);
+  int64_t const ncl = (int64_t)to_host_scalar(wp.data() + nw, s);
+  out.resize(std::max<int64_t>(ncl, 1), s);
+  if (nw) hipLaunchKernelGGL(k_emit_bits, dim3(blocks(nw)), dim3(kBlock), 0, s, bm.data(), wp.data(), nw, out.data());
+  CGX_LAUNCH_CHECK();
+  if (n) hipLaunchKernelGGL(k_rank_bits, dim3(blocks(n)), dim3(kBlock), 0, s, in, n, bm.data(), wp.data(), rank);
+  CGX_LAUNCH_CHECK();
+  return ncl;
+}
+
 // per-owner counts of a sorted id list (owner ranges voff, device copy voff_d)
 std::vector<size_t> owner_counts(uint32_t const* ids, int64_t n, dbuf<int64_t> const& voff_d, int P, hipStream_t s)
 {
@@ -2599,12 +2645,10 @@ void mg_view(louvain_state& S, mg_level& L, bool all_present, mg_sweep_view& W)
   if (L.nr) HIP_CHECK(hipMemcpyAsync(all.data(), L.c_own.data(), L.nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   if (L.ng)
     HIP_CHECK(hipMemcpyAsync(all.data() + L.nr, L.c_gh.data(), L.ng * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  W.ncl = sort_unique_u32(all.data(), n, W.ref, bits_for((unsigned long long)std::max<int64_t>(L.nv - 1, 1)), s);
+  // the referenced clusters, sorted, and the local (order-preserving) ids: a bitmap of
+  // the level's ids (nv / 8 bytes) where a radix sort of the nr + ng ids ran each sweep
   W.c_loc.resize(std::max<int64_t>(n, 1), s);
-  if (n)
-    hipLaunchKernelGGL(k_rank_in, dim3(blocks(n)), dim3(kBlock), 0, s, all.data(), n, W.ref.data(), W.ncl,
-                       W.c_loc.data());
-  CGX_LAUNCH_CHECK();
+  W.ncl = unique_ranks_bitmap(all.data(), n, L.nv, W.ref, W.c_loc.data(), s);
   auto af = collect_by_key<long long>(S, W.ref.data(), W.ncl, L.voff_d, L.lo, L.afix.data());
   auto pc = collect_by_key<int>(S, W.ref.data(), W.ncl, L.voff_d, L.lo, L.pcnt.data());
   W.a.resize(std::max<int64_t>(W.ncl, 1), s);
