@@ -2795,33 +2795,44 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
   }
   ka.free();
   wa.free();
-  // 2. to the owner of label(u) (keys sorted, owner ranges ascending)
-  dbuf<int64_t> bnd(P + 1, s);
-  hipLaunchKernelGGL(k_key_bounds, dim3(1), dim3(256), 0, s, keys.data(), nce, L.voff_d.data(), P, bnd.data());
-  CGX_LAUNCH_CHECK();
-  auto c64 = bounds_to_counts(bnd, P, s);
-  std::vector<size_t> counts(c64.begin(), c64.end()), rc;
-  auto rk = exchange<u64>(comm, keys.data(), counts, rc, s);
-  keys.free();
-  auto rw = exchange<double>(comm, cw.data(), counts, rc, s);
-  cw.free();
-  int64_t const nrcv = (int64_t)rk.n, r1 = std::max<int64_t>(nrcv, 1);
-  dbuf<u64> mk, mk2(r1, s);
-  dbuf<double> mw, mw2(r1, s);
+  // 2. to the owner of label(u) (keys sorted, owner ranges ascending); one rank owns
+  //    every label: its pairs are already sorted and summed
+  dbuf<u64> mk, mk2;
+  dbuf<double> mw;
   int64_t nm = 0;
-  if (nrcv) {
-    if (radix_sort_pairs_db<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0, 32 + lb, s)) {
-      std::swap(rk, mk2);
-      std::swap(rw, mw2);
+  if (P == 1) {
+    nm = nce;
+    mk = std::move(keys);
+    mw = std::move(cw);
+    mk2.resize(std::max<int64_t>(nm, 1), s);  // (scratch for the relabelled keys below)
+  } else {
+    dbuf<int64_t> bnd(P + 1, s);
+    hipLaunchKernelGGL(k_key_bounds, dim3(1), dim3(256), 0, s, keys.data(), nce, L.voff_d.data(), P, bnd.data());
+    CGX_LAUNCH_CHECK();
+    auto c64 = bounds_to_counts(bnd, P, s);
+    std::vector<size_t> counts(c64.begin(), c64.end()), rc;
+    auto rk = exchange<u64>(comm, keys.data(), counts, rc, s);
+    keys.free();
+    auto rw = exchange<double>(comm, cw.data(), counts, rc, s);
+    cw.free();
+    int64_t const nrcv = (int64_t)rk.n, r1 = std::max<int64_t>(nrcv, 1);
+    mk2.resize(r1, s);
+    dbuf<double> mw2(r1, s);
+    if (nrcv) {
+      if (radix_sort_pairs_db<u64, double>(rk.data(), mk2.data(), rw.data(), mw2.data(), (size_t)nrcv, 0, 32 + lb,
+                                           s)) {
+        std::swap(rk, mk2);
+        std::swap(rw, mw2);
+      }
+      // sorted in rk / rw; merged sums into mk2 / mw2
+      nm = reduce_by_key(rk.data(), rw.data(), (size_t)nrcv, mk2.data(), mw2.data(), rocprim::plus<double>(),
+                         rocprim::equal_to<u64>(), s);
     }
-    // sorted in rk / rw; merged sums into mk2 / mw2
-    nm = reduce_by_key(rk.data(), rw.data(), (size_t)nrcv, mk2.data(), mw2.data(), rocprim::plus<double>(),
-                       rocprim::equal_to<u64>(), s);
+    mk  = std::move(mk2);
+    mw  = std::move(mw2);
+    mk2 = std::move(rk);  // (scratch for the relabelled keys below)
+    rw.free();
   }
-  mk = std::move(mk2);
-  mw = std::move(mw2);
-  mk2 = std::move(rk);  // (scratch for the relabelled keys below)
-  rw.free();
   // 3. used labels: every rank sends its rows' distinct labels to their owners
   dbuf<uint32_t> ul;
   int64_t const nul = sort_unique_u32(lab_own, nr, ul, lb, s);
