@@ -61,7 +61,9 @@ struct level_graph {
   int64_t base = 0, nrows = 0;
   dbuf<uint32_t> src, dst;  // sorted by (src, dst)
   dbuf<double> w;
-  float const* wf = nullptr;  // level 0 of fp32 input: the same weights as fp32 (the graph's own array)
+  float const* wf = nullptr;  // level 0 of fp32 input: the same weights as fp32 (the graph's own array,
+                              // or wfbuf on the multi-GPU level 0)
+  dbuf<float> wfbuf;
 };
 
 struct gain_t {
@@ -2237,17 +2239,28 @@ level_graph mg_level0(handle_t& h, graph_t& g)
   out.w.resize(m1, s);
   if (m) {
     dbuf<u64> k1(m, s), k2(m, s);
-    dbuf<double> w1(m, s);
     hipLaunchKernelGGL(k_mg_row_keys<V>, dim3(blocks(m)), dim3(kBlock), 0, s, rs.data(), rd.data(), m, out.base,
                        k1.data());
     CGX_LAUNCH_CHECK();
     rs.free();
     rd.free();
-    convert<double, R>(w1.data(), rw.data(), m, s);
-    rw.free();
-    bool const in1 = radix_sort_pairs_db<u64, double>(k1.data(), k2.data(), w1.data(), out.w.data(), (size_t)m, 0,
-                                                      32 + bits_for(std::max<int64_t>(out.nrows - 1, 0)), s);
-    if (!in1) std::swap(out.w, w1);
+    int const kb = 32 + bits_for(std::max<int64_t>(out.nrows - 1, 0));
+    bool in1     = false;
+    if constexpr (std::is_same_v<R, float>) {
+      // fp32 input: the weights are sorted as fp32 and kept beside the fp64 copy, for
+      // the level-0 hash sweeps (as the single-GPU level 0 reads the adjacency's)
+      dbuf<float> f2(m, s);
+      in1 = radix_sort_pairs_db<u64, float>(k1.data(), k2.data(), rw.data(), f2.data(), (size_t)m, 0, kb, s);
+      out.wfbuf = std::move(in1 ? f2 : rw);
+      out.wf    = out.wfbuf.data();
+      convert<double, float>(out.w.data(), out.wf, m, s);
+    } else {
+      dbuf<double> w1(m, s);
+      convert<double, R>(w1.data(), rw.data(), m, s);
+      rw.free();
+      in1 = radix_sort_pairs_db<u64, double>(k1.data(), k2.data(), w1.data(), out.w.data(), (size_t)m, 0, kb, s);
+      if (!in1) std::swap(out.w, w1);
+    }
     hipLaunchKernelGGL(k_split_pairs, dim3(blocks(m)), dim3(kBlock), 0, s, in1 ? k2.data() : k1.data(), m,
                        out.src.data(), out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
