@@ -102,6 +102,22 @@ def test_resolution_and_max_level():
         assert h.last_louvain_levels() == olevels <= ml
 
 
+def test_isolated_ids_inside_chunks():
+    """Unrenumbered ids with isolated vertices between the connected ones (every third id
+    has edges): zero-degree rows sit inside the hash chunks, where an edge's row is found
+    by a binary search over the chunk's row offsets (empty rows share their start).
+    Integer weights: the clustering and Q must be the oracle's exactly."""
+    s, d = rmat.rmat(10, 16 << 10, seed=11)
+    w = np.floor(rmat.rmat_weights(s.size, seed=12).astype(np.float64) * 8.0) + 1.0
+    s, d, w = og.symmetrize_dedup(s, d, w)
+    s, d = s * 3, d * 3
+    h, G = make_graph(s, d, w.astype(np.float32), renumber=False, symmetric=True)
+    v, c, q = run(h, G)
+    OG, oc, oq, olevels = oracle_run(s, d, w, renumber=False)
+    assert np.array_equal(c, oc) and q == oq
+    assert h.last_louvain_levels() == olevels
+
+
 def test_int64_and_double():
     s, d, w = og.read_csv(dataset_path("karate.csv"))
     h, G = make_graph(s, d, w, renumber=True, symmetric=True, vdtype=np.int64, wdtype=np.float64)
