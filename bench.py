@@ -24,6 +24,9 @@ Extra fields on the same JSON line:
   pagerank_rmat22  -- (N=1) configs[1]: the same measurement on RMAT-22.
   pagerank_rmat26  -- (N=8) configs[3]: RMAT-26 on the 2D partition.
   pagerank_alt_grid-- (N>1) the headline graph on the other R x C grid (1 x P).
+  pagerank_overlap_k4 -- (N>1, several grid rows) the headline graph with the
+                      column reduce-scatter overlapped in 4 row chunks, and whether
+                      its ranks equal the default's bit for bit.
   bfs              -- configs[2]: RMAT-24 BFS, Graph500 MTEPS (harmonic mean over
                       8 roots), its roofline (4E_cc + 16V_cc per traversal) and PMC
                       traffic, and CPU baselines (NetworkX on a bounded sample,
@@ -258,6 +261,24 @@ def pagerank_summary(r, args, grid=None):
             "roofline": {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": r["achieved"] / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": r["bytes_per_iter"],
                          "avg_kernel_ms": r["avg_ms"]}}
+
+
+def overlap_leg(p, args, mg_ref, C):
+    """N > 1 with several grid rows: the headline graph with the column reduce-scatter
+    overlapped with the push in K = 4 row chunks (option mg_chunks; the default is one
+    chunk), timed like the headline and checked bitwise equal to the
+    default's ranks on every rank (same graph, same partition: the sums are integer)."""
+    import torch
+    r2 = pagerank_leg(p, args, args.scale, args.steps, args.warmup, args.ctx, options={"mg_chunks": 4})
+    v2, x2 = p.pagerank(r2["h"], r2["g"], None, None, None, None, args.alpha, args.epsilon, 500, False)
+    same = (torch.equal(v2, mg_ref[0]) and torch.equal(x2.view(torch.int32), mg_ref[1])
+            and r2["h"].last_iterations() == mg_ref[2])
+    bad = int(sum_over_ranks(args, 0.0 if same else 1.0))
+    out = pagerank_summary(r2, args, grid_name(args, C) + ", mg_chunks 4")
+    out["bitwise_equal_to_default"] = bad == 0
+    out["ranks_differing"] = bad
+    del v2, x2, r2
+    return out
 
 
 # ----------------------------------------------------------------------------- PMC traffic
@@ -744,6 +765,11 @@ def main():
             out["cpu_baseline"] = pagerank_cpu_baseline(p, r, args)
         except Exception as e:  # noqa: BLE001
             out["cpu_baseline"] = {"error": repr(e)[:300]}
+    mg_ref = None
+    if world > 1:  # the default (K = 1) result, for the overlapped-chunk leg's bitwise check
+        v1, x1 = p.pagerank(r["h"], r["g"], None, None, None, None, args.alpha, args.epsilon, 500, False)
+        mg_ref = (v1.clone(), x1.view(torch.int32).clone(), r["h"].last_iterations())
+        del v1, x1
     del r
     release_caches(p)
 
@@ -785,6 +811,9 @@ def main():
                     release_caches(p)
                     barrier(args)
                     ctx2.free()
+                if world // C > 1 and mg_ref is not None:
+                    out["pagerank_overlap_k4"] = overlap_leg(p, args, mg_ref, C)
+                    release_caches(p)
                 if world == 8:
                     r2 = pagerank_leg(p, args, 26, max(1, args.steps // 2), 1, args.ctx)
                     out["pagerank_rmat26"] = pagerank_summary(r2, args, grid_name(args, C))

@@ -41,9 +41,8 @@ struct tuning_t {
   bool pr_hub          = true;  // hub x~ staged in LDS (16K windows)
   int64_t pr_band_cut  = -1;    // banded push source cut (-1: by size, 0: no bands)
   int pr_share_div     = 0;     // items per push block on average (0: kShareDiv); windows above 1.5x are shared
-  bool pr_carry_check  = true;  // 32K push: returning LDS adds + carries (0: measurement only, wrong sums)
   bool pr_fast_build   = true;  // symmetric unweighted schedules through one-word keys (else the general build)
-  int mg_chunks        = 0;     // MG overlap chunks (0: by size)
+  int mg_chunks        = 0;     // MG overlap chunks (0: one chunk, no overlap)
   double bfs_alpha     = 40.0;  // direction switch (Beamer's alpha / beta)
   double bfs_beta      = 64.0;
   double mg_bfs_alpha  = 40.0;  // multi-GPU BFS direction switch (mg_bfs.hip; one-rank RMAT-24: 40 / 64

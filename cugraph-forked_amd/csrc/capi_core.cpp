@@ -529,7 +529,6 @@ extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t
     else if (n == "pr_hub") b(t.pr_hub);
     else if (n == "pr_band_cut") t.pr_band_cut = (int64_t)value;
     else if (n == "pr_fast_build") b(t.pr_fast_build);
-    else if (n == "pr_carry_check") b(t.pr_carry_check);
     else if (n == "pr_share_div") i32(t.pr_share_div);
     else if (n == "mg_chunks") i32(t.mg_chunks);
     else if (n == "bfs_alpha") t.bfs_alpha = value;

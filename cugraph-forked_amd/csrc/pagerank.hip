@@ -438,10 +438,10 @@ __global__ __launch_bounds__(256) void k_pr_iter(pr_args<V, E, R> a)
 //    x~ lines one gathers are in that XCD's L2 for the others: an offline LRU
 //    model of the 8 L2s (RMAT-24) gives 12.9M x~ misses per iteration against
 //    22.4M for one queue of 8-unit tiles;
-//  * sums are 64-bit fixed point (scale 2^52; every destination's sum is at most
-//    the total rank mass 1 since x~[u] w(u, v) summed over v is pr[u]).  Integer
-//    addition is associative: the result is bitwise deterministic whatever the
-//    order of the atomics.  2^52 (2^62 until round 5) keeps a typical contribution
+//  * sums are 64-bit fixed point (scale fix_scale<R>: 2^52 for fp32, 2^62 for fp64;
+//    every destination's sum is at most the total rank mass 1 since x~[u] w(u, v)
+//    summed over v is pr[u]).  Integer addition is associative: the result is bitwise
+//    deterministic whatever the order of the atomics.  fp32's 2^52 keeps a typical contribution
 //    (x~ ~ 2^-27 at RMAT-24) well below 2^32, so the 32K-destination windows can sum
 //    in 32-bit LDS words with rare carries (push_body16, WB = 15); the resolution
 //    2^-52 is about half an fp32 ulp of the smallest rank, (1 - alpha) / V, at RMAT-26.
@@ -471,8 +471,22 @@ constexpr int kHubBytes = 32768 - 512;
 #ifndef CGX_APPLY_BATCH
 #define CGX_APPLY_BATCH 4
 #endif
-constexpr double kFixScale    = 4503599627370496.0;  // 2^52
-constexpr double kFixScaleInv = 1.0 / 4503599627370496.0;
+// Fixed-point scale of the push's per-destination sums, by result type.  fp32: 2^52
+// on every schedule, so the 32K-window push's 32-bit LDS words (a typical term ~2^-27
+// stays far below 2^32) and every other schedule -- MG blocks included -- give the same
+// bits; the resolution is half an fp32 ulp of the smallest rank at RMAT-26.  fp64: 2^62
+// (every destination's sum <= sum(pr) = 1, below 2 with accepted precomputed
+// out-weights), and fp64 never takes 32K windows (build_pr_push_schedule).
+template <typename R>
+__host__ __device__ constexpr double fix_scale()
+{
+  return sizeof(R) == 8 ? 4611686018427387904.0 /* 2^62 */ : 4503599627370496.0 /* 2^52 */;
+}
+template <typename R>
+__host__ __device__ constexpr double fix_scale_inv()
+{
+  return 1.0 / fix_scale<R>();
+}
 
 // Window bits: about 500-600 windows measured best -- fewer x~ line visits per
 // entry as windows grow, against the load balance of few windows.  14 (16K
@@ -529,8 +543,6 @@ struct push_args {
   push_unit const* units;
   int64_t nunits;
   unsigned long long* acc;  // [n_rows] fixed-point sums, zero between iterations
-  int acc32_nocheck;        // measurement only (tuning_t::pr_carry_check = 0): the 32K push's LDS adds
-                            // without returns -- wrong sums once a word wraps; timing A/B
   uint32_t* carry;          // 32K windows (WB = 15): per destination, 2^32 units of its sum that the
                             // 32-bit LDS words carried out (and high words of large terms); zero
                             // between iterations, read and cleared with the sums; else nullptr
@@ -571,9 +583,10 @@ __device__ __forceinline__ T nt_load(T const* p)
   return __builtin_nontemporal_load(p);
 }
 
+template <typename R>
 __device__ __forceinline__ unsigned long long to_fixed(double v)
 {
-  return (unsigned long long)__double2ll_rn(v * kFixScale);
+  return (unsigned long long)__double2ll_rn(v * fix_scale<R>());
 }
 
 // The same value, round-to-nearest-even(x * 2^52), for an fp32 x in [0, 1) in fp32
@@ -595,7 +608,7 @@ template <typename R>
 __device__ __forceinline__ unsigned long long fixed_of(R x)
 {
   if constexpr (std::is_same<R, float>::value) return to_fixed_f32(x);
-  else return to_fixed((double)x);
+  else return to_fixed<R>((double)x);
 }
 
 // push_unit::win of an item's first unit carries kWholeItem when the item is all of
@@ -686,7 +699,7 @@ __device__ __forceinline__ void apply_window(push_args<V, E, R> const& sa, int64
     for (int j = 0; j < kB; ++j) {
       int const i = i0 + j * kPushThreads;
       if (i < n)
-        vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf,
+        vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * fix_scale_inv<R>(), old[j], ow[j], base, pf,
                                     my_diff, my_dang);
     }
   }
@@ -744,7 +757,7 @@ __device__ __forceinline__ void apply_window_banded(push_args<V, E, R> const& sa
     for (int j = 0; j < kB; ++j) {
       int const i = i0 + j * kPushThreads;
       if (i < n)
-        vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf,
+        vertex_update_from<V, E, R>(a, (V)(v0 + i), (double)(long long)f[j] * fix_scale_inv<R>(), old[j], ow[j], base, pf,
                                     my_diff, my_dang);
     }
   }
@@ -962,7 +975,7 @@ __device__ __forceinline__ void push_body(push_args<V, E, R> const& sa)
 #pragma unroll
       for (int j = 0; j < kPerThread; ++j) {
         if constexpr (WEIGHTED) {
-          atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed((double)xv[j] * (double)w[j]));
+          atomicAdd(&acc[ent[j] & (kWin - 1)], to_fixed<R>((double)xv[j] * (double)w[j]));
         } else {
           atomicAdd(&acc[ent[j] & (kWin - 1)], fixed_of(xv[j]));
         }
@@ -1173,17 +1186,6 @@ __device__ __forceinline__ void push_body16(push_args<V, E, R> const& sa)
         // return is waited for.
         uint32_t lo[kRows], old[kRows];
         uint32_t* const cw = sa.carry + ((win & kWinMask) << WB);
-        if (sa.acc32_nocheck) {  // measurement only (pr_carry_check = 0): no returns, carries lost
-#pragma unroll
-          for (int j = 0; j < kRows; ++j) {
-            uint32_t const e = entry(w, j);
-            unsigned long long fix;
-            if constexpr (ENC) fix = dec_fixed(xv[j]);
-            else fix = fixed_of(xv[j]);
-            if ((e >> WB) != kJump) atomicAdd(&acc[e & kLow], (uint32_t)fix);
-          }
-          return;
-        }
 #pragma unroll
         for (int j = 0; j < kRows; ++j) {
           uint32_t const e = entry(w, j);
@@ -1335,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           int64_t const vj = 4 * q + j;
-          double n = base + a.alpha * ((double)(long long)f[j] * kFixScaleInv);
+          double n = base + a.alpha * ((double)(long long)f[j] * fix_scale_inv<R>());
           if (a.pers) n += pf * (double)a.pers[vj];
           nr[j] = (float)n;
           acc_add(my_diff, fabs((double)nr[j] - (double)o[j]));
@@ -1370,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
       int64_t const vj = v + j * stride;
       if (!sa.keep_acc && f[j] && (!sa.win_multi || sa.win_multi[vj >> sa.win_bits])) sa.acc[vj] = 0ull;
       f[j] += take_carry(vj);
-      vertex_update_from<V, E, R>(a, (V)vj, (double)(long long)f[j] * kFixScaleInv, old[j], ow[j], base, pf, my_diff,
+      vertex_update_from<V, E, R>(a, (V)vj, (double)(long long)f[j] * fix_scale_inv<R>(), old[j], ow[j], base, pf, my_diff,
                                   my_dang);
     }
   }
@@ -1378,7 +1380,7 @@ __global__ __launch_bounds__(256) void k_pr_apply(push_args<V, E, R> sa)
     unsigned long long f = sa.acc[v];
     if (!sa.keep_acc && f && (!sa.win_multi || sa.win_multi[v >> sa.win_bits])) sa.acc[v] = 0ull;
     f += take_carry(v);
-    vertex_update<V, E, R>(a, (V)v, (double)(long long)f * kFixScaleInv, base, pf, my_diff, my_dang);
+    vertex_update<V, E, R>(a, (V)v, (double)(long long)f * fix_scale_inv<R>(), base, pf, my_diff, my_dang);
   }
   finish_iteration<V, E, R>(a, my_diff, my_dang, true);
 }
@@ -2202,9 +2204,9 @@ void sort_window_keys(rocprim::double_buffer<uint64_t>& db, int64_t ne, int shv,
 // stream would not pack -- nothing built, the caller takes the general path.
 template <typename E, typename CM>
 bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, int64_t ne, int64_t nv, pr_push_t& pp,
-                              tuning_t const& tu, int64_t band_cut)
+                              tuning_t const& tu, int64_t band_cut, bool wide)
 {
-  int const wb = push_win_bits(nv, tu, true);
+  int const wb = push_win_bits(nv, tu, wide);
   if (wb != 14 || band_cut >= nv) band_cut = 0;
   int64_t const nwin_real = std::max<int64_t>(1, (nv + (int64_t(1) << wb) - 1) >> wb);
   int64_t const nwin      = band_cut > 0 ? 2 * nwin_real : nwin_real;
@@ -2316,10 +2318,10 @@ bool build_push_packed_sym_cm(hipStream_t s, E const* off, uint32_t const* idx, 
 
 template <typename E>
 bool build_push_packed_sym(hipStream_t s, E const* off, uint32_t const* idx, int64_t ne, int64_t nv, pr_push_t& pp,
-                           tuning_t const& tu, int64_t band_cut)
+                           tuning_t const& tu, int64_t band_cut, bool wide)
 {
-  if (ne < (int64_t(1) << 31)) return build_push_packed_sym_cm<E, uint32_t>(s, off, idx, ne, nv, pp, tu, band_cut);
-  return build_push_packed_sym_cm<E, unsigned long long>(s, off, idx, ne, nv, pp, tu, band_cut);
+  if (ne < (int64_t(1) << 31)) return build_push_packed_sym_cm<E, uint32_t>(s, off, idx, ne, nv, pp, tu, band_cut, wide);
+  return build_push_packed_sym_cm<E, unsigned long long>(s, off, idx, ne, nv, pp, tu, band_cut, wide);
 }
 
 template <typename V, typename E, typename R>
@@ -2336,7 +2338,7 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_
   if constexpr (sizeof(V) == 4) {
     if (g.symmetric && !use_weights && h.tune.pr_packed && h.tune.pr_fast_build &&
         build_push_packed_sym<E>(s, adj.offsets.data<E>(), reinterpret_cast<uint32_t const*>(adj.indices.data<V>()), ne,
-                                 nv, adj.pr, h.tune, push_band_cut(nv, h.tune)))
+                                 nv, adj.pr, h.tune, push_band_cut(nv, h.tune), /*wide=*/sizeof(R) == 4))
       return;
   }
   dbuf<uint32_t> rows(std::max<int64_t>(ne, 1), s);
@@ -2348,12 +2350,12 @@ void build_pr_push_schedule(handle_t& h, graph_t& g, adjacency_t& adj, bool use_
     if (g.symmetric) {  // the same edges read as out-edges: (source = row, destination = index), source-sorted
       build_push_from_coo<uint32_t, R>(s, reinterpret_cast<uint32_t const*>(adj.indices.data<V>()), rows.data(),
                                        use_weights ? adj.weights.data<R>() : nullptr, ne, nv, nv, adj.pr, h.tune,
-                                       /*col_sorted=*/true, push_band_cut(nv, h.tune));
+                                       /*col_sorted=*/true, push_band_cut(nv, h.tune), /*wide=*/sizeof(R) == 4);
       return;
     }
   }
   build_push_from_coo<V, R>(s, rows.data(), adj.indices.data<V>(), use_weights ? adj.weights.data<R>() : nullptr, ne,
-                            nv, nv, adj.pr, h.tune, false, push_band_cut(nv, h.tune));
+                            nv, nv, adj.pr, h.tune, false, push_band_cut(nv, h.tune), /*wide=*/sizeof(R) == 4);
 }
 
 template <typename V, typename R>
@@ -2599,7 +2601,6 @@ void pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_vie
     nblk_apply = (int)grid_for(nv, kBlock, 512);  // fewer tickets: 512 measured best
     sa.fuse    = fuse ? 1 : 0;
     sa.nhub    = h.tune.pr_hub ? nv : 0;  // hub x~ staged in LDS (16K windows; A/B switch)
-    sa.acc32_nocheck = h.tune.pr_carry_check ? 0 : 1;
   }
   // measured-cost queues: the first launch on this schedule records item durations
   bool calibrating = push && calibration_wanted(adj.pr, h.tune);
@@ -2838,11 +2839,15 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
                        mg.dst.data<V>(), ne, voff_d.data(), P, C, blk->nmax_row, blk->nmax_col, rows.data(),
                        cols.data());
   CGX_LAUNCH_CHECK();
-  // row chunks: K = 4 from 64K rows per owner when the column has several ranks
-  // (tuning_t::mg_chunks: any K, for the tests), else one chunk = the whole block
+  // row chunks (overlapped column reduce-scatters, several grid rows only): K =
+  // tuning_t::mg_chunks; the default is one chunk = the whole block.  The overlap's
+  // device-side concurrency with RCCL has never run on more than one GPU (the
+  // rehearsals go through gloo, which host-synchronises every collective), so it
+  // stays opt-in; bench.py --gpus N > 1 times K = 4 beside the default and checks
+  // the ranks bitwise equal
   int K = 1;
   if (R_ > 1) {
-    K = h.tune.mg_chunks > 0 ? h.tune.mg_chunks : (blk->nmax_col >= 4 * 16384 ? 4 : 1);
+    K = h.tune.mg_chunks > 0 ? h.tune.mg_chunks : 1;
     K = (int)std::min<int64_t>(K, std::max<int64_t>(blk->nmax_col, 1));
   }
   blk->K  = K;
@@ -2854,7 +2859,7 @@ mg_pr_block& mg_block(handle_t& h, graph_t& g)
   if (K == 1) {  // (cs = nmax_col: the rows are already owner * cs + owner-local row)
     // one grid row: the sums stay on this rank, so 32K windows as on one GPU
     build_push_from_coo<uint32_t, R>(s, rows.data(), cols.data(), w_in, ne, n_rows_k, n_cols, blk->ch[0].pp, h.tune,
-                                     false, 0, R_ == 1);
+                                     false, 0, R_ == 1 && sizeof(R) == 4);
   } else {
     dbuf<uint32_t> chunk(ne, s), chunk_s(ne, s), iv(ne, s), perm(ne, s), rows_s(ne, s), cols_s(ne, s);
     dbuf<R> w_s(w_in ? ne : 1, s);
@@ -3152,7 +3157,6 @@ void mg_pagerank_impl(handle_t& h, graph_t& g, array_view_t const* pow_v, array_
     spk[k].a      = a;
     set_queue_args(spk[k], pp, s);
     spk[k].win_bits      = pp.win_bits;
-    spk[k].acc32_nocheck = h.tune.pr_carry_check ? 0 : 1;
     nblk_push[k]    = spk[k].nitems && pp.nunits ? push_blocks(pp.win_bits) : 0;
     // the push's persistent blocks fill every CU (LDS or registers), so an RCCL
     // kernel launched beside it would wait for the push to end: with overlapped

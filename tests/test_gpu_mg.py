@@ -687,3 +687,159 @@ def _dask_worker(rank, world, port, C):
 @pytest.mark.parametrize("world,C", [(2, 1), (4, 2)])
 def test_dask_api_vs_single_gpu(world, C):
     _spawn(_dask_worker, (world, _free_port(), C), world)
+
+
+def _csr(V, src, dst, w):
+    """CSR (offsets int64, indices int32, weights fp64) of a COO in ids [0, V), rows
+    sorted by destination (the compiled oracle's input)."""
+    order = np.lexsort((dst, src))
+    off = np.zeros(V + 1, np.int64)
+    np.cumsum(np.bincount(src, minlength=V), out=off[1:])
+    return off, dst[order].astype(np.int32), w[order].astype(np.float64)
+
+
+def _mg_rmat20_worker(rank, world, port, C, scale):
+    """The reference's MG test size (RMAT(20, 32): mg_pagerank_test.cpp:333-347,
+    mg_bfs_test.cpp:298, mg_louvain_test.cpp:270,307) on the reference's 8-GPU grid,
+    rehearsed with 8 ranks on the one test GPU over gloo -- several ranks, so none of the
+    one-rank shortcuts (the P == 1 contraction, the one-grid-row PageRank schedule) run.
+    The graph is R-MAT(scale, 16) with integer weights 1..8, symmetrised, generated on
+    the device by every rank (bit-identical to oracle/rmat.py).
+    * PageRank (unweighted) bit for bit per external id against single-GPU PageRank,
+      same iteration count;
+    * BFS (direction-optimising) from the largest hub: distances equal to SG's,
+      predecessors equal to SG's on the graph renumbered by the MG number map;
+    * Louvain (integer weights: every sum exact): each MG dendrogram level is the
+      compiled oracle's single-level Louvain (oracle/cpu_louvain.c, max_level 1) on the
+      level graph numbered by the MG ids -- the same partition and the same modularity
+      bits -- and the reported Q is the last improving level's
+      (mg_louvain_test.cpp:82-151's method).  The graph has rows far over 1024 edges
+      (the heavy-row passes k_big_*) and several levels (the P > 1 contraction's owner
+      exchange)."""
+    import sys
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    _rank_setup(port, rank)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pylibcugraph as plc
+
+    h1 = plc.ResourceHandle()
+    n = 16 << scale
+    s, d = plc.generators.generate_rmat_edgelist(h1, scale, n, 0.57, 0.19, 0.19, 7, False, True)
+    w = torch.floor(plc.generators.generate_edge_weights(h1, n, 8) * 8.0) + 1.0
+    s, d, w = plc.generators.symmetrize_dedup(h1, s, d, w, True)
+    E = s.numel()
+    lo, hi = rank * E // world, (rank + 1) * E // world
+    ctx = plc.comms.init_torch(C)
+    h = plc.ResourceHandle(ctx.ptr)
+    props = plc.GraphProperties(is_symmetric=True, is_multigraph=False)
+    part = lambda t: t[lo:hi].contiguous()  # noqa: E731
+    Gp = plc.MGGraph(h, props, part(s), part(d), None, store_transposed=True, num_edges=E)
+    v, x = plc.pagerank(h, Gp, None, None, None, None, 0.85, 1e-6, 500, False)
+    it = h.last_iterations()
+    Gp = None
+    Gb = plc.MGGraph(h, props, part(s), part(d), None, store_transposed=False, num_edges=E)
+    deg = torch.bincount(s.to(torch.int64))
+    root = int(torch.argmax(deg))
+    maxdeg = int(deg.max())
+    del deg
+    dd, pp, vb = plc.bfs(h, Gb, torch.tensor([root] if rank == 0 else [], dtype=torch.int32, device="cuda"), True,
+                         0, True, False)
+    bu = h.last_bfs_bottom_up_steps()
+    Gb = None
+    Gl = plc.MGGraph(h, props, part(s), part(d), part(w), store_transposed=False, num_edges=E)
+    lv_v, lv_c, q, levels = plc.louvain_dendrogram(h, Gl, 100, 1.0)
+    Gl = None
+    mine = (v.cpu().numpy(), x.cpu().numpy(), it, vb.cpu().numpy(), dd.cpu().numpy(), pp.cpu().numpy(), bu,
+            lv_v.cpu().numpy(), lv_c.cpu().numpy(), q, [t.cpu().numpy() for t in levels])
+    del v, x, vb, dd, pp, lv_v, lv_c, levels
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    if rank == 0:
+        from oracle import cpu_native
+        sh, dh, wh = s.cpu().numpy().astype(np.int64), d.cpu().numpy().astype(np.int64), w.cpu().numpy()
+        # -- PageRank: bitwise SG
+        vv = np.concatenate([a[0] for a in allr]).astype(np.int64)
+        xx = np.concatenate([a[1] for a in allr])
+        assert all(a[2] == it for a in allr)
+        G1 = plc.SGGraph(h1, props, s, d, None, store_transposed=True, renumber=True)
+        v1, x1 = plc.pagerank(h1, G1, None, None, None, None, 0.85, 1e-6, 500, False)
+        it1 = h1.last_iterations()
+        v1, x1 = v1.cpu().numpy().astype(np.int64), x1.cpu().numpy()
+        G1 = None
+        nx = int(max(vv.max(), v1.max())) + 1
+        a_mg, a_sg = np.zeros(nx, np.float32), np.zeros(nx, np.float32)
+        a_mg[vv], a_sg[v1] = xx, x1
+        assert np.array_equal(np.sort(vv), np.sort(v1))
+        print(f"RMAT-{scale} MG {world // C}x{C}: V={vv.size} E={E} max degree {maxdeg}; PageRank iterations MG {it} "
+              f"SG {it1}, equal bits {np.mean(a_mg[v1] == a_sg[v1]):.6f}; BFS bottom-up steps {[a[6] for a in allr]}")
+        assert it == it1
+        assert np.array_equal(a_mg.view(np.int32), a_sg.view(np.int32)), "MG PageRank differs from SG"
+        # -- BFS: distances = SG; predecessors = SG on the MG-numbered graph
+        vb_all = np.concatenate([a[3] for a in allr]).astype(np.int64)
+        db_all = np.concatenate([a[4] for a in allr])
+        pb_all = np.concatenate([a[5] for a in allr]).astype(np.int64)
+        assert max(a[6] for a in allr) > 0
+        Gs = plc.SGGraph(h1, props, s, d, None, store_transposed=False, renumber=True)
+        d1, _, u1 = plc.bfs(h1, Gs, torch.tensor([root], dtype=torch.int32, device="cuda"), True, 0, True, False)
+        dist_sg = np.full(nx, -7, np.int64)
+        dist_sg[u1.cpu().numpy()] = d1.cpu().numpy()
+        Gs = None
+        assert np.array_equal(db_all, dist_sg[vb_all]), "MG BFS distances differ from SG"
+        inv = np.zeros(nx, dtype=np.int64)
+        inv[vb_all] = np.arange(vb_all.size)
+        dev = lambda a: torch.as_tensor(np.ascontiguousarray(a).astype(np.int32), device="cuda")  # noqa: E731
+        Gm = plc.SGGraph(h1, props, dev(inv[sh]), dev(inv[dh]), None, store_transposed=False, renumber=False)
+        d2, p2, u2 = plc.bfs(h1, Gm, dev([inv[root]]), True, 0, True, False)
+        Gm = None
+        assert np.array_equal(u2.cpu().numpy(), np.arange(vb_all.size))
+        assert np.array_equal(d2.cpu().numpy(), db_all)
+        pm = np.where(pb_all >= 0, inv[np.maximum(pb_all, 0)], -1)
+        assert np.array_equal(p2.cpu().numpy().astype(np.int64), pm), "MG BFS predecessors differ from SG"
+        # -- Louvain, level by level against the compiled oracle on the MG numbering
+        nmap = np.concatenate([a[7] for a in allr]).astype(np.int64)
+        assert np.array_equal(np.sort(nmap), np.sort(vb_all))
+        inv = np.zeros(nx, dtype=np.int64)
+        inv[nmap] = np.arange(nmap.size)
+        L = len(allr[0][10])
+        lv = [np.concatenate([a[10][i] for a in allr]).astype(np.int64) for i in range(L)]
+        gs, gd, gw, V = inv[sh], inv[dh], wh.astype(np.float64), nmap.size
+        best, qs = -1.0, []
+        for i in range(L):
+            assert lv[i].size == V
+            off, idx, ww = _csr(V, gs, gd, gw)
+            oc, oq, _ = cpu_native.louvain(off, idx, ww, max_level=1, threads=16)
+            assert _same_partition(oc, lv[i]), f"level {i}: MG differs from the oracle's single level"
+            qs.append(oq)
+            if oq <= best:
+                assert i == L - 1, "MG went on after a level without gain"
+                break
+            best = oq
+            if i + 1 < L:  # coarsen by the MG level (mg_louvain_helper coarsen_graph)
+                m = lv[i].max() + 1
+                uk, inv_k = np.unique(lv[i][gs] * m + lv[i][gd], return_inverse=True)
+                gw = np.bincount(inv_k, weights=gw)
+                gs, gd = uk // m, uk % m
+                V = lv[i + 1].size
+        assert all(a[9] == q for a in allr)
+        print(f"RMAT-{scale} MG Louvain {world} ranks: {L} levels, Q {q!r}, oracle per level {qs}")
+        assert L >= 2, "a single level leaves the P > 1 contraction unexercised"
+        assert q == best, (q, best)  # integer weights: the same bits
+        flat = np.arange(nmap.size)
+        for x_ in lv:
+            flat = x_[flat]
+        assert np.array_equal(np.concatenate([a[8] for a in allr]).astype(np.int64), flat)
+    dist.barrier()
+    h = None
+    ctx.free()
+    dist.destroy_process_group()
+
+
+def test_mg_world8_rmat20_equals_sg():
+    """8 ranks, the reference's 4 x 2 grid, RMAT-20 (see _mg_rmat20_worker)."""
+    _spawn(_mg_rmat20_worker, (8, _free_port(), 2, 20), 8, deadline=600.0)

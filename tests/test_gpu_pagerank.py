@@ -120,6 +120,55 @@ def test_rmat_float64_and_int64():
     assert np.max(np.abs(got[vv] - ref_ext[vv]) / ref_ext[vv]) < 1e-9
 
 
+def _fp64_vs_oracle(got, ref, it_gpu, it_ref, what):
+    """fp64 at size: with the same iteration count the two differ only by rounding
+    (the push's 2^-62 fixed point against fp64 sums), so 1e-10 relative; a
+    quantisation of 2^-52 (fp32's scale) puts low-degree x~ terms (~2^-26 at RMAT-20)
+    at ~1e-8 and fails it."""
+    rel = np.abs(got - ref) / ref
+    print(f"{what}: iterations gpu {it_gpu} oracle {it_ref}, max rel {rel.max():.3e}")
+    assert it_gpu == it_ref
+    assert rel.max() < 1e-10, rel.max()
+
+
+def test_rmat20_float64_unit_weights_vs_compiled_oracle():
+    """fp64 PageRank at RMAT-20 (symmetric, all-ones fp64 weights: the packed
+    unweighted push with R = double) against the compiled fp64 oracle on the
+    library's own CSC (internal ids), epsilon 1e-10."""
+    import torch
+    from oracle import cpu_native
+    p = plc()
+    h = p.ResourceHandle()
+    n = 16 << 20
+    s, d = p.generators.generate_rmat_edgelist(h, 20, n, 0.57, 0.19, 0.19, 42, False, True)
+    s, d, _ = p.generators.symmetrize_dedup(h, s, d, None, True)
+    w = torch.ones(s.numel(), dtype=torch.float64, device=s.device)
+    G = p.SGGraph(h, p.GraphProperties(is_symmetric=True, is_multigraph=False), s, d, w, store_transposed=True,
+                  renumber=True)
+    v, pr = p.pagerank(h, G, None, None, None, None, 0.85, 1e-10, 1000, False)
+    assert str(pr.dtype) == "torch.float64"
+    it_gpu = h.last_iterations()
+    off, idx, _ = G.adjacency(h, transposed=True)
+    ref, it_ref = cpu_native.pagerank_f64(host(off).astype(np.int64), host(idx), 0.85, 1e-10, 1000, threads=8)
+    _fp64_vs_oracle(host(pr), ref, it_gpu, it_ref, f"RMAT-20 fp64 unit weights V={ref.size} E={idx.numel()}")
+
+
+def test_rmat18_float64_weighted_vs_oracle():
+    """fp64 PageRank with random fp64 weights at RMAT-18 (the 32-bit entry + weight
+    push, to_fixed<double>) against the numpy fp64 oracle, epsilon 1e-10."""
+    s, d, w = rmat_graph(18, True)
+    h, G = make_graph(s, d, w, transposed=True, renumber=True, symmetric=True, wdtype=np.float64)
+    v, pr = plc().pagerank(h, G, None, None, None, None, 0.85, 1e-10, 1000, False)
+    it_gpu = h.last_iterations()
+    og_g = og.create_graph(s, d, w, store_transposed=True, renumber=True)
+    ref, it_ref = opr.pagerank_from_graph(og_g, alpha=0.85, epsilon=1e-10, max_iterations=1000,
+                                          return_iterations=True)
+    ref_ext = np.zeros(int(og_g.number_map.max()) + 1)
+    ref_ext[og_g.number_map] = ref
+    vv = host(v)
+    _fp64_vs_oracle(by_ext(v, pr)[vv], ref_ext[vv], it_gpu, it_ref, "RMAT-18 fp64 weighted")
+
+
 def test_initial_guess_and_precomputed_outw():
     s, d, _ = rmat_graph(10, False)
     h, G = make_graph(s, d, None, transposed=True, renumber=True, symmetric=True)
