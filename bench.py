@@ -31,6 +31,9 @@ Extra fields on the same JSON line:
                       8 roots), its roofline (4E_cc + 16V_cc per traversal) and PMC
                       traffic, and CPU baselines (NetworkX on a bounded sample,
                       compiled C restatement on the same graph).
+  sssp             -- (N=1) SSSP (near-far) on the BFS graph with uniform [0, 1)
+                      weights from 4 roots: MTEPS, rounds, PMC traffic, and the
+                      compiled near-far restatement as CPU baseline.
   louvain          -- configs[4]: Louvain time-to-solution on RMAT 23 + log2(N)
                       (RMAT-26 at 8 GPUs), uniform weights.
 
@@ -538,6 +541,112 @@ def bfs_leg(p, args, child=False):
     return out
 
 
+# ----------------------------------------------------------------------------- SSSP
+SSSP_KERNELS = ("k_relax", "k_split", "k_sssp_", "k_pred_none", "k_weight_stats")
+
+
+def sssp_leg(p, args, child=False):
+    """SSSP (near-far, csrc/sssp.hip) on the BFS leg's graph with the bench's uniform
+    [0, 1) fp32 weights (seed 43, cugraph_funcs.py:56-58; the reference benchmarks SSSP
+    beside BFS, benchmarks/python_e2e/cugraph_funcs.py:122-123) from the first
+    sssp_roots Graph500 roots, predecessors on; per source the median of bfs_reps timed
+    calls.  TEPS counting as BFS (undirected edges of the source's component / time)."""
+    import torch
+    h = p.ResourceHandle(args.ctx.ptr if args.ctx else None)
+    ab_options(h, args)
+    scale = args.bfs_scale
+    g, roots, _ = build_rmat_graph(p, h, scale, weighted=True, transposed=False, want_roots=args.bfs_roots)
+    roots = roots[:args.sssp_roots]
+    V, E = g.number_of_vertices(), g.number_of_edges()
+    off, _, _ = g.adjacency(h, transposed=False)
+    deg_int = (off[1:] - off[:-1]).to(torch.int64)
+    del off
+    times, rates, rounds, spread, bytes_alg, reached_n = [], [], [], [], [], []
+    number_map = None
+    first_ms = None
+    for i, r in enumerate(roots):
+        if child:
+            p.sssp(h, g, int(r), float("inf"), True, False)
+            continue
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = p.sssp(h, g, int(r), float("inf"), True, False)  # warm (the first: per-graph work inside)
+        torch.cuda.synchronize()
+        if i == 0:
+            first_ms = (time.perf_counter() - t0) * 1e3
+        samples = []
+        for _ in range(args.bfs_reps):
+            res = None
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = p.sssp(h, g, int(r), float("inf"), True, False)
+            torch.cuda.synchronize()
+            samples.append(time.perf_counter() - t0)
+        verts, dist, _ = res
+        if number_map is None:
+            number_map = verts
+        t = sorted(samples)[len(samples) // 2]
+        reached = dist < torch.finfo(dist.dtype).max
+        e_cc = int(deg_int[reached].sum().item())
+        v_cc = int(reached.sum().item())
+        times.append(t)
+        spread.append((min(samples), max(samples)))
+        rates.append((e_cc / 2) / t / 1e6)
+        rounds.append(h.last_iterations())
+        reached_n.append(v_cc)
+        # algorithmic bytes: every reached vertex's adjacency (4 B index + 4 B weight per
+        # edge) and offsets (8 B), its distance and predecessor (4 + 4 B)
+        bytes_alg.append(8 * e_cc + 16 * v_cc)
+        del res, verts, dist, reached
+    if child:
+        return None
+    hm = len(rates) / sum(1.0 / m for m in rates)
+    achieved = sum(bytes_alg) / sum(times) / 1e9
+    out = {"scale": scale, "vertices": V, "edges": E, "weights": "uniform [0,1) fp32, seed 43", "roots": len(rates),
+           "mteps_harmonic_mean": hm, "ms_mean": 1e3 * sum(times) / len(times),
+           "ms_per_root_median": [round(1e3 * x, 4) for x in times],
+           "ms_per_root_min_max": [[round(1e3 * a, 4), round(1e3 * b, 4)] for a, b in spread],
+           "reps_per_root": args.bfs_reps, "rounds": rounds, "reached": reached_n,
+           "first_call_ms": round(first_ms, 3), "predecessors": True,
+           "teps_counting": "Graph500: undirected edges of the source component / time",
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "achieved_kind": "algorithmic-equivalent: 8 E_cc + 16 V_cc per traversal (each reached "
+                                         "adjacency read once with its weights) / time",
+                        "ms_per_traversal": 1e3 * sum(times) / len(times)}}
+    if args.rank == 0 and args.world == 1 and not args.no_cpu_baseline:
+        try:
+            import numpy as np
+            from oracle import cpu_native
+            off, idx, w = g.adjacency(h, transposed=False)
+            off, idx, w = off.cpu().numpy().astype(np.int64), idx.cpu().numpy(), w.cpu().numpy()
+            nm = number_map.cpu().numpy()
+            root_int = int(np.nonzero(nm == roots[0])[0][0])
+            t1, d1, _, rr = cpu_native.sssp(off, idx, w, root_int)
+            e_cc = int((off[1:] - off[:-1])[d1 < np.finfo(np.float32).max].sum())
+            out["cpu_baseline"] = {
+                "kind": "port", "source": "oracle/cpu_sssp.c (sssp_impl.cuh:79-270 near-far restated, fp32)",
+                "value": (e_cc / 2) / t1 / 1e6, "unit": "MTEPS", "cores": 1, "seconds": t1, "rounds": rr,
+                "sample": f"one traversal from the first root on the same RMAT-{scale} graph, predecessors "
+                          "resolved after the timed loop",
+                "host": host_info(1)}
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline"] = {"error": repr(e)[:200]}
+    return out
+
+
+def sssp_traffic(args):
+    """HBM bytes per SSSP traversal (every SSSP kernel), 2 x FETCH_SIZE + WRITE_SIZE."""
+    per = {}
+    child = ["--traffic-child", "sssp", "--bfs-scale", str(args.bfs_scale), "--bfs-roots", str(args.bfs_roots),
+             "--sssp-roots", str(args.sssp_roots)]
+    n = args.sssp_roots
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        vals = pmc_pass(ctr, child, SSSP_KERNELS)
+        per[ctr] = sum(sum(v) for v in vals.values()) / n
+    return (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0, per
+
+
 # ----------------------------------------------------------------------------- Louvain
 def louvain_leg(p, args, scale=None):
     """configs[4]: Louvain time-to-solution on a symmetrised R-MAT graph with uniform
@@ -628,6 +737,9 @@ def main():
     ap.add_argument("--bfs-scale", type=int, default=24)
     ap.add_argument("--bfs-roots", type=int, default=8)
     ap.add_argument("--bfs-reps", type=int, default=5, help="timed traversals per root (median reported)")
+    ap.add_argument("--sssp", dest="sssp", action="store_true", default=True)
+    ap.add_argument("--no-sssp", dest="sssp", action="store_false")
+    ap.add_argument("--sssp-roots", type=int, default=4, help="SSSP sources (the first BFS roots)")
     ap.add_argument("--no-rmat26", dest="rmat26", action="store_false", default=True,
                     help="skip the one-GPU RMAT-26 PageRank and Louvain legs (configs[3]/[4]'s graph)")
     ap.add_argument("--louvain", dest="louvain", action="store_true", default=True)
@@ -643,7 +755,8 @@ def main():
                     help="MG collectives: RCCL inside libcugraph_c (default), or torch.distributed callbacks "
                          "(code-path rehearsal with several ranks on one GPU; not a performance number)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
-    ap.add_argument("--traffic-child", choices=["pagerank", "bfs"], default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--traffic-child", choices=["pagerank", "bfs", "sssp"], default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--sssp-only", action="store_true", help="A/B aid: only the SSSP leg, its dict on stdout")
     ap.add_argument("--bfs-only", action="store_true", help="A/B aid: only the BFS leg, its dict on stdout")
     ap.add_argument("--louvain-only", action="store_true", help="A/B aid: only the Louvain leg, its dict on stdout")
     ap.add_argument("--options", default="", help="A/B aid: handle options name=value,... for the BFS / Louvain legs")
@@ -683,6 +796,15 @@ def main():
         return
     if args.traffic_child == "bfs":
         bfs_leg(p, args, child=True)
+        return
+    if args.traffic_child == "sssp":
+        sssp_leg(p, args, child=True)
+        return
+    if args.sssp_only:
+        r = sssp_leg(p, args)
+        log(f"[bench] sssp RMAT-{args.bfs_scale}: {r['mteps_harmonic_mean']:.1f} MTEPS, {r['ms_mean']:.3f} ms/traversal, "
+            f"rounds {r['rounds']}")
+        print(json.dumps(r), flush=True)
         return
     if args.bfs_only:
         r = bfs_leg(p, args)
@@ -829,6 +951,14 @@ def main():
         except Exception as e:  # noqa: BLE001
             out["bfs"] = {"status": "failed", "error": repr(e)[:300]}
         release_caches(p)
+    if args.sssp and world == 1:
+        try:
+            out["sssp"] = sssp_leg(p, args)
+            log(f"[bench] sssp RMAT-{args.bfs_scale}: {out['sssp']['mteps_harmonic_mean']:.1f} MTEPS, "
+                f"{out['sssp']['ms_mean']:.3f} ms/traversal, rounds {out['sssp']['rounds']}")
+        except Exception as e:  # noqa: BLE001
+            out["sssp"] = {"status": "failed", "error": repr(e)[:300]}
+        release_caches(p)
     if args.louvain:
         try:
             out["louvain"] = louvain_leg(p, args)
@@ -868,6 +998,17 @@ def main():
                     f"--pmc passes over one traversal per root: {detail}")
             except Exception as e:  # noqa: BLE001
                 out["bfs"]["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]
+        if isinstance(out.get("sssp"), dict) and "roofline" in out["sssp"]:
+            try:
+                tb, detail = sssp_traffic(args)
+                out["sssp"]["roofline"]["traffic"] = tb
+                ms_t = out["sssp"]["roofline"]["ms_per_traversal"]
+                out["sssp"]["roofline"]["frac_counter"] = tb / (ms_t * 1e-3) / 1e9 / HBM_PEAK_GBS
+                out["sssp"]["roofline"]["traffic_note"] = (
+                    "HBM bytes per traversal (every SSSP kernel) = 2 x FETCH_SIZE + WRITE_SIZE (KiB) from "
+                    f"separate rocprofv3 --pmc passes over one traversal per root: {detail}")
+            except Exception as e:  # noqa: BLE001
+                out["sssp"]["roofline"]["traffic_note"] = f"unavailable: {e!r}"[:300]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             nxb = networkx_cpu_legs(args)

@@ -57,6 +57,7 @@ struct tuning_t {
   int louvain_big_cap  = 0;     // (row, bucket) table cap below the built-in one (tests of the fallback)
   int64_t louvain_big_maxdeg = 0;  // heavy rows above this degree on the sort path (0: the table limit)
   bool louvain_wide_keys = false;  // 64-bit hash keys below 2^24 ids (tests)
+  double sssp_delta    = 0;     // SSSP delta = sssp_delta * average weight / average degree (0: sssp.hip kDeltaScale)
 };
 
 struct handle_t {
@@ -216,6 +217,10 @@ struct adjacency_t {
   // built on the first direction-optimising BFS and kept for the adjacency's lifetime like pr and
   // items (freed with the graph; trim_device_cache returns only the allocator's free blocks)
   buffer bfs_head;
+  double wsum = -1;  // SSSP: sum of the weights (delta), cached on first use; -1 = not known yet
+  // SSSP (sssp.hip): the adjacency with each row's light edges (w < delta) first, for one delta
+  double sssp_delta = -1;
+  buffer sssp_idx, sssp_w, sssp_nlight;
   pr_push_t pr;  // PageRank windowed-push schedule (pagerank.hip), built on first use
 };
 

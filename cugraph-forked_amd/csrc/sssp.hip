@@ -1,214 +1,617 @@
-// Single-source shortest paths, near-far (Davidson et al.) on the GPU.
+// Single-source shortest paths on the GPU: near-far buckets (Davidson et al., the
+// reference's scheme) with light / heavy edges (Meyer and Sanders' delta-stepping).
 //
 // Reference: cpp/src/traversal/sssp_impl.cuh:79-270 (+ c_api/sssp.cpp:60-145):
 // distances start at numeric_limits<weight_t>::max(), a relaxation dist[u] + w is
 // kept only if it is < min(cutoff, dist[v]) (e_op :49-72); the frontier is split
 // into near / far piles by a threshold that grows by delta (:143-157, :235-262).
+// Every vertex there relaxes all its edges each time it is processed; on RMAT-24
+// with the bench's weights that is 3-6 E of relaxations per traversal (the compiled
+// restatement counts 3.0 E at RMAT-20).  Here a bucket [lo, thr) relaxes only its
+// vertices' light edges (w < delta) while it fills, then each of its vertices' heavy
+// edges once, when the bucket is done: a heavy edge lands at d + w >= lo + delta =
+// thr (rounding is monotone and thr is computed as the same fp sum), outside the
+// bucket, so nothing the bucket settles changes by it.  The distances are the same
+// fixed point (the minimum over paths of the left-folded weight_t sums below the
+// cutoff); the order of work differs.
 //
-// Here: distances are relaxed with atomicMin on their bit patterns (non-negative
-// IEEE values order like integers); each round appends every improved vertex once
-// (a round stamp per vertex) to a "changed" list, which is then split by the
-// current threshold into the next near frontier (by degree class, as the BFS
-// queues) or the far pile.  Predecessors are resolved once at the end: the
-// smallest internal id among in-neighbours u with dist[u] + w == dist[v]
+// Every round runs on the device with no host read in between:
+//  * a frontier list lives in an edge space: each appended vertex gets a slot and
+//    the start of its edges from one 64-bit counter, (slots << eb) | edges, added
+//    once per wave stage, and the slot holding the start of every 2048-edge chunk is
+//    recorded;
+//  * k_relax: persistent blocks take 2048-edge chunks of the near list's light edges
+//    (light round) or the bucket list's heavy edges (heavy round) -- a hub's 400K
+//    edges spread over the grid, a chunk of low-degree vertices holds up to 2048 of
+//    them -- find each position's vertex by a max-scan of the chunk's slot starts in
+//    LDS, load 8 edges a thread coalesced with every load issued before the first
+//    compare, and relax with non-returning atomicMin on the distance's bit pattern
+//    (non-negative IEEE values order like integers), marking every improved vertex
+//    in a changed bitmap;
+//  * k_split: the changed bitmap (V / 8 bytes, read and cleared whole): below thr ->
+//    the next near list and (once per bucket) the bucket list; otherwise the vertex
+//    is in the far set, whose smallest distance is kept;
+//  * k_sssp_ctl: the next round -- light while the near list fills, one heavy round
+//    when it empties, then a far split (split_bucket, :235-262) with the threshold
+//    raised past the smallest far distance (the reference raises it by delta until
+//    the near bucket fills: the same buckets, fewer empty passes);
+//  * k_far_split: a dense pass over the distances -- [old, thr) to the near list, the
+//    far set's minimum -- instead of a pile of ids (the reference's far bucket: each
+//    split re-reads every far entry in arbitrary order, 0.3-0.5 ms a split at
+//    RMAT-24); k_sssp_fin: the termination flag.
+// The state lives in one device block; the host enqueues kChunkRounds rounds and
+// reads the state once per chunk (rounds after termination return at once).  Every
+// grid is fixed and grid-strides over device-side counts.  The light-first copy of
+// the adjacency is built once per graph and delta (adjacency_t::sssp_*).
+// Predecessors are resolved once at the end by a pull over the in-edges (sorted
+// ascending): the first -- smallest-id -- in-neighbour u with dist[u] + w == dist[v]
 // (deterministic; every reference golden vector satisfies it).
 #include "capi.hpp"
 #include "prims.hpp"
 
 #include <cfloat>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 
 namespace cgx {
 
 namespace {
 
-constexpr int kSmallDeg = 16;
-constexpr int kMidDeg   = 1024;
+constexpr int kChunk       = 2048;  // edges per relax work item: 256 threads x 8
+constexpr int kPerThread   = kChunk / 256;
+constexpr int kRelaxGrid   = 1024;  // persistent relax blocks (LDS: 4 per CU)
+constexpr int kSplitGrid   = 1024;
+constexpr int kStage       = 128;   // staged entries per wave and list
+constexpr int kChunkRounds = 8;     // rounds enqueued per host read
+// delta = kDeltaScale * average weight / average degree (tuning_t::sssp_delta)
+constexpr double kDeltaScale = 8.0;
 
 template <typename W>
 struct bits_of;
 template <>
 struct bits_of<float> {
-  using type = int;
+  using type  = int;
+  using utype = unsigned int;
 };
 template <>
 struct bits_of<double> {
-  using type = long long;
+  using type  = long long;
+  using utype = unsigned long long;
 };
 
+enum : int { kLight = 0, kHeavy = 1 };
+
+// device-side state of one SSSP call (counters 128 B apart: same-address atomics of
+// different counters do not share a line)
 template <typename W>
-__device__ __forceinline__ W atomic_min_nonneg(W* p, W x)
-{
-  using B = typename bits_of<W>::type;
-  B old   = atomicMin(reinterpret_cast<B*>(p), *reinterpret_cast<B*>(&x));
-  return *reinterpret_cast<W*>(&old);
-}
+struct sssp_state {
+  unsigned long long nq[2][16];   // near lists by parity: (slots << eb) | light edges
+  unsigned long long nr[2][16];   // bucket lists (the bucket's vertices): (slots << eb) | heavy edges
+  typename bits_of<W>::utype minfar;  // smallest distance at or past thr noted since the last far split
+  W thr, old, delta;
+  int fs;     // this round splits the far set
+  int phase;  // the next relax: kLight (near list nq[P]) or kHeavy (bucket list nr[hl])
+  int rp;     // bucket list receiving this bucket's vertices
+  int hl;     // bucket list a heavy round relaxes
+  int epoch;  // a vertex joins bucket list rp once per epoch (stamp)
+  int done;
+  int bad;    // the source is not a vertex
+  unsigned long long rounds;  // relax rounds with work
+  unsigned long long work[16][16];  // CGX_SSSP_TRACE partials: [p][0] light edges, [p][1] vertices improved,
+                                    // [p][2] distance atomics, [p][3] heavy edges
+};
 
-__device__ __forceinline__ long long wave_append(unsigned long long* tail, bool take)
-{
-  unsigned long long mask = __ballot(take);
-  if (mask == 0) return -1;
-  int lane   = threadIdx.x & 63;
-  int leader = __ffsll((long long)mask) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(tail, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader, 64);
-  if (!take) return -1;
-  return (long long)(base + __popcll(mask & ((1ull << lane) - 1ull)));
-}
-
-struct sssp_ctr {
-  unsigned long long changed;
-  unsigned long long near[3];
-  unsigned long long far;
-  unsigned long long pad[3];
+// one frontier list in an edge space: vertex, first edge in the list's edge space,
+// and the slot holding edge c * kChunk
+template <typename V>
+struct flist {
+  V* q;
+  int64_t* ep;
+  int64_t* cs;
 };
 
 template <typename V, typename E, typename W>
 struct sssp_args {
   E const* off;
-  V const* idx;
+  V const* idx;       // adjacency with each row's light edges (w < delta) first, then its heavy ones
   W const* wgt;
+  int const* nlight;  // light edges per row
   W* dist;
-  int* stamp;
-  int round;
+  int* stamp;         // bucket-list epoch of each vertex
   W cutoff;
-  V const* q[3];
-  unsigned long long n[3];
-  V* changed;
-  sssp_ctr* ctr;
-  long long blk_mid_start, blk_small_start;
+  flist<V> near[2];    // by parity
+  flist<V> bucket[2];  // by index (rp / hl)
+  uint32_t* cbits;     // the round's changed vertices (a bit each), cleared by k_split
+  sssp_state<W>* st;
+  int64_t nv;
+  int eb;     // edge field bits of the list counters
+  int trace;  // CGX_SSSP_TRACE: count the work (debug output only)
 };
 
-template <typename V, typename E, typename W>
-__device__ __forceinline__ void relax(sssp_args<V, E, W> const& a, W du, E e, bool act)
-{
-  bool take = false;
-  V v       = 0;
-  if (act) {
-    v    = a.idx[e];
-    W nd = du + a.wgt[e];
-    if (nd < a.cutoff && nd < a.dist[v]) {
-      W old = atomic_min_nonneg<W>(a.dist + v, nd);
-      if (nd < old) take = atomicExch(a.stamp + v, a.round) != a.round;
-    }
-  }
-  long long slot = wave_append(&a.ctr->changed, take);
-  if (slot >= 0) a.changed[slot] = v;
-}
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-template <typename V, typename E, typename W>
-__global__ __launch_bounds__(256) void k_relax(sssp_args<V, E, W> a)
-{
-  long long b = blockIdx.x;
-  int tid     = threadIdx.x;
-  if (b < a.blk_mid_start) {
-    for (long long i = b; i < (long long)a.n[2]; i += a.blk_mid_start) {
-      V u  = a.q[2][i];
-      W du = a.dist[u];
-      E beg = a.off[u], end = a.off[u + 1];
-      for (E base = beg; base < end; base += 256) relax<V, E, W>(a, du, base + tid, base + tid < end);
-    }
-  } else if (b < a.blk_small_start) {
-    long long nb   = a.blk_small_start - a.blk_mid_start;
-    long long widx = (b - a.blk_mid_start) * 4 + (tid >> 6);
-    int lane       = tid & 63;
-    for (long long i = widx; i < (long long)a.n[1]; i += nb * 4) {
-      V u  = a.q[1][i];
-      W du = a.dist[u];
-      E beg = a.off[u], end = a.off[u + 1];
-      for (E base = beg; base < end; base += 64) relax<V, E, W>(a, du, base + lane, base + lane < end);
-    }
-  } else {
-    long long nb = gridDim.x - a.blk_small_start;
-    int lane     = tid & 3;
-    for (long long i0 = (b - a.blk_small_start) * 64; i0 < (long long)a.n[0]; i0 += nb * 64) {
-      long long i = i0 + (tid >> 2);
-      bool have   = i < (long long)a.n[0];
-      V u         = have ? a.q[0][i] : V(0);
-      W du        = have ? a.dist[u] : W(0);
-      E beg = have ? a.off[u] : E(0), end = have ? a.off[u + 1] : E(0);
-      for (int r = 0; r < kSmallDeg / 4; ++r) {
-        E e = beg + r * 4 + lane;
-        relax<V, E, W>(a, du, e, e < end);
-      }
-    }
-  }
-}
-
-// Split a vertex list by the current distances.
-//  from_far == false (the round's changed list, unique): dist < hi -> near queue (by
-//    degree class); otherwise -> far pile, unless already in it (infar flag).
-//  from_far == true (the far pile, unique by the infar invariant): dist < lo -> drop
-//    (it was improved into an earlier near pile and processed there); dist < hi ->
-//    near; else stays in the far pile (written to `far`).
-template <typename V, typename E, typename W>
-__global__ void k_split(V const* in, unsigned long long n, W const* dist, E const* off, W lo, W hi, int* infar,
-                        bool from_far, V* near0, V* near1, V* near2, V* far, sssp_ctr* ctr)
-{
-  for (unsigned long long base = blockIdx.x * (unsigned long long)blockDim.x; base < n;
-       base += (unsigned long long)gridDim.x * blockDim.x) {
-    unsigned long long i = base + threadIdx.x;
-    bool have            = i < n;
-    V v                  = have ? in[i] : V(0);
-    W d                  = have ? dist[v] : W(0);
-    bool is_near = false, to_far = false;
-    if (have) {
-      if (from_far) {
-        infar[v] = 0;
-        if (d >= lo) {
-          is_near = d < hi;
-          to_far  = !is_near;
-          if (to_far) infar[v] = 1;
-        }
-      } else {
-        is_near = d < hi;
-        if (!is_near) to_far = atomicExch(infar + v, 1) == 0;
-      }
-    }
-    int cls = 0;
-    if (is_near) {
-      E deg = off[v + 1] - off[v];
-      cls   = deg <= kSmallDeg ? 0 : (deg <= kMidDeg ? 1 : 2);
-    }
-    long long s0 = wave_append(&ctr->near[0], is_near && cls == 0);
-    long long s1 = wave_append(&ctr->near[1], is_near && cls == 1);
-    long long s2 = wave_append(&ctr->near[2], is_near && cls == 2);
-    long long sf = wave_append(&ctr->far, to_far);
-    if (s0 >= 0) near0[s0] = v;
-    if (s1 >= 0) near1[s1] = v;
-    if (s2 >= 0) near2[s2] = v;
-    if (sf >= 0) far[sf] = v;
-  }
-}
-
-template <typename V, typename E, typename W>
-__global__ void k_sssp_pred(E const* off, V const* idx, W const* wgt, W const* dist, int64_t nv, V src, V* pred)
-{
-  // thread per source vertex u: for each out-edge (u, v) tight -> atomicMin(pred[v], u)
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < nv; u += (int64_t)gridDim.x * blockDim.x) {
-    W du = dist[u];
-    if (du == std::numeric_limits<W>::max()) continue;
-    for (E e = off[u]; e < off[u + 1]; ++e) {
-      V v = idx[e];
-      if (v == src) continue;
-      if (du + wgt[e] == dist[v]) {
-        if constexpr (sizeof(V) == 4) atomicMin(reinterpret_cast<int*>(pred + v), (int)u);
-        else atomicMin(reinterpret_cast<long long*>(pred + v), (long long)u);
-      }
-    }
-  }
-}
-
+// A wave's appends to one frontier list (vertex, edges) staged in its own LDS slice
+// and moved out with one 64-bit atomic per full slice: slots and edge starts come
+// from the same add, so both are monotonic in slot order (every wave appending with
+// its own atomic to one list counter serialised at the memory side: the first
+// version's changed list took 148 ms per RMAT-24 traversal that way).  Every call
+// is made by the whole wave (wave-uniform control flow).
 template <typename V>
-__global__ void k_pred_none(V* pred, int64_t n, V none)
+struct edge_stage {
+  V* vb;
+  uint32_t* db;
+  int n;
+  __device__ __forceinline__ void flush(flist<V> const& L, unsigned long long* ctr, int eb)
+  {
+    if (n == 0) return;
+    __builtin_amdgcn_wave_barrier();
+    int const lane     = lane_id();
+    constexpr int kPer = kStage / 64;  // entries per lane, contiguous
+    unsigned long long d[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      int const i = lane * kPer + k;
+      d[k]        = i < n ? (unsigned long long)db[i] : 0ull;
+      sum += d[k];
+    }
+    unsigned long long pre = sum;  // inclusive wave scan of the lane sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      unsigned long long const y = __shfl_up(pre, o, 64);
+      if (lane >= o) pre += y;
+    }
+    unsigned long long const total = __shfl(pre, 63, 64);
+    pre -= sum;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(ctr, ((unsigned long long)n << eb) | total);
+    base                = __shfl(base, 0, 64);
+    int64_t const slot0 = (int64_t)(base >> eb);
+    int64_t e           = (int64_t)(base & ((1ull << eb) - 1ull)) + (int64_t)pre;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      int const i = lane * kPer + k;
+      if (i < n) {
+        int64_t const slot = slot0 + i;
+        L.q[slot]          = vb[i];
+        L.ep[slot]         = e;
+        for (int64_t c = (e + kChunk - 1) / kChunk; c * kChunk < e + (int64_t)d[k]; ++c) L.cs[c] = slot;
+        e += (int64_t)d[k];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    n = 0;
+  }
+  __device__ __forceinline__ void push(flist<V> const& L, unsigned long long* ctr, int eb, bool take, V v,
+                                       uint32_t deg)
+  {
+    unsigned long long const m = __ballot(take);
+    int const lane             = lane_id();
+    if (take) {
+      int const i = n + __popcll(m & ((1ull << lane) - 1ull));
+      vb[i]       = v;
+      db[i]       = deg;
+    }
+    n += __popcll(m);
+    if (n > kStage - 64) flush(L, ctr, eb);
+  }
+};
+
+// A wave's stages of the two lists a split fills (LDS slices of the block)
+template <typename V>
+struct split_stages {
+  edge_stage<V> nst, bst;
+};
+
+#define CGX_SPLIT_LDS(V)                                \
+  __shared__ V s_v[4][kStage], s_b[4][kStage];          \
+  __shared__ uint32_t s_dn[4][kStage], s_db[4][kStage]; \
+  int const wv_ = threadIdx.x >> 6;                     \
+  split_stages<V> sg{{s_v[wv_], s_dn[wv_], 0}, {s_b[wv_], s_db[wv_], 0}}
+
+// The smallest of every thread's v into st->minfar: one atomic per block (every
+// thread of the block calls)
+template <typename W>
+__device__ __forceinline__ void block_min_far(sssp_state<W>* st, W v)
 {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    if (pred[i] == none) pred[i] = (V)-1;
+  using U = typename bits_of<W>::utype;
+  __shared__ W s_m[4];
+  for (int o = 32; o > 0; o >>= 1) {
+    W const y = __shfl_xor(v, o, 64);
+    v         = y < v ? y : v;
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) v = s_m[w] < v ? s_m[w] : v;
+    if (v < std::numeric_limits<W>::max()) atomicMin(&st->minfar, *reinterpret_cast<U const*>(&v));
+  }
+}
+
+// A vertex at distance d with `light` light and `heavy` heavy edges leaving a split:
+// below thr -> the next near list (its light edges) and, once per bucket epoch, the
+// bucket list (its heavy edges, relaxed when the bucket is done); otherwise it is
+// in the far set (every reached vertex at or past thr), whose smallest distance is
+// kept in fmin.  Vertices without edges go nowhere.
+template <typename V, typename E, typename W>
+__device__ __forceinline__ void route(sssp_args<V, E, W> const& a, split_stages<V>& sg, int Q, bool have, V v, W d,
+                                      W thr, uint32_t light, uint32_t heavy, W& fmin)
+{
+  sssp_state<W>* st = a.st;
+  bool const live   = have && light + heavy > 0;
+  bool const near   = live && d < thr;
+  bool to_bucket    = false;
+  if (near && heavy > 0) to_bucket = atomicExch(a.stamp + v, st->epoch) != st->epoch;
+  if (live && !near) fmin = d < fmin ? d : fmin;
+  int const rp = st->rp;
+  sg.nst.push(a.near[Q], &st->nq[Q][0], a.eb, near && light > 0, v, light);
+  sg.bst.push(a.bucket[rp], &st->nr[rp][0], a.eb, to_bucket, v, heavy);
 }
 
 template <typename V, typename E, typename W>
-__global__ void k_weight_stats(E const* off, W const* w, int64_t nv, size_t ne, double* out)
+__device__ __forceinline__ void route_flush(sssp_args<V, E, W> const& a, split_stages<V>& sg, int Q)
+{
+  sssp_state<W>* st = a.st;
+  int const rp      = st->rp;
+  sg.nst.flush(a.near[Q], &st->nq[Q][0], a.eb);
+  sg.bst.flush(a.bucket[rp], &st->nr[rp][0], a.eb);
+}
+
+// One relax round over a list's edge space, chunk by chunk: the near list's light
+// edges (kLight) or the bucket list's heavy edges (kHeavy).  Block 0 clears the
+// next near counter.
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_relax(sssp_args<V, E, W> a, int round)
+{
+  using B           = typename bits_of<W>::type;
+  sssp_state<W>* st = a.st;
+  if (st->done) return;
+  int const P = round & 1, Q = P ^ 1;
+  int const tid   = threadIdx.x;
+  bool const hvy  = st->phase == kHeavy;
+  int const hl    = st->hl;
+  if (blockIdx.x == 0 && tid == 0) st->nq[Q][0] = 0;
+  flist<V> const L            = hvy ? a.bucket[hl] : a.near[P];
+  unsigned long long const c0 = hvy ? st->nr[hl][0] : st->nq[P][0];
+  int64_t const n   = (int64_t)(c0 >> a.eb);
+  int64_t const tot = (int64_t)(c0 & ((1ull << a.eb) - 1ull));
+  int64_t const nch = (tot + kChunk - 1) / kChunk;
+  __shared__ int64_t s_ob[kChunk + 1];  // per slot of the chunk: first edge of the row's part - its edge start
+  __shared__ W s_du[kChunk + 1];        // per slot: dist[u]
+  __shared__ int s_slot[kChunk];        // per position: the slot (a max-scan of the slot starts)
+  __shared__ int s_wmax[4];
+  unsigned long long my_e = 0, my_a = 0;
+  for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    int64_t const t0 = c * kChunk;
+    int64_t const t1 = t0 + kChunk < tot ? t0 + kChunk : tot;
+    int64_t const s0 = L.cs[c];
+    int64_t const s1 = c + 1 < nch ? L.cs[c + 1] : n - 1;
+    int const ns     = (int)(s1 - s0 + 1);  // <= kChunk + 1: every slot holds at least one edge
+    for (int p = tid; p < kChunk; p += 256) s_slot[p] = 0;
+    __syncthreads();
+    for (int i = tid; i < ns; i += 256) {
+      V const u        = L.q[s0 + i];
+      int64_t const e0 = L.ep[s0 + i];
+      int64_t const rb = (int64_t)a.off[u] + (hvy ? (int64_t)a.nlight[u] : 0);
+      s_ob[i]          = rb - e0;
+      s_du[i]          = a.dist[u];
+      int64_t const p  = e0 - t0;
+      if (i > 0 && p < kChunk) s_slot[p] = i;  // (slot 0 starts at or before t0)
+    }
+    __syncthreads();
+    {  // inclusive max-scan: thread tid owns positions [8 tid, 8 tid + 8)
+      int m = 0, loc[kPerThread];
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        int const x = s_slot[tid * kPerThread + k];
+        m           = x > m ? x : m;
+        loc[k]      = m;
+      }
+      int pre = m;  // inclusive wave max-scan of the thread maxima
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int const y = __shfl_up(pre, o, 64);
+        if ((tid & 63) >= o) pre = y > pre ? y : pre;
+      }
+      if ((tid & 63) == 63) s_wmax[tid >> 6] = pre;
+      int excl = __shfl_up(pre, 1, 64);
+      if ((tid & 63) == 0) excl = 0;
+      __syncthreads();
+      for (int w = 0; w < (tid >> 6); ++w) excl = s_wmax[w] > excl ? s_wmax[w] : excl;
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) s_slot[tid * kPerThread + k] = loc[k] > excl ? loc[k] : excl;
+    }
+    __syncthreads();
+    // 8 edges a thread, position k * 256 + tid: coalesced loads of each row
+    V v[kPerThread];
+    W nd[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      int const p     = k * 256 + tid;
+      int64_t const t = t0 + p;
+      v[k]            = V(-1);
+      nd[k]           = W(0);
+      if (t < t1) {
+        int const j     = s_slot[p];
+        int64_t const e = s_ob[j] + t;
+        v[k]            = a.idx[e];
+        nd[k]           = s_du[j] + a.wgt[e];
+      }
+    }
+    W dv[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) dv[k] = v[k] >= 0 ? a.dist[v[k]] : W(0);
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      if (v[k] >= 0 && nd[k] < a.cutoff && nd[k] < dv[k]) {
+        atomicMin(reinterpret_cast<B*>(a.dist + v[k]), *reinterpret_cast<B const*>(&nd[k]));
+        atomicOr(a.cbits + (v[k] >> 5), 1u << (uint32_t(v[k]) & 31u));
+        ++my_a;
+      }
+    }
+    if (tid == 0) my_e += (unsigned long long)(t1 - t0);
+    __syncthreads();
+  }
+  if (a.trace) {
+    for (int o = 32; o > 0; o >>= 1) {
+      my_e += __shfl_xor(my_e, o, 64);
+      my_a += __shfl_xor(my_a, o, 64);
+    }
+    int const p = (int)((blockIdx.x * 4 + (tid >> 6)) & 15);
+    if ((tid & 63) == 0 && my_e) atomicAdd(&st->work[p][hvy ? 3 : 0], my_e);
+    if ((tid & 63) == 0 && my_a) atomicAdd(&st->work[p][2], my_a);
+  }
+}
+
+// The round's changed bitmap (cleared as it is read) through route().
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_split(sssp_args<V, E, W> a, int round)
+{
+  sssp_state<W>* st = a.st;
+  if (st->done) return;
+  int const Q = (round & 1) ^ 1;
+  W const thr = st->thr;
+  CGX_SPLIT_LDS(V);
+  int64_t const nwords        = (a.nv + 31) >> 5;
+  unsigned long long improved = 0;
+  W fmin                      = std::numeric_limits<W>::max();
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nwords; base += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const wi = base + threadIdx.x;
+    uint32_t word    = wi < nwords ? a.cbits[wi] : 0u;
+    if (word) a.cbits[wi] = 0u;
+    improved += (unsigned long long)__popc(word);
+    while (__any(word != 0)) {
+      bool const have = word != 0;
+      V v             = 0;
+      if (have) {
+        v = (V)(wi * 32 + (__ffs(word) - 1));
+        word &= word - 1;
+      }
+      uint32_t light = 0, heavy = 0;
+      W d = W(0);
+      if (have) {
+        light = (uint32_t)a.nlight[v];
+        heavy = (uint32_t)(a.off[v + 1] - a.off[v]) - light;
+        d     = a.dist[v];
+      }
+      route(a, sg, Q, have, v, d, thr, light, heavy, fmin);
+    }
+  }
+  route_flush(a, sg, Q);
+  block_min_far(st, fmin);
+  if (a.trace) {
+    for (int o = 32; o > 0; o >>= 1) improved += __shfl_xor(improved, o, 64);
+    if ((threadIdx.x & 63) == 0 && improved) atomicAdd(&st->work[(blockIdx.x * 4 + wv_) & 15][1], improved);
+  }
+}
+
+// One thread, after the split: what the next round does.
+//  * the next near list is not empty -> a light round;
+//  * else, after light rounds, a bucket list with heavy edges -> a heavy round (the
+//    list is swapped out: vertices that join later start the next epoch's list);
+//  * else the bucket is done: with a far set (a distance noted at or past thr), a far
+//    split over the distances with the threshold past the smallest far distance
+//    (split_bucket, :235-262; the reference raises it by delta until the near bucket
+//    fills).
+template <typename W>
+__global__ void k_sssp_ctl(sssp_state<W>* st, int round, int eb)
+{
+  if (st->done) return;
+  using U     = typename bits_of<W>::utype;
+  U const inf = ~U(0) >> 1;  // above every non-negative value's bits
+  int const P = round & 1, Q = P ^ 1;
+  unsigned long long const did = st->phase == kHeavy ? st->nr[st->hl][0] : st->nq[P][0];
+  st->rounds += (did >> eb) > 0;
+  st->fs = 0;
+  if ((st->nq[Q][0] >> eb) > 0) {
+    st->phase = kLight;
+  } else if (st->phase == kLight && (st->nr[st->rp][0] >> eb) > 0) {
+    st->phase = kHeavy;
+    st->hl    = st->rp;
+    st->rp ^= 1;
+    st->nr[st->rp][0] = 0;
+    st->epoch += 1;
+  } else {
+    st->phase = kLight;
+    if (st->minfar != inf) {
+      U const mb  = st->minfar;
+      W const mf  = *reinterpret_cast<W const*>(&mb);
+      W const old = st->thr;
+      W thr       = old + st->delta;
+      if (!(mf < thr)) thr = mf + st->delta;
+      st->old    = old;
+      st->thr    = thr;
+      st->fs     = 1;
+      st->minfar = inf;  // k_far_split notes the far set's exact minimum past the new thr
+      st->epoch += 1;
+    }
+  }
+}
+
+// The far split, dense: every vertex with old <= dist < thr (unprocessed: the
+// buckets below old are done) through route(); the smallest distance at or past thr
+// (the rest of the far set) noted exactly.  One pass over the distances in id order
+// (coalesced) instead of a pile of ids in arbitrary order.
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_far_split(sssp_args<V, E, W> a, int round)
+{
+  sssp_state<W>* st = a.st;
+  if (st->done || !st->fs) return;
+  int const Q = (round & 1) ^ 1;
+  W const lo = st->old, thr = st->thr;
+  W const BIG = std::numeric_limits<W>::max();
+  CGX_SPLIT_LDS(V);
+  W fmin = BIG;
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < a.nv; base += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const i = base + threadIdx.x;
+    W const d       = i < a.nv ? a.dist[i] : BIG;
+    bool const cand = d >= lo && d < thr;
+    uint32_t light = 0, heavy = 0;
+    if (cand) {
+      light = (uint32_t)a.nlight[i];
+      heavy = (uint32_t)(a.off[i + 1] - a.off[i]) - light;
+    }
+    route(a, sg, Q, cand, (V)i, d, thr, light, heavy, fmin);
+    if (!cand && d >= thr && d < BIG && (a.off[i + 1] > a.off[i])) fmin = d < fmin ? d : fmin;
+  }
+  route_flush(a, sg, Q);
+  block_min_far(st, fmin);
+}
+
+// One thread: termination (no near list, no bucket list waiting for its heavy
+// round, no far set).
+template <typename W>
+__global__ void k_sssp_fin(sssp_state<W>* st, int round, int eb)
+{
+  if (st->done) return;
+  using U     = typename bits_of<W>::utype;
+  int const Q = (round & 1) ^ 1;
+  if (st->phase == kLight && (st->nq[Q][0] >> eb) == 0 && (st->nr[st->rp][0] >> eb) == 0 &&
+      st->minfar == (~U(0) >> 1))
+    st->done = 1;
+}
+
+// One wave: the source (an internal id, -1 when the external id is not a vertex)
+// through route() as the only vertex of the first split (parity 0); distance 0.
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(64) void k_sssp_init(sssp_args<V, E, W> a, V const* src, W delta)
+{
+  sssp_state<W>* st = a.st;
+  V const s_        = *src;
+  if (threadIdx.x == 0) {
+    st->delta  = delta;
+    st->thr    = delta;
+    st->minfar = ~typename bits_of<W>::utype(0) >> 1;
+    st->epoch  = 1;
+  }
+  if (s_ < 0 || (int64_t)s_ >= a.nv) {
+    if (threadIdx.x == 0) {
+      st->bad  = 1;
+      st->done = 1;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) a.dist[s_] = W(0);
+  __shared__ V s_v[1][kStage], s_b[1][kStage];
+  __shared__ uint32_t s_dn[1][kStage], s_db[1][kStage];
+  split_stages<V> sg{{s_v[0], s_dn[0], 0}, {s_b[0], s_db[0], 0}};
+  uint32_t const light = (uint32_t)a.nlight[s_];
+  uint32_t const heavy = (uint32_t)(a.off[s_ + 1] - a.off[s_]) - light;
+  W fmin               = std::numeric_limits<W>::max();
+  route(a, sg, 0, threadIdx.x == 0, s_, W(0), delta, light, heavy, fmin);
+  route_flush(a, sg, 0);
+  __syncthreads();
+  // a source with light edges starts with a light round; with heavy edges only, its
+  // bucket list goes first; without edges there is nothing to do
+  if (threadIdx.x == 0 && (st->nq[0][0] >> a.eb) == 0) {
+    if ((st->nr[st->rp][0] >> a.eb) > 0) {
+      st->phase = kHeavy;
+      st->hl    = st->rp;
+      st->rp ^= 1;
+      st->epoch += 1;
+    } else {
+      st->done = 1;
+    }
+  }
+}
+
+// The adjacency with each row's light edges (w < delta) first, then its heavy ones
+// (each part in the row's order), and the light count per row: a wave per row,
+// ballot compaction, two passes.
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_partition_rows(E const* off, V const* idx, W const* wgt, int64_t nv, W delta,
+                                                         V* pidx, W* pw, int* nlight)
+{
+  int const lane = lane_id();
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < nv;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    E const beg = off[r], end = off[r + 1];
+    E out       = beg;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (E base = beg; base < end; base += 64) {
+        E const e     = base + lane;
+        bool const in = e < end;
+        V v           = 0;
+        W w           = W(0);
+        if (in) {
+          v = idx[e];
+          w = wgt[e];
+        }
+        bool const take            = in && ((w < delta) == (pass == 0));
+        unsigned long long const m = __ballot(take);
+        if (take) {
+          E const o = out + (E)__popcll(m & ((1ull << lane) - 1ull));
+          pidx[o]   = v;
+          pw[o]     = w;
+        }
+        out += (E)__popcll(m);
+      }
+      if (pass == 0 && lane == 0) nlight[r] = (int)(out - beg);
+    }
+  }
+}
+
+// Predecessors by a pull over the in-edges (sorted ascending): a 16-lane group per
+// vertex walks its in-neighbours 16 at a time and stops at the first u with
+// dist[u] + w == dist[v] -- the smallest tight in-neighbour.  -1 for the source and
+// unreached vertices.
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_sssp_pred(E const* off, V const* idx, W const* wgt, W const* dist, int64_t nv,
+                                                   V const* src, V* pred)
+{
+  int const lane = threadIdx.x & 15;
+  int const gsh  = threadIdx.x & 48;  // the group's first lane within the wave
+  V const s_     = *src;
+  W const BIG    = std::numeric_limits<W>::max();
+  for (int64_t v0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; v0 < nv;
+       v0 += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+    V const v  = (V)v0;
+    W const dv = dist[v];
+    V found    = V(-1);
+    if (v != s_ && dv != BIG) {
+      E const beg = off[v], end = off[v + 1];
+      for (E base = beg; base < end; base += 16) {
+        E const e  = base + lane;
+        bool tight = false;
+        V u        = 0;
+        if (e < end) {
+          u     = idx[e];
+          tight = (W)(dist[u] + wgt[e]) == dv;
+        }
+        unsigned long long const m = (__ballot(tight) >> gsh) & 0xffffull;
+        if (m) {
+          found = __shfl(u, gsh + __ffsll((long long)m) - 1, 64);
+          break;
+        }
+      }
+    }
+    if (lane == 0) pred[v] = found;
+  }
+}
+
+template <typename W>
+__global__ void k_weight_stats(W const* w, size_t ne, double* out)
 {
   __shared__ double sm[4];
   double acc = 0;
@@ -225,6 +628,12 @@ __global__ void k_count_neg(W const* w, size_t n, int* bad)
     if (w[i] < W(0)) atomicAdd(bad, 1);
 }
 
+template <typename V>
+flist<V> make_list(dbuf<V>& q, dbuf<int64_t>& ep, dbuf<int64_t>& cs)
+{
+  return flist<V>{q.data(), ep.data(), cs.data()};
+}
+
 template <typename V, typename E, typename W>
 void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_pred, bool expensive,
                paths_result_t& res)
@@ -234,19 +643,13 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   CGX_INPUT(g.weighted,
             "Invalid input argument: an unweighted graph is passed to SSSP, BFS is more efficient for unweighted "
             "graphs.");
-  // the source is an external id (c_api/sssp.cpp renumbers it)
-  dbuf<V> src_id(1, s);
+  // the source is an external id (c_api/sssp.cpp renumbers it): looked up on the
+  // device, checked by k_sssp_init, reported with the first chunk's state read
   V hs = (V)source;
   CGX_INPUT((int64_t)source >= 0 && (size_t)(V)source == source, "Invalid input argument: source vertex out-of-range.");
+  dbuf<V> src_id(1, s);
   to_device(src_id.data(), &hs, 1, s);
-  {
-    try {
-      renumber_ext_to_int(h, g, src_id.data(), 1, true);
-    } catch (cgx::error const&) {
-      fail(CUGRAPH_INVALID_INPUT, "Invalid input argument: source vertex out-of-range.");
-    }
-  }
-  V src = to_host_scalar(src_id.data(), s);
+  renumber_ext_to_int_unchecked(h, g, src_id.data(), 1);
   res.vertices     = number_map_copy(h, g);
   res.distances    = std::make_unique<device_array_t>((size_t)nv, dtype_of<W>(), s);
   res.predecessors = std::make_unique<device_array_t>(want_pred ? (size_t)nv : 0, dtype_of<V>(), s);
@@ -254,8 +657,6 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   W const BIG      = std::numeric_limits<W>::max();
   fill<W>(dist, nv, BIG, s);
   if (nv == 0) return;
-  W zero = 0;
-  to_device(dist + src, &zero, 1, s);
 
   adjacency_t& adj = ensure_adjacency(h, g, false);
   size_t ne        = (size_t)g.num_edges;
@@ -271,121 +672,108 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
               "Invalid input argument: input graph should have non-negative edge weights.");
   }
   W cut = (cutoff >= (double)BIG || !(cutoff == cutoff)) ? BIG : (W)cutoff;
+  // list counters: (slots << eb) | edges in one 64-bit word
+  int const eb = bits_for((unsigned long long)std::max<size_t>(ne, 1));
+  CGX_EXPECTS(bits_for((unsigned long long)nv) + eb <= 64, CUGRAPH_NOT_IMPLEMENTED,
+              "SSSP: vertex and edge counts exceed the 64-bit frontier counter");
 
-  if (ne) {
-    // delta = 64 * average edge weight / average degree (wave-64 analogue of :143-157)
+  // delta = kDeltaScale * average edge weight / average degree (the reference:
+  // warp_size = 32 times the same, :143-157); the weight sum is cached on the
+  // adjacency (one read of the weights per graph, not per call)
+  if (adj.wsum < 0 && ne) {
     dbuf<double> wsum(1, s);
     fill<double>(wsum.data(), 1, 0.0, s);
-    hipLaunchKernelGGL((k_weight_stats<V, E, W>), dim3(grid_for(ne, kBlock, 1024)), dim3(kBlock), 0, s, off, wgt, nv,
-                       ne, wsum.data());
+    hipLaunchKernelGGL(k_weight_stats<W>, dim3(grid_for(ne, kBlock, 1024)), dim3(kBlock), 0, s, wgt, ne, wsum.data());
     CGX_LAUNCH_CHECK();
-    double avg_w   = to_host_scalar(wsum.data(), s) / (double)ne;
-    double avg_deg = (double)ne / (double)nv;
-    W delta        = (W)std::max(64.0 * avg_w / avg_deg, 1e-30);
+    adj.wsum = to_host_scalar(wsum.data(), s);
+  }
+  double const avg_w   = ne ? std::max(adj.wsum, 0.0) / (double)ne : 0.0;
+  double const avg_deg = (double)ne / (double)nv;
+  double const dscale  = h.tune.sssp_delta > 0 ? h.tune.sssp_delta : kDeltaScale;
+  W const delta        = (W)std::max(avg_deg > 0 ? dscale * avg_w / avg_deg : 1.0, 1e-30);
+  // the light-first adjacency for this delta (cached on the adjacency)
+  if (adj.sssp_delta != (double)delta) {
+    adj.sssp_idx.set_stream(s);
+    adj.sssp_w.set_stream(s);
+    adj.sssp_nlight.set_stream(s);
+    adj.sssp_idx.resize(std::max<size_t>(ne, 1) * sizeof(V));
+    adj.sssp_w.resize(std::max<size_t>(ne, 1) * sizeof(W));
+    adj.sssp_nlight.resize((size_t)nv * sizeof(int));
+    hipLaunchKernelGGL((k_partition_rows<V, E, W>), dim3(grid_for((size_t)nv * 64, 256, 16384)), dim3(256), 0, s, off,
+                       idx, wgt, nv, delta, adj.sssp_idx.data<V>(), adj.sssp_w.data<W>(), adj.sssp_nlight.data<int>());
+    CGX_LAUNCH_CHECK();
+    adj.sssp_delta = (double)delta;
+  }
 
-    dbuf<int> stamp(nv, s);
-    fill<int>(stamp.data(), nv, -1, s);
-    dbuf<V> qa[3], qb[3];
-    for (int c = 0; c < 3; ++c) {
-      qa[c].resize(nv, s);
-      qb[c].resize(nv, s);
+  int64_t const nchunk_max = (int64_t)(ne + kChunk - 1) / kChunk + 1;
+  dbuf<int> stamp(nv, s);
+  fill<int>(stamp.data(), nv, 0, s);
+  dbuf<uint32_t> cbits((nv + 31) / 32, s);
+  HIP_CHECK(hipMemsetAsync(cbits.data(), 0, ((nv + 31) / 32) * sizeof(uint32_t), s));
+  dbuf<V> q[4] = {dbuf<V>(nv, s), dbuf<V>(nv, s), dbuf<V>(nv, s), dbuf<V>(nv, s)};
+  dbuf<int64_t> ep[4] = {dbuf<int64_t>(nv, s), dbuf<int64_t>(nv, s), dbuf<int64_t>(nv, s), dbuf<int64_t>(nv, s)};
+  dbuf<int64_t> cs[4] = {dbuf<int64_t>(nchunk_max, s), dbuf<int64_t>(nchunk_max, s), dbuf<int64_t>(nchunk_max, s),
+                         dbuf<int64_t>(nchunk_max, s)};
+  dbuf<sssp_state<W>> st(1, s);
+  HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(sssp_state<W>), s));
+  sssp_args<V, E, W> a{};
+  a.off    = off;
+  a.idx    = adj.sssp_idx.data<V>();
+  a.wgt    = adj.sssp_w.data<W>();
+  a.nlight = adj.sssp_nlight.data<int>();
+  a.dist   = dist;
+  a.stamp  = stamp.data();
+  a.cutoff = cut;
+  for (int i = 0; i < 2; ++i) {
+    a.near[i]   = make_list(q[i], ep[i], cs[i]);
+    a.bucket[i] = make_list(q[2 + i], ep[2 + i], cs[2 + i]);
+  }
+  a.cbits  = cbits.data();
+  a.st     = st.data();
+  a.nv     = nv;
+  a.eb     = eb;
+  static bool const trace = std::getenv("CGX_SSSP_TRACE") != nullptr;
+  a.trace                 = trace ? 1 : 0;
+  hipLaunchKernelGGL((k_sssp_init<V, E, W>), dim3(1), dim3(64), 0, s, a, src_id.data(), delta);
+  CGX_LAUNCH_CHECK();
+  auto* hs_st = h.pinned_as<sssp_state<W>>();
+  int round   = 0;
+  while (true) {
+    for (int k = 0; k < kChunkRounds; ++k, ++round) {
+      hipLaunchKernelGGL((k_relax<V, E, W>), dim3(kRelaxGrid), dim3(256), 0, s, a, round);
+      hipLaunchKernelGGL((k_split<V, E, W>), dim3(kSplitGrid), dim3(256), 0, s, a, round);
+      hipLaunchKernelGGL(k_sssp_ctl<W>, dim3(1), dim3(1), 0, s, a.st, round, eb);
+      hipLaunchKernelGGL((k_far_split<V, E, W>), dim3(kSplitGrid), dim3(256), 0, s, a, round);
+      hipLaunchKernelGGL(k_sssp_fin<W>, dim3(1), dim3(1), 0, s, a.st, round, eb);
+      CGX_LAUNCH_CHECK();
     }
-    dbuf<V> changed(nv, s), farA(nv, s), farB(nv, s);
-    dbuf<int> infar(nv, s);
-    fill<int>(infar.data(), nv, 0, s);
-    dbuf<sssp_ctr> ctr(1, s);
-    sssp_ctr* hc = nullptr;
-    hc = h.pinned_as<sssp_ctr>();
-    try {
-      auto read_ctr = [&]() {
-        HIP_CHECK(hipMemcpyAsync(hc, ctr.data(), sizeof(sssp_ctr), hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-      };
-      // initial near frontier: the source
-      auto o2 = to_host(off + src, 2, s);
-      E deg0  = o2[1] - o2[0];
-      int c0 = deg0 <= kSmallDeg ? 0 : (deg0 <= kMidDeg ? 1 : 2);
-      to_device(qa[c0].data(), &src, 1, s);
-      unsigned long long ncur[3] = {0, 0, 0};
-      ncur[c0]                   = 1;
-      unsigned long long nfar    = 0;
-      W thr                      = delta;
-      int round                  = 0;
-      sssp_args<V, E, W> a{};
-      a.off    = off;
-      a.idx    = idx;
-      a.wgt    = wgt;
-      a.dist   = dist;
-      a.stamp  = stamp.data();
-      a.cutoff = cut;
-      a.changed = changed.data();
-      a.ctr    = ctr.data();
-      size_t rounds = 0;
-      while (true) {
-        unsigned long long nn = ncur[0] + ncur[1] + ncur[2];
-        if (nn > 0) {
-          HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(sssp_ctr), s));
-          a.round = round++;
-          for (int c = 0; c < 3; ++c) {
-            a.q[c] = qa[c].data();
-            a.n[c] = ncur[c];
-          }
-          long long nb_large = (long long)std::min<unsigned long long>(ncur[2], 1024);
-          long long nb_mid   = (long long)std::min<unsigned long long>((ncur[1] + 3) / 4, 4096);
-          long long nb_small = (long long)std::min<unsigned long long>((ncur[0] + 63) / 64, 8192);
-          a.blk_mid_start    = nb_large;
-          a.blk_small_start  = nb_large + nb_mid;
-          hipLaunchKernelGGL((k_relax<V, E, W>), dim3(nb_large + nb_mid + nb_small), dim3(kBlock), 0, s, a);
-          CGX_LAUNCH_CHECK();
-          read_ctr();
-          unsigned long long nch = hc->changed;
-          // split the changed vertices: near (< thr) -> next frontier, else -> far pile
-          HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(sssp_ctr), s));
-          if (nch)
-            hipLaunchKernelGGL((k_split<V, E, W>), dim3(grid_for(nch, kBlock, 4096)), dim3(kBlock), 0, s,
-                               changed.data(), nch, dist, off, W(0), thr, infar.data(), false, qb[0].data(),
-                               qb[1].data(), qb[2].data(), farA.data() + nfar, ctr.data());
-          CGX_LAUNCH_CHECK();
-          read_ctr();
-          for (int c = 0; c < 3; ++c) ncur[c] = hc->near[c];
-          nfar += hc->far;
-          for (int c = 0; c < 3; ++c) std::swap(qa[c], qb[c]);
-          ++rounds;
-          continue;
-        }
-        if (nfar == 0) break;
-        // near pile empty: advance the threshold and split the far pile (split_bucket, :235-262)
-        while (true) {
-          W old = thr;
-          thr   = thr + delta;
-          HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(sssp_ctr), s));
-          hipLaunchKernelGGL((k_split<V, E, W>), dim3(grid_for(nfar, kBlock, 4096)), dim3(kBlock), 0, s,
-                             farA.data(), nfar, dist, off, old, thr, infar.data(), true, qa[0].data(), qa[1].data(),
-                             qa[2].data(), farB.data(), ctr.data());
-          CGX_LAUNCH_CHECK();
-          read_ctr();
-          for (int c = 0; c < 3; ++c) ncur[c] = hc->near[c];
-          nfar = hc->far;
-          std::swap(farA, farB);
-          if (ncur[0] + ncur[1] + ncur[2] > 0 || nfar == 0) break;
-        }
-        if (ncur[0] + ncur[1] + ncur[2] == 0 && nfar == 0) break;
-      }
-      h.last_iterations = rounds;
-    } catch (...) {
-      throw;
+    HIP_CHECK(hipMemcpyAsync(hs_st, st.data(), sizeof(sssp_state<W>), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    CGX_INPUT(!hs_st->bad, "Invalid input argument: source vertex out-of-range.");
+    if (hs_st->done) break;
+  }
+  h.last_iterations = (size_t)hs_st->rounds;
+  if (trace) {
+    unsigned long long light = 0, heavy = 0, impr = 0, atom = 0;
+    for (int p = 0; p < 16; ++p) {
+      light += hs_st->work[p][0];
+      impr += hs_st->work[p][1];
+      atom += hs_st->work[p][2];
+      heavy += hs_st->work[p][3];
     }
+    double const E1 = ne ? (double)ne : 1.0;
+    std::fprintf(stderr, "[sssp] V %lld E %zu delta %.6g: %llu rounds (%d enqueued), edges relaxed %.2f E (light %.2f, "
+                 "heavy %.2f), %llu distance atomics (%.3f per edge), %llu improved vertices (%.2f V)\n",
+                 (long long)nv, ne, (double)delta, hs_st->rounds, round, (double)(light + heavy) / E1,
+                 (double)light / E1, (double)heavy / E1, atom, (light + heavy) ? (double)atom / (double)(light + heavy) : 0.0,
+                 impr, (double)impr / (double)nv);
   }
   if (want_pred) {
     V* pred = res.predecessors->buf.data<V>();
-    V none  = std::numeric_limits<V>::max();
-    fill<V>(pred, nv, none, s);
-    if (ne) {
-      hipLaunchKernelGGL((k_sssp_pred<V, E, W>), dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, off, idx, wgt,
-                         dist, nv, src, pred);
-      CGX_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_pred_none<V>, dim3(grid_for(nv, kBlock, 8192)), dim3(kBlock), 0, s, pred, nv, none);
+    // in-edges: a symmetric graph's own rows, else the cached CSC
+    adjacency_t& in = g.symmetric ? adj : ensure_adjacency(h, g, true);
+    hipLaunchKernelGGL((k_sssp_pred<V, E, W>), dim3(grid_for((size_t)nv * 16, 256, 16384)), dim3(256), 0, s,
+                       in.offsets.data<E>(), in.indices.data<V>(), in.weights.data<W>(), dist, nv, src_id.data(), pred);
     CGX_LAUNCH_CHECK();
     unrenumber_int_to_ext(h, g, pred, (size_t)nv);
   }

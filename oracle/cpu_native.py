@@ -1,5 +1,5 @@
 """ctypes loader for the compiled CPU restatements (oracle/cpu_baseline.c,
-oracle/cpu_louvain.c).
+oracle/cpu_louvain.c, oracle/cpu_sssp.c).
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): bench.py's cpu_baseline leg
 times it as the secondary CPU baseline of SURVEY.md §8d.  Built by
@@ -30,6 +30,10 @@ def lib():
                                           ctypes.c_int, P]
         _lib.cpu_bfs.restype = ctypes.c_double
         _lib.cpu_bfs.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int, P, P]
+        for f in (_lib.cpu_sssp_f32, _lib.cpu_sssp_f64):
+            f.restype = ctypes.c_int
+            f.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, P, P,
+                          ctypes.POINTER(ctypes.c_double)]
         _lib.cpu_louvain.restype = ctypes.c_int
         _lib.cpu_louvain.argtypes = [ctypes.c_int64, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_int, P, P, P]
     return _lib
@@ -96,3 +100,23 @@ def louvain(offsets, indices, weights, max_level=100, resolution=1.0, threads=0)
     if rc == -2:
         raise MemoryError("cpu_louvain allocation failed")
     return c[:nv], q.value, lv.value
+
+
+def sssp(offsets, indices, weights, source, cutoff=float("inf")):
+    """Near-far SSSP (oracle/cpu_sssp.c: sssp_impl.cuh:79-270 restated, one thread)
+    on a CSR in internal ids; weights float32 or float64 pick the weight type.
+    Returns (seconds, distances, predecessors int32 (-1: none), rounds)."""
+    off = np.ascontiguousarray(offsets, dtype=np.int64)
+    idx = np.ascontiguousarray(indices, dtype=np.int32)
+    w = np.ascontiguousarray(weights)
+    if w.dtype not in (np.float32, np.float64):
+        w = w.astype(np.float32)
+    nv = off.size - 1
+    dist = np.empty(nv, dtype=w.dtype)
+    pred = np.empty(nv, dtype=np.int32)
+    t = ctypes.c_double(0.0)
+    f = lib().cpu_sssp_f32 if w.dtype == np.float32 else lib().cpu_sssp_f64
+    rounds = f(_p(off), _p(idx), _p(w), nv, int(source), float(cutoff), _p(dist), _p(pred), ctypes.byref(t))
+    if rounds == -2:
+        raise MemoryError("cpu_sssp allocation failed")
+    return t.value, dist, pred, rounds

@@ -1,7 +1,8 @@
 """The compiled CPU restatements (oracle/cpu_baseline.c, bench.py's secondary CPU
-baseline, and oracle/cpu_louvain.c) agree with the numpy oracle: PageRank iterates
-converge to the oracle's ranks, BFS distances are exact, single-threaded and with
-OpenMP, and Louvain gives the oracle's clustering, modularity and levels."""
+baseline, oracle/cpu_louvain.c and oracle/cpu_sssp.c) agree with the numpy oracle:
+PageRank iterates converge to the oracle's ranks, BFS distances are exact,
+single-threaded and with OpenMP, Louvain gives the oracle's clustering, modularity
+and levels, and near-far SSSP the oracle's distances and predecessors bit for bit."""
 import numpy as np
 import pytest
 
@@ -86,3 +87,28 @@ def test_louvain_matches_oracle(case, threads):
         assert abs(q - oq) <= 1e-12 * abs(oq)
     else:
         assert np.array_equal(c, oc) and q == oq and levels == olevels
+
+
+@pytest.mark.parametrize("scale,symmetric,wdtype,cutoff", [(11, True, np.float32, np.inf), (12, False, np.float32, np.inf),
+                                                          (11, True, np.float64, np.inf), (11, True, np.float32, 0.05)])
+def test_sssp_matches_oracle(scale, symmetric, wdtype, cutoff):
+    from oracle import sssp as osssp
+    s, d = rmat.rmat(scale, 16 << scale, seed=42)
+    w = rmat.rmat_weights(s.size, seed=43).astype(np.float64)
+    s, d, w = og.symmetrize_dedup(s, d, w, symmetrize=symmetric)
+    g = og.create_graph(s, d, w.astype(wdtype), renumber=True)
+    for src in (0, g.num_vertices // 3):
+        rd, rp = osssp.sssp(g.num_vertices, g.offsets, g.indices, g.weights, src, cutoff=cutoff, dtype=wdtype)
+        _, dist, pred, rounds = cpu.sssp(g.offsets, g.indices, g.weights.astype(wdtype), src, cutoff)
+        assert dist.dtype == wdtype and rounds > 0
+        assert np.array_equal(dist, rd)
+        assert np.array_equal(pred.astype(np.int64), rp)
+
+
+def test_sssp_c_golden(golden):
+    """cpp/tests/c_api/sssp_test.c:178-230 through the compiled restatement."""
+    g = golden["sssp_c"]
+    G = og.create_graph(g["src"], g["dst"], np.asarray(g["w"], np.float32), renumber=False)
+    _, dist, pred, _ = cpu.sssp(G.offsets, G.indices, G.weights.astype(np.float32), g["source"], g["cutoff"])
+    assert np.allclose(dist, np.asarray(g["expected_distances"], np.float32), rtol=1e-6)
+    assert pred.tolist() == g["expected_predecessors"]

@@ -95,3 +95,46 @@ def test_bad_source():
     h, G = make_graph([0, 1], [1, 2], [1.0, 1.0], renumber=False)
     with pytest.raises(ValueError):
         run(h, G, 9)
+
+
+@pytest.mark.parametrize("scale,wdtype", [(20, np.float32), (18, np.float64)])
+def test_rmat_uniform_weights_vs_compiled_oracle(scale, wdtype):
+    """The reference's SSSP test size (RMAT(20, ...), sssp_test.cpp:305), symmetric
+    with the bench's uniform [0, 1) weights (cugraph_funcs.py:56-58), from 4 sources
+    (the largest hub, two random vertices, a low-degree vertex): distances bit-exact
+    against the compiled near-far restatement (oracle/cpu_sssp.c) on the library's own
+    CSR, and every predecessor the smallest tight in-neighbour."""
+    import torch
+    from oracle import cpu_native
+    p = plc()
+    h = p.ResourceHandle()
+    n = 16 << scale
+    s, d = p.generators.generate_rmat_edgelist(h, scale, n, 0.57, 0.19, 0.19, 42, False, True)
+    w = p.generators.generate_edge_weights(h, n, 43)
+    if wdtype == np.float64:
+        w = w.to(torch.float64)
+    s, d, w = p.generators.symmetrize_dedup(h, s, d, w, True)
+    G = p.SGGraph(h, p.GraphProperties(is_symmetric=True, is_multigraph=False), s, d, w, store_transposed=False,
+                  renumber=True)
+    off, idx, ww = G.adjacency(h, transposed=False)
+    off, idx, ww = host(off).astype(np.int64), host(idx), host(ww)
+    assert ww.dtype == wdtype
+    V = off.size - 1
+    rng = np.random.default_rng(5)
+    nm = None
+    for k in range(4):
+        if nm is None:  # the first call (from an edge's source) also gives the number map
+            ext = int(s[0])
+        else:
+            ext = int(nm[[0, int(rng.integers(V)), V - 1][k - 1]])  # the largest hub, a random, the last vertex
+        v, dist, pred = run(h, G, ext)
+        nm = v if nm is None else nm
+        assert np.array_equal(v, nm)
+        src_int = int(np.nonzero(nm == ext)[0][0])
+        t, rd, rp, rounds = cpu_native.sssp(off, idx, ww, src_int)
+        assert np.array_equal(dist, rd), f"source {src_int}: distances differ from the compiled oracle"
+        want = np.where(rp >= 0, nm[np.maximum(rp, 0)], -1)
+        assert np.array_equal(pred.astype(np.int64), want.astype(np.int64)), f"source {src_int}: predecessors"
+        reached = int((rd < np.finfo(wdtype).max).sum())
+        print(f"RMAT-{scale} {np.dtype(wdtype).name} SSSP from internal {src_int}: reached {reached} of {V}, "
+              f"GPU rounds {h.last_iterations()}, oracle rounds {rounds} ({t:.2f} s)")
