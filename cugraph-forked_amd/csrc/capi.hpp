@@ -58,6 +58,7 @@ struct tuning_t {
   int64_t louvain_big_maxdeg = 0;  // heavy rows above this degree on the sort path (0: the table limit)
   bool louvain_wide_keys = false;  // 64-bit hash keys below 2^24 ids (tests)
   double sssp_delta    = 0;     // SSSP delta = sssp_delta * average weight / average degree (0: sssp.hip kDeltaScale)
+  int sssp_pull        = 0;     // SSSP dense rounds by pull: 0 by size (sssp.hip kPullDiv), -1 never, n: list > part / n
 };
 
 struct handle_t {
@@ -218,9 +219,11 @@ struct adjacency_t {
   // items (freed with the graph; trim_device_cache returns only the allocator's free blocks)
   buffer bfs_head;
   double wsum = -1;  // SSSP: sum of the weights (delta), cached on first use; -1 = not known yet
-  // SSSP (sssp.hip): the adjacency with each row's light edges (w < delta) first, for one delta
+  // SSSP (sssp.hip): the light (w < delta) and heavy edges as two CSRs, with each part's
+  // chunk rows, for one delta
   double sssp_delta = -1;
-  buffer sssp_idx, sssp_w, sssp_nlight;
+  int64_t sssp_eL = 0, sssp_eH = 0;
+  buffer sssp_offL, sssp_offH, sssp_idxL, sssp_wL, sssp_idxH, sssp_wH, sssp_crowL, sssp_crowH;
   pr_push_t pr;  // PageRank windowed-push schedule (pagerank.hip), built on first use
 };
 

@@ -531,6 +531,7 @@ extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t
     else if (n == "pr_fast_build") b(t.pr_fast_build);
     else if (n == "pr_share_div") i32(t.pr_share_div);
     else if (n == "mg_chunks") i32(t.mg_chunks);
+    else if (n == "sssp_pull") i32(t.sssp_pull);
     else if (n == "sssp_delta") {
       CGX_INPUT(value >= 0, "Invalid input argument: sssp_delta must be >= 0");
       t.sssp_delta = value;

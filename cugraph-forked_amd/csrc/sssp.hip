@@ -31,14 +31,20 @@
 //  * k_split: the changed bitmap (V / 8 bytes, read and cleared whole): below thr ->
 //    the next near list and (once per bucket) the bucket list; otherwise the vertex
 //    is in the far set, whose smallest distance is kept;
-//  * k_sssp_ctl: the next round -- light while the near list fills, one heavy round
-//    when it empties, then a far split (split_bucket, :235-262) with the threshold
-//    raised past the smallest far distance (the reference raises it by delta until
-//    the near bucket fills: the same buckets, fewer empty passes);
+//  * k_pull: a dense list (its edges above a quarter of its part's) is relaxed as a
+//    pull over the part in order instead: rows above the round's floor take the
+//    smallest candidate from frontier sources (the list's bitmap), one atomic per
+//    row and chunk -- the part read coalesced, only the frontier's distances
+//    gathered (symmetric graphs);
+//  * k_sssp_ctl: the next round -- light while the near list
+//    fills, one heavy round when it empties, then a far split (split_bucket,
+//    :235-262) with the threshold raised past the smallest far distance (the
+//    reference raises it by delta until the near bucket fills: the same buckets,
+//    fewer empty passes);
 //  * k_far_split: a dense pass over the distances -- [old, thr) to the near list, the
 //    far set's minimum -- instead of a pile of ids (the reference's far bucket: each
 //    split re-reads every far entry in arbitrary order, 0.3-0.5 ms a split at
-//    RMAT-24); k_sssp_fin: the termination flag.
+//    RMAT-24); k_sssp_fin: the termination flag and push or pull.
 // The state lives in one device block; the host enqueues kChunkRounds rounds and
 // reads the state once per chunk (rounds after termination return at once).  Every
 // grid is fixed and grid-strides over device-side counts.  The light-first copy of
@@ -60,12 +66,15 @@ namespace {
 
 constexpr int kChunk       = 2048;  // edges per relax work item: 256 threads x 8
 constexpr int kPerThread   = kChunk / 256;
-constexpr int kRelaxGrid   = 1024;  // persistent relax blocks (LDS: 4 per CU)
+constexpr int kRelaxGrid   = 1280;  // persistent relax blocks (32 KB of LDS: 5 per CU)
+constexpr int kPullGrid    = 1024;  // persistent pull blocks (2048: 4.6 vs 4.2 ms of pulls per RMAT-24 traversal)
 constexpr int kSplitGrid   = 1024;
 constexpr int kStage       = 128;   // staged entries per wave and list
 constexpr int kChunkRounds = 8;     // rounds enqueued per host read
 // delta = kDeltaScale * average weight / average degree (tuning_t::sssp_delta)
 constexpr double kDeltaScale = 8.0;
+// a list whose edges exceed its part's / kPullDiv is relaxed by a pull (tuning_t::sssp_pull)
+constexpr int kPullDiv = 4;
 
 template <typename W>
 struct bits_of;
@@ -92,6 +101,7 @@ struct sssp_state {
   W thr, old, delta;
   int fs;     // this round splits the far set
   int phase;  // the next relax: kLight (near list nq[P]) or kHeavy (bucket list nr[hl])
+  int pull;   // the next relax is a pull over the part (dense list)
   int rp;     // bucket list receiving this bucket's vertices
   int hl;     // bucket list a heavy round relaxes
   int epoch;  // a vertex joins bucket list rp once per epoch (stamp)
@@ -111,12 +121,23 @@ struct flist {
   int64_t* cs;
 };
 
+// one part of the adjacency (the light or the heavy edges of every row) as a CSR,
+// with the row holding edge c * kChunk of the part (the pull's chunk starts)
+template <typename V, typename E, typename W>
+struct part_t {
+  E const* off;
+  V const* idx;
+  W const* w;
+  int64_t const* crow;
+  int64_t ne;
+};
+
 template <typename V, typename E, typename W>
 struct sssp_args {
-  E const* off;
-  V const* idx;       // adjacency with each row's light edges (w < delta) first, then its heavy ones
-  W const* wgt;
-  int const* nlight;  // light edges per row
+  E const* off;          // the graph's rows (degrees)
+  part_t<V, E, W> pt[2]; // kLight: edges with w < delta, kHeavy: the rest
+  uint32_t* fbits[4];    // frontier bitmaps of the lists: near by parity (0, 1), bucket by index (2, 3)
+  int pull_div;          // a list whose edges exceed its part's / pull_div is relaxed by a pull (0: never)
   W* dist;
   int* stamp;         // bucket-list epoch of each vertex
   W cutoff;
@@ -245,6 +266,10 @@ __device__ __forceinline__ void route(sssp_args<V, E, W> const& a, split_stages<
   if (near && heavy > 0) to_bucket = atomicExch(a.stamp + v, st->epoch) != st->epoch;
   if (live && !near) fmin = d < fmin ? d : fmin;
   int const rp = st->rp;
+  if (a.pull_div) {  // the lists' frontier bits (a pull reads them)
+    if (near && light > 0) atomicOr(a.fbits[Q] + (v >> 5), 1u << (uint32_t(v) & 31u));
+    if (to_bucket) atomicOr(a.fbits[2 + rp] + (v >> 5), 1u << (uint32_t(v) & 31u));
+  }
   sg.nst.push(a.near[Q], &st->nq[Q][0], a.eb, near && light > 0, v, light);
   sg.bst.push(a.bucket[rp], &st->nr[rp][0], a.eb, to_bucket, v, heavy);
 }
@@ -272,6 +297,8 @@ __global__ __launch_bounds__(256) void k_relax(sssp_args<V, E, W> a, int round)
   bool const hvy  = st->phase == kHeavy;
   int const hl    = st->hl;
   if (blockIdx.x == 0 && tid == 0) st->nq[Q][0] = 0;
+  if (st->pull) return;  // (k_pull relaxes this round)
+  part_t<V, E, W> const pt    = a.pt[hvy ? kHeavy : kLight];
   flist<V> const L            = hvy ? a.bucket[hl] : a.near[P];
   unsigned long long const c0 = hvy ? st->nr[hl][0] : st->nq[P][0];
   int64_t const n   = (int64_t)(c0 >> a.eb);
@@ -293,8 +320,7 @@ __global__ __launch_bounds__(256) void k_relax(sssp_args<V, E, W> a, int round)
     for (int i = tid; i < ns; i += 256) {
       V const u        = L.q[s0 + i];
       int64_t const e0 = L.ep[s0 + i];
-      int64_t const rb = (int64_t)a.off[u] + (hvy ? (int64_t)a.nlight[u] : 0);
-      s_ob[i]          = rb - e0;
+      s_ob[i]          = (int64_t)pt.off[u] - e0;
       s_du[i]          = a.dist[u];
       int64_t const p  = e0 - t0;
       if (i > 0 && p < kChunk) s_slot[p] = i;  // (slot 0 starts at or before t0)
@@ -335,8 +361,8 @@ __global__ __launch_bounds__(256) void k_relax(sssp_args<V, E, W> a, int round)
       if (t < t1) {
         int const j     = s_slot[p];
         int64_t const e = s_ob[j] + t;
-        v[k]            = a.idx[e];
-        nd[k]           = s_du[j] + a.wgt[e];
+        v[k]            = pt.idx[e];
+        nd[k]           = s_du[j] + pt.w[e];
       }
     }
     W dv[kPerThread];
@@ -370,8 +396,9 @@ __global__ __launch_bounds__(256) void k_split(sssp_args<V, E, W> a, int round)
 {
   sssp_state<W>* st = a.st;
   if (st->done) return;
-  int const Q = (round & 1) ^ 1;
+  int const P = round & 1, Q = P ^ 1;
   W const thr = st->thr;
+  uint32_t* const Fu = a.pull_div ? a.fbits[st->phase == kHeavy ? 2 + st->hl : P] : nullptr;
   CGX_SPLIT_LDS(V);
   int64_t const nwords        = (a.nv + 31) >> 5;
   unsigned long long improved = 0;
@@ -380,6 +407,7 @@ __global__ __launch_bounds__(256) void k_split(sssp_args<V, E, W> a, int round)
     int64_t const wi = base + threadIdx.x;
     uint32_t word    = wi < nwords ? a.cbits[wi] : 0u;
     if (word) a.cbits[wi] = 0u;
+    if (Fu && wi < nwords && Fu[wi]) Fu[wi] = 0u;  // the relaxed list's frontier bits
     improved += (unsigned long long)__popc(word);
     while (__any(word != 0)) {
       bool const have = word != 0;
@@ -391,8 +419,8 @@ __global__ __launch_bounds__(256) void k_split(sssp_args<V, E, W> a, int round)
       uint32_t light = 0, heavy = 0;
       W d = W(0);
       if (have) {
-        light = (uint32_t)a.nlight[v];
-        heavy = (uint32_t)(a.off[v + 1] - a.off[v]) - light;
+        light = (uint32_t)(a.pt[kLight].off[v + 1] - a.pt[kLight].off[v]);
+        heavy = (uint32_t)(a.pt[kHeavy].off[v + 1] - a.pt[kHeavy].off[v]);
         d     = a.dist[v];
       }
       route(a, sg, Q, have, v, d, thr, light, heavy, fmin);
@@ -467,29 +495,155 @@ __global__ __launch_bounds__(256) void k_far_split(sssp_args<V, E, W> a, int rou
     int64_t const i = base + threadIdx.x;
     W const d       = i < a.nv ? a.dist[i] : BIG;
     bool const cand = d >= lo && d < thr;
+    if (!cand && d >= thr && d < BIG) fmin = d < fmin ? d : fmin;  // (a vertex without edges only lowers fmin)
+    if (!__any(cand)) continue;
     uint32_t light = 0, heavy = 0;
     if (cand) {
-      light = (uint32_t)a.nlight[i];
-      heavy = (uint32_t)(a.off[i + 1] - a.off[i]) - light;
+      light = (uint32_t)(a.pt[kLight].off[i + 1] - a.pt[kLight].off[i]);
+      heavy = (uint32_t)(a.pt[kHeavy].off[i + 1] - a.pt[kHeavy].off[i]);
     }
     route(a, sg, Q, cand, (V)i, d, thr, light, heavy, fmin);
-    if (!cand && d >= thr && d < BIG && (a.off[i + 1] > a.off[i])) fmin = d < fmin ? d : fmin;
   }
   route_flush(a, sg, Q);
   block_min_far(st, fmin);
 }
 
-// One thread: termination (no near list, no bucket list waiting for its heavy
-// round, no far set).
-template <typename W>
-__global__ void k_sssp_fin(sssp_state<W>* st, int round, int eb)
+// One thread, after the far split: termination (no near list, no bucket list waiting for its heavy
+// round, no far set), and whether the next round pulls: its list's edges above the
+// part's / pull_div (a dense round: a pull reads the part in order and gathers only
+// the frontier sources' distances; a push gathers every destination's).
+template <typename V, typename E, typename W>
+__global__ void k_sssp_fin(sssp_args<V, E, W> a, int round)
 {
+  sssp_state<W>* st = a.st;
   if (st->done) return;
   using U     = typename bits_of<W>::utype;
   int const Q = (round & 1) ^ 1;
+  int const eb = a.eb;
   if (st->phase == kLight && (st->nq[Q][0] >> eb) == 0 && (st->nr[st->rp][0] >> eb) == 0 &&
       st->minfar == (~U(0) >> 1))
     st->done = 1;
+  bool const hvy               = st->phase == kHeavy;
+  unsigned long long const c0  = hvy ? st->nr[st->hl][0] : st->nq[Q][0];
+  unsigned long long const tot = c0 & ((1ull << eb) - 1ull);
+  st->pull = a.pull_div > 0 && tot * (unsigned long long)a.pull_div > (unsigned long long)a.pt[hvy ? kHeavy : kLight].ne;
+}
+
+// A dense round as a pull over the part (the light edges of every row in a light
+// round, the heavy edges in a heavy one), 2048 edges per chunk in order: a row
+// whose distance is above the round's floor (bucket start, or thr for heavy edges:
+// nothing below can improve) takes the smallest dist[u] + w over its edges from
+// frontier sources u (the list's bitmap), and an improvement is one atomicMin per
+// row and chunk (a per-row minimum in LDS first).  A row's edges here are its
+// in-edges: symmetric graphs only.  Block 0 clears the next near counter (as
+// k_relax does on push rounds).
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_pull(sssp_args<V, E, W> a, int round)
+{
+  using B           = typename bits_of<W>::type;
+  sssp_state<W>* st = a.st;
+  if (st->done || !st->pull) return;
+  int const P = round & 1;
+  int const tid    = threadIdx.x;
+  bool const hvy   = st->phase == kHeavy;
+  part_t<V, E, W> const pt = a.pt[hvy ? kHeavy : kLight];
+  uint32_t const* F        = a.fbits[hvy ? 2 + st->hl : P];
+  W const floor_           = hvy ? st->thr : st->old;
+  W const BIG              = std::numeric_limits<W>::max();
+  int64_t const nch        = (pt.ne + kChunk - 1) / kChunk;
+  __shared__ int s_row[kChunk];  // per position: its row (a max-scan of the row starts)
+  __shared__ B s_best[kChunk];   // per row start position: the row's best candidate (bits)
+  __shared__ int s_wmax[4];
+  unsigned long long my_e = 0;
+  for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    int64_t const t0 = c * kChunk;
+    int64_t const t1 = t0 + kChunk < pt.ne ? t0 + kChunk : pt.ne;
+    int64_t const r0 = pt.crow[c];
+    int64_t const r1 = c + 1 < nch ? pt.crow[c + 1] : a.nv - 1;
+    B const binf     = *reinterpret_cast<B const*>(&BIG);
+    for (int p = tid; p < kChunk; p += 256) {
+      s_row[p]  = p == 0 ? (int)(r0 - r0) : -1;
+      s_best[p] = binf;
+    }
+    __syncthreads();
+    for (int64_t r = r0 + 1 + tid; r <= r1; r += 256) {  // rows starting inside the chunk (the last of equal starts wins)
+      int64_t const p = (int64_t)pt.off[r] - t0;
+      if (p > 0 && p < kChunk) atomicMax(&s_row[p], (int)(r - r0));
+    }
+    __syncthreads();
+    {  // inclusive max-scan: thread tid owns positions [8 tid, 8 tid + 8)
+      int m = -1, loc[kPerThread];
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) {
+        int const x = s_row[tid * kPerThread + k];
+        m           = x > m ? x : m;
+        loc[k]      = m;
+      }
+      int pre = m;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int const y = __shfl_up(pre, o, 64);
+        if ((tid & 63) >= o) pre = y > pre ? y : pre;
+      }
+      if ((tid & 63) == 63) s_wmax[tid >> 6] = pre;
+      int excl = __shfl_up(pre, 1, 64);
+      if ((tid & 63) == 0) excl = -1;
+      __syncthreads();
+      for (int w = 0; w < (tid >> 6); ++w) excl = s_wmax[w] > excl ? s_wmax[w] : excl;
+#pragma unroll
+      for (int k = 0; k < kPerThread; ++k) s_row[tid * kPerThread + k] = loc[k] > excl ? loc[k] : excl;
+    }
+    __syncthreads();
+    V u[kPerThread];
+    W w[kPerThread], dv[kPerThread];
+    int rl[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      int const p     = k * 256 + tid;
+      int64_t const t = t0 + p;
+      u[k]            = V(-1);
+      rl[k]           = -1;
+      if (t < t1) {
+        rl[k] = s_row[p];
+        dv[k] = a.dist[r0 + rl[k]];
+        if (dv[k] > floor_) {
+          u[k] = pt.idx[t];
+          w[k] = pt.w[t];
+        }
+      }
+    }
+    bool fr[kPerThread];
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) fr[k] = u[k] >= 0 && ((F[u[k] >> 5] >> (uint32_t(u[k]) & 31u)) & 1u);
+#pragma unroll
+    for (int k = 0; k < kPerThread; ++k) {
+      if (!fr[k]) continue;
+      W const nd = a.dist[u[k]] + w[k];
+      if (nd < a.cutoff && nd < dv[k]) {
+        int64_t const rs = (int64_t)pt.off[r0 + rl[k]] - t0;  // the row's start position in the chunk (0 if before)
+        atomicMin(&s_best[rs > 0 ? rs : 0], *reinterpret_cast<B const*>(&nd));
+      }
+    }
+    if (tid == 0) my_e += (unsigned long long)(t1 - t0);
+    __syncthreads();
+    for (int p = tid; p < kChunk; p += 256) {
+      B const bb = s_best[p];
+      if (bb != binf) {
+        int64_t const v = r0 + s_row[p];
+        W const nd      = *reinterpret_cast<W const*>(&bb);
+        if (nd < a.dist[v]) {
+          atomicMin(reinterpret_cast<B*>(a.dist + v), bb);
+          atomicOr(a.cbits + (v >> 5), 1u << (uint32_t(v) & 31u));
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.trace) {
+    for (int o = 32; o > 0; o >>= 1) my_e += __shfl_xor(my_e, o, 64);
+    int const p = (int)((blockIdx.x * 4 + (tid >> 6)) & 15);
+    if ((tid & 63) == 0 && my_e) atomicAdd(&st->work[p][hvy ? 5 : 4], my_e);
+  }
 }
 
 // One wave: the source (an internal id, -1 when the external id is not a vertex)
@@ -516,8 +670,8 @@ __global__ __launch_bounds__(64) void k_sssp_init(sssp_args<V, E, W> a, V const*
   __shared__ V s_v[1][kStage], s_b[1][kStage];
   __shared__ uint32_t s_dn[1][kStage], s_db[1][kStage];
   split_stages<V> sg{{s_v[0], s_dn[0], 0}, {s_b[0], s_db[0], 0}};
-  uint32_t const light = (uint32_t)a.nlight[s_];
-  uint32_t const heavy = (uint32_t)(a.off[s_ + 1] - a.off[s_]) - light;
+  uint32_t const light = (uint32_t)(a.pt[kLight].off[s_ + 1] - a.pt[kLight].off[s_]);
+  uint32_t const heavy = (uint32_t)(a.pt[kHeavy].off[s_ + 1] - a.pt[kHeavy].off[s_]);
   W fmin               = std::numeric_limits<W>::max();
   route(a, sg, 0, threadIdx.x == 0, s_, W(0), delta, light, heavy, fmin);
   route_flush(a, sg, 0);
@@ -536,77 +690,147 @@ __global__ __launch_bounds__(64) void k_sssp_init(sssp_args<V, E, W> a, V const*
   }
 }
 
-// The adjacency with each row's light edges (w < delta) first, then its heavy ones
-// (each part in the row's order), and the light count per row: a wave per row,
-// ballot compaction, two passes.
+// The light (w < delta) and heavy edges of every row as two CSRs: light counts
+// (a wave per row), their scan (host), then the rows' edges scattered in order.
 template <typename V, typename E, typename W>
-__global__ __launch_bounds__(256) void k_partition_rows(E const* off, V const* idx, W const* wgt, int64_t nv, W delta,
-                                                         V* pidx, W* pw, int* nlight)
+__global__ __launch_bounds__(256) void k_count_light(E const* off, W const* wgt, int64_t nv, W delta, E* nl)
 {
   int const lane = lane_id();
   for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < nv;
        r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
     E const beg = off[r], end = off[r + 1];
-    E out       = beg;
-    for (int pass = 0; pass < 2; ++pass) {
-      for (E base = beg; base < end; base += 64) {
-        E const e     = base + lane;
-        bool const in = e < end;
-        V v           = 0;
-        W w           = W(0);
-        if (in) {
-          v = idx[e];
-          w = wgt[e];
-        }
-        bool const take            = in && ((w < delta) == (pass == 0));
-        unsigned long long const m = __ballot(take);
-        if (take) {
-          E const o = out + (E)__popcll(m & ((1ull << lane) - 1ull));
-          pidx[o]   = v;
-          pw[o]     = w;
-        }
-        out += (E)__popcll(m);
+    E cnt       = 0;
+    for (E base = beg; base < end; base += 64) {
+      E const e = base + lane;
+      cnt += (E)__popcll(__ballot(e < end && wgt[e] < delta));
+    }
+    if (lane == 0) nl[r] = cnt;
+  }
+}
+
+template <typename E>
+__global__ void k_heavy_offsets(E const* off, E const* offL, int64_t n, E* offH)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    offH[i] = off[i] - offL[i];
+}
+
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_scatter_parts(E const* off, V const* idx, W const* wgt, int64_t nv, W delta,
+                                                        E const* offL, E const* offH, V* idxL, W* wL, V* idxH,
+                                                        W* wH)
+{
+  int const lane = lane_id();
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < nv;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    E const beg = off[r], end = off[r + 1];
+    E oL = offL[r], oH = offH[r];
+    for (E base = beg; base < end; base += 64) {
+      E const e     = base + lane;
+      bool const in = e < end;
+      V v           = 0;
+      W w           = W(0);
+      if (in) {
+        v = idx[e];
+        w = wgt[e];
       }
-      if (pass == 0 && lane == 0) nlight[r] = (int)(out - beg);
+      bool const lt               = in && w < delta;
+      unsigned long long const ml = __ballot(lt), mh = __ballot(in && !lt);
+      unsigned long long const below = (1ull << lane) - 1ull;
+      if (lt) {
+        E const o = oL + (E)__popcll(ml & below);
+        idxL[o]   = v;
+        wL[o]     = w;
+      } else if (in) {
+        E const o = oH + (E)__popcll(mh & below);
+        idxH[o]   = v;
+        wH[o]     = w;
+      }
+      oL += (E)__popcll(ml);
+      oH += (E)__popcll(mh);
     }
   }
 }
 
-// Predecessors by a pull over the in-edges (sorted ascending): a 16-lane group per
-// vertex walks its in-neighbours 16 at a time and stops at the first u with
-// dist[u] + w == dist[v] -- the smallest tight in-neighbour.  -1 for the source and
-// unreached vertices.
+// the row holding edge c * kChunk of a CSR, for every chunk c
+template <typename E>
+__global__ void k_chunk_rows(E const* off, int64_t nv, int64_t* crow)
+{
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nv; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const b = (int64_t)off[r], e = (int64_t)off[r + 1];
+    for (int64_t c = (b + kChunk - 1) / kChunk; c * kChunk < e; ++c) crow[c] = r;
+  }
+}
+
+// Predecessors by a pull over the in-edges (sorted ascending): the first -- the
+// smallest-id -- in-neighbour u with dist[u] + w == dist[v]; -1 for the source and
+// unreached vertices.  k_sssp_pred_probe: a lane per vertex tests its first 4
+// in-edges with every load issued at once (ids descend by degree, so a vertex's
+// first neighbours are its hubs, usually the tight ones) and marks the rest kMiss;
+// k_sssp_pred_scan: a 16-lane group per marked vertex walks the list from the 5th
+// edge on, 16 at a time.
+constexpr int kPredProbe = 4;
+
 template <typename V, typename E, typename W>
-__global__ __launch_bounds__(256) void k_sssp_pred(E const* off, V const* idx, W const* wgt, W const* dist, int64_t nv,
-                                                   V const* src, V* pred)
+__global__ __launch_bounds__(256) void k_sssp_pred_probe(E const* off, V const* idx, W const* wgt, W const* dist,
+                                                         int64_t nv, V const* src, V* pred)
+{
+  V const s_  = *src;
+  W const BIG = std::numeric_limits<W>::max();
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    W const dv      = dist[v];
+    bool const want = (V)v != s_ && dv != BIG;
+    E beg = 0, end = 0;
+    if (want) {
+      beg = off[v];
+      end = off[v + 1];
+    }
+    V u[kPredProbe];
+    W w[kPredProbe];
+#pragma unroll
+    for (int k = 0; k < kPredProbe; ++k) {
+      bool const in = want && beg + k < end;
+      u[k]          = in ? idx[beg + k] : V(-1);
+      w[k]          = in ? wgt[beg + k] : W(0);
+    }
+    W du[kPredProbe];
+#pragma unroll
+    for (int k = 0; k < kPredProbe; ++k) du[k] = u[k] >= 0 ? dist[u[k]] : BIG;
+    V found = V(-1);
+#pragma unroll
+    for (int k = kPredProbe - 1; k >= 0; --k)
+      if (u[k] >= 0 && (W)(du[k] + w[k]) == dv) found = u[k];
+    pred[v] = want && found < 0 && end - beg > kPredProbe ? V(-2) : found;
+  }
+}
+
+template <typename V, typename E, typename W>
+__global__ __launch_bounds__(256) void k_sssp_pred_scan(E const* off, V const* idx, W const* wgt, W const* dist,
+                                                        int64_t nv, V* pred)
 {
   int const lane = threadIdx.x & 15;
   int const gsh  = threadIdx.x & 48;  // the group's first lane within the wave
-  V const s_     = *src;
-  W const BIG    = std::numeric_limits<W>::max();
   for (int64_t v0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; v0 < nv;
        v0 += ((int64_t)gridDim.x * blockDim.x) >> 4) {
-    V const v  = (V)v0;
-    W const dv = dist[v];
-    V found    = V(-1);
-    if (v != s_ && dv != BIG) {
-      E const beg = off[v], end = off[v + 1];
-      for (E base = beg; base < end; base += 16) {
-        E const e  = base + lane;
-        bool tight = false;
-        V u        = 0;
-        if (e < end) {
-          u     = idx[e];
-          tight = (W)(dist[u] + wgt[e]) == dv;
-        }
-        unsigned long long const m = (__ballot(tight) >> gsh) & 0xffffull;
-        if (m) {
-          found = __shfl(u, gsh + __ffsll((long long)m) - 1, 64);
-          break;
-        }
+    if (pred[v0] != V(-2)) continue;
+    W const dv  = dist[v0];
+    E const beg = off[v0] + kPredProbe, end = off[v0 + 1];
+    V found     = V(-1);
+    for (E base = beg; base < end; base += 16) {
+      E const e  = base + lane;
+      bool tight = false;
+      V u        = 0;
+      if (e < end) {
+        u     = idx[e];
+        tight = (W)(dist[u] + wgt[e]) == dv;
+      }
+      unsigned long long const m = (__ballot(tight) >> gsh) & 0xffffull;
+      if (m) {
+        found = __shfl(u, gsh + __ffsll((long long)m) - 1, 64);
+        break;
       }
     }
-    if (lane == 0) pred[v] = found;
+    if (lane == 0) pred[v0] = found;
   }
 }
 
@@ -691,16 +915,45 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   double const avg_deg = (double)ne / (double)nv;
   double const dscale  = h.tune.sssp_delta > 0 ? h.tune.sssp_delta : kDeltaScale;
   W const delta        = (W)std::max(avg_deg > 0 ? dscale * avg_w / avg_deg : 1.0, 1e-30);
-  // the light-first adjacency for this delta (cached on the adjacency)
+  // the light and heavy CSRs for this delta (cached on the adjacency)
   if (adj.sssp_delta != (double)delta) {
-    adj.sssp_idx.set_stream(s);
-    adj.sssp_w.set_stream(s);
-    adj.sssp_nlight.set_stream(s);
-    adj.sssp_idx.resize(std::max<size_t>(ne, 1) * sizeof(V));
-    adj.sssp_w.resize(std::max<size_t>(ne, 1) * sizeof(W));
-    adj.sssp_nlight.resize((size_t)nv * sizeof(int));
-    hipLaunchKernelGGL((k_partition_rows<V, E, W>), dim3(grid_for((size_t)nv * 64, 256, 16384)), dim3(256), 0, s, off,
-                       idx, wgt, nv, delta, adj.sssp_idx.data<V>(), adj.sssp_w.data<W>(), adj.sssp_nlight.data<int>());
+    for (buffer* b : {&adj.sssp_offL, &adj.sssp_offH, &adj.sssp_idxL, &adj.sssp_wL, &adj.sssp_idxH, &adj.sssp_wH,
+                      &adj.sssp_crowL, &adj.sssp_crowH})
+      b->set_stream(s);
+    adj.sssp_offL.resize((size_t)(nv + 1) * sizeof(E));
+    adj.sssp_offH.resize((size_t)(nv + 1) * sizeof(E));
+    E* offL = adj.sssp_offL.data<E>();
+    E* offH = adj.sssp_offH.data<E>();
+    {
+      dbuf<E> nl(nv + 1, s);
+      HIP_CHECK(hipMemsetAsync(nl.data() + nv, 0, sizeof(E), s));
+      hipLaunchKernelGGL((k_count_light<V, E, W>), dim3(grid_for((size_t)nv * 64, 256, 16384)), dim3(256), 0, s, off,
+                         wgt, nv, delta, nl.data());
+      CGX_LAUNCH_CHECK();
+      exclusive_scan<E, E>(nl.data(), offL, (size_t)nv + 1, s);
+    }
+    hipLaunchKernelGGL(k_heavy_offsets<E>, dim3(grid_for((size_t)nv + 1, kBlock, 8192)), dim3(kBlock), 0, s, off, offL,
+                       nv + 1, offH);
+    CGX_LAUNCH_CHECK();
+    E eL = 0;
+    HIP_CHECK(hipMemcpyAsync(&eL, offL + nv, sizeof(E), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    adj.sssp_eL = (int64_t)eL;
+    adj.sssp_eH = (int64_t)ne - (int64_t)eL;
+    adj.sssp_idxL.resize(std::max<int64_t>(adj.sssp_eL, 1) * sizeof(V));
+    adj.sssp_wL.resize(std::max<int64_t>(adj.sssp_eL, 1) * sizeof(W));
+    adj.sssp_idxH.resize(std::max<int64_t>(adj.sssp_eH, 1) * sizeof(V));
+    adj.sssp_wH.resize(std::max<int64_t>(adj.sssp_eH, 1) * sizeof(W));
+    hipLaunchKernelGGL((k_scatter_parts<V, E, W>), dim3(grid_for((size_t)nv * 64, 256, 16384)), dim3(256), 0, s, off,
+                       idx, wgt, nv, delta, offL, offH, adj.sssp_idxL.data<V>(), adj.sssp_wL.data<W>(),
+                       adj.sssp_idxH.data<V>(), adj.sssp_wH.data<W>());
+    CGX_LAUNCH_CHECK();
+    adj.sssp_crowL.resize((size_t)(adj.sssp_eL / kChunk + 2) * sizeof(int64_t));
+    adj.sssp_crowH.resize((size_t)(adj.sssp_eH / kChunk + 2) * sizeof(int64_t));
+    hipLaunchKernelGGL(k_chunk_rows<E>, dim3(grid_for((size_t)nv, kBlock, 8192)), dim3(kBlock), 0, s, offL, nv,
+                       adj.sssp_crowL.data<int64_t>());
+    hipLaunchKernelGGL(k_chunk_rows<E>, dim3(grid_for((size_t)nv, kBlock, 8192)), dim3(kBlock), 0, s, offH, nv,
+                       adj.sssp_crowH.data<int64_t>());
     CGX_LAUNCH_CHECK();
     adj.sssp_delta = (double)delta;
   }
@@ -708,8 +961,10 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   int64_t const nchunk_max = (int64_t)(ne + kChunk - 1) / kChunk + 1;
   dbuf<int> stamp(nv, s);
   fill<int>(stamp.data(), nv, 0, s);
-  dbuf<uint32_t> cbits((nv + 31) / 32, s);
-  HIP_CHECK(hipMemsetAsync(cbits.data(), 0, ((nv + 31) / 32) * sizeof(uint32_t), s));
+  int64_t const nwords = (nv + 31) / 32;
+  dbuf<uint32_t> cbits(nwords, s), fbits(4 * nwords, s);
+  HIP_CHECK(hipMemsetAsync(cbits.data(), 0, nwords * sizeof(uint32_t), s));
+  HIP_CHECK(hipMemsetAsync(fbits.data(), 0, 4 * nwords * sizeof(uint32_t), s));
   dbuf<V> q[4] = {dbuf<V>(nv, s), dbuf<V>(nv, s), dbuf<V>(nv, s), dbuf<V>(nv, s)};
   dbuf<int64_t> ep[4] = {dbuf<int64_t>(nv, s), dbuf<int64_t>(nv, s), dbuf<int64_t>(nv, s), dbuf<int64_t>(nv, s)};
   dbuf<int64_t> cs[4] = {dbuf<int64_t>(nchunk_max, s), dbuf<int64_t>(nchunk_max, s), dbuf<int64_t>(nchunk_max, s),
@@ -717,10 +972,14 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   dbuf<sssp_state<W>> st(1, s);
   HIP_CHECK(hipMemsetAsync(st.data(), 0, sizeof(sssp_state<W>), s));
   sssp_args<V, E, W> a{};
-  a.off    = off;
-  a.idx    = adj.sssp_idx.data<V>();
-  a.wgt    = adj.sssp_w.data<W>();
-  a.nlight = adj.sssp_nlight.data<int>();
+  a.off   = off;
+  a.pt[kLight] = part_t<V, E, W>{adj.sssp_offL.data<E>(), adj.sssp_idxL.data<V>(), adj.sssp_wL.data<W>(),
+                                 adj.sssp_crowL.data<int64_t>(), adj.sssp_eL};
+  a.pt[kHeavy] = part_t<V, E, W>{adj.sssp_offH.data<E>(), adj.sssp_idxH.data<V>(), adj.sssp_wH.data<W>(),
+                                 adj.sssp_crowH.data<int64_t>(), adj.sssp_eH};
+  // a pull reads a row's edges as its in-edges: symmetric graphs only
+  a.pull_div = g.symmetric && h.tune.sssp_pull >= 0 ? (h.tune.sssp_pull > 0 ? h.tune.sssp_pull : kPullDiv) : 0;
+  for (int i = 0; i < 4; ++i) a.fbits[i] = fbits.data() + i * nwords;
   a.dist   = dist;
   a.stamp  = stamp.data();
   a.cutoff = cut;
@@ -741,10 +1000,11 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   while (true) {
     for (int k = 0; k < kChunkRounds; ++k, ++round) {
       hipLaunchKernelGGL((k_relax<V, E, W>), dim3(kRelaxGrid), dim3(256), 0, s, a, round);
+      hipLaunchKernelGGL((k_pull<V, E, W>), dim3(kPullGrid), dim3(256), 0, s, a, round);
       hipLaunchKernelGGL((k_split<V, E, W>), dim3(kSplitGrid), dim3(256), 0, s, a, round);
       hipLaunchKernelGGL(k_sssp_ctl<W>, dim3(1), dim3(1), 0, s, a.st, round, eb);
       hipLaunchKernelGGL((k_far_split<V, E, W>), dim3(kSplitGrid), dim3(256), 0, s, a, round);
-      hipLaunchKernelGGL(k_sssp_fin<W>, dim3(1), dim3(1), 0, s, a.st, round, eb);
+      hipLaunchKernelGGL((k_sssp_fin<V, E, W>), dim3(1), dim3(1), 0, s, a, round);
       CGX_LAUNCH_CHECK();
     }
     HIP_CHECK(hipMemcpyAsync(hs_st, st.data(), sizeof(sssp_state<W>), hipMemcpyDeviceToHost, s));
@@ -754,26 +1014,30 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
   }
   h.last_iterations = (size_t)hs_st->rounds;
   if (trace) {
-    unsigned long long light = 0, heavy = 0, impr = 0, atom = 0;
+    unsigned long long light = 0, heavy = 0, impr = 0, atom = 0, pl = 0, ph = 0;
     for (int p = 0; p < 16; ++p) {
       light += hs_st->work[p][0];
       impr += hs_st->work[p][1];
       atom += hs_st->work[p][2];
       heavy += hs_st->work[p][3];
+      pl += hs_st->work[p][4];
+      ph += hs_st->work[p][5];
     }
     double const E1 = ne ? (double)ne : 1.0;
-    std::fprintf(stderr, "[sssp] V %lld E %zu delta %.6g: %llu rounds (%d enqueued), edges relaxed %.2f E (light %.2f, "
-                 "heavy %.2f), %llu distance atomics (%.3f per edge), %llu improved vertices (%.2f V)\n",
-                 (long long)nv, ne, (double)delta, hs_st->rounds, round, (double)(light + heavy) / E1,
-                 (double)light / E1, (double)heavy / E1, atom, (light + heavy) ? (double)atom / (double)(light + heavy) : 0.0,
-                 impr, (double)impr / (double)nv);
+    std::fprintf(stderr, "[sssp] V %lld E %zu delta %.6g (light part %.3f E): %llu rounds (%d enqueued), pushed "
+                 "light %.2f E heavy %.2f E, pulled light %.2f E heavy %.2f E, %llu push atomics, %llu improved "
+                 "vertices (%.2f V)\n", (long long)nv, ne, (double)delta, (double)adj.sssp_eL / E1, hs_st->rounds,
+                 round, (double)light / E1, (double)heavy / E1, (double)pl / E1, (double)ph / E1, atom, impr,
+                 (double)impr / (double)nv);
   }
   if (want_pred) {
     V* pred = res.predecessors->buf.data<V>();
     // in-edges: a symmetric graph's own rows, else the cached CSC
     adjacency_t& in = g.symmetric ? adj : ensure_adjacency(h, g, true);
-    hipLaunchKernelGGL((k_sssp_pred<V, E, W>), dim3(grid_for((size_t)nv * 16, 256, 16384)), dim3(256), 0, s,
+    hipLaunchKernelGGL((k_sssp_pred_probe<V, E, W>), dim3(grid_for((size_t)nv, 256, 8192)), dim3(256), 0, s,
                        in.offsets.data<E>(), in.indices.data<V>(), in.weights.data<W>(), dist, nv, src_id.data(), pred);
+    hipLaunchKernelGGL((k_sssp_pred_scan<V, E, W>), dim3(grid_for((size_t)nv * 16, 256, 16384)), dim3(256), 0, s,
+                       in.offsets.data<E>(), in.indices.data<V>(), in.weights.data<W>(), dist, nv, pred);
     CGX_LAUNCH_CHECK();
     unrenumber_int_to_ext(h, g, pred, (size_t)nv);
   }

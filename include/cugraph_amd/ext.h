@@ -116,7 +116,7 @@ size_t cugraph_amd_last_iterations(const cugraph_resource_handle_t* handle);
  * mg_chunks, bfs_alpha, bfs_beta, bfs_probe_vec, bfs_head, bfs_res_grid,
  * bfs_probe_grid, bfs_td_cap, louvain_hash, louvain_big_hash, louvain_big_cap,
  * louvain_big_maxdeg, louvain_wide_keys, sssp_delta (0 | scale: delta = scale * average weight /
- * average degree); "defaults" resets them all.  Booleans
+ * average degree), sssp_pull (0 by size | -1 never | n); "defaults" resets them all.  Booleans
  * are 0 / 1.  Unknown names: CUGRAPH_INVALID_INPUT.
  */
 cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t* handle, const char* name, double value,

@@ -3,7 +3,7 @@ bench's weighted R-MAT graph from the first 4 bench roots, for each delta scale
 (handle option sssp_delta: delta = scale * average weight / average degree).
 With CGX_SSSP_TRACE=1 the library prints the rounds, edges relaxed and improvements.
 
-usage: sssp_ab.py SCALE DELTA [DELTA ...]
+usage: sssp_ab.py SCALE DELTA[:PULL] [DELTA[:PULL] ...]   (PULL: option sssp_pull, default 0)
 """
 import os
 import statistics
@@ -23,8 +23,11 @@ def main():
     h = p.ResourceHandle()
     g, roots, _ = bench.build_rmat_graph(p, h, scale, weighted=True, transposed=False, want_roots=8)
     roots = [int(x) for x in roots[:4]]
-    for d in [float(x) for x in sys.argv[2:]]:
+    for arg in sys.argv[2:]:
+        d, pl = (arg.split(":") + ["0"])[:2]
+        d, pl = float(d), int(pl)
         h.set_option("sssp_delta", d)
+        h.set_option("sssp_pull", pl)
         per, rounds = [], []
         for r in roots:
             p.sssp(h, g, r, float("inf"), True, False)  # warm
@@ -38,7 +41,7 @@ def main():
                 del res
             per.append(statistics.median(ts) * 1e3)
             rounds.append(h.last_iterations())
-        print(f"delta scale {d:g}: mean {statistics.mean(per):.3f} ms/traversal, per root "
+        print(f"delta scale {d:g} pull {pl}: mean {statistics.mean(per):.3f} ms/traversal, per root "
               f"{[round(x, 3) for x in per]}, rounds {rounds}", flush=True)
 
 
