@@ -45,6 +45,7 @@
 #include <rocprim/device/device_select.hpp>
 
 #include <limits>
+#include <tuple>
 
 namespace cgx {
 
@@ -60,7 +61,25 @@ struct bfs_rows_t {
   buffer pos;  // uint32 bitmap positions of the neighbours (q * W + local id), ascending per row
                // (+ 16 entries of padding: the probe's vector loads)
   int64_t words = 0;  // 32-bit words of each rank's bitmap segment (max over ranks); W = 32 * words
+  buffer head;        // bottom-up probe's head table (k_mg_head), built by the first direction-optimising call
 };
+
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+constexpr int kHeadN = 3;  // neighbours in the head table (bfs.hip's kHeadN)
+
+// per own vertex 16 bytes: its first kHeadN neighbour positions (the first repeated
+// past the list) and its degree clamped to 32 bits -- the probe reads 16 contiguous
+// bytes per vertex instead of two offsets and a span of the adjacency (bfs.hip)
+__global__ void k_mg_head(int64_t const* off, uint32_t const* pos, int64_t n, v4u_t* head)
+{
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const beg = off[v], deg = off[v + 1] - beg;
+    uint32_t w[kHeadN];
+#pragma unroll
+    for (int t = 0; t < kHeadN; ++t) w[t] = deg > 0 ? pos[beg + (t < deg ? t : 0)] : 0u;
+    head[v] = v4u_t{w[0], w[1], w[2], (uint32_t)std::min<int64_t>(deg, 0xffffffffll)};
+  }
+}
 
 // global id -> position in the allgathered frontier bitmap
 __global__ void k_global_to_pos(uint32_t* ids, int64_t n, int64_t const* voff, int P, int64_t W)
@@ -233,7 +252,8 @@ struct level_ctr {
   unsigned long long next_n;  // own vertices discovered (top-down appends)
   unsigned long long next_m;  // sum of their degrees
   unsigned long long nconv;   // bitmap -> queue conversion appends
-  unsigned long long pad[29];
+  unsigned long long bad;     // sources that are not vertices (k_init_sources)
+  unsigned long long pad[28];
   unsigned long long part[kParts][32];  // bottom-up: [p][0] vertices, [p][1] edges, [p][2] residual sub-queue p
 };
 
@@ -283,17 +303,22 @@ __device__ __forceinline__ void block_add(unsigned long long* dst, unsigned long
   }
 }
 
+// every source (all ranks' lists, gathered; pads -2, unknown ids -1): the owner
+// claims it (frontier count and degree sum into the level counters), every rank
+// counts the unknown ones (the same count on every rank: the same list)
 template <typename V>
 __global__ void k_init_sources(V const* src_global, size_t n, int64_t lo, int64_t hi, V* dist, uint32_t* queue,
-                               unsigned long long* nq, int* flag)
+                               level_ctr* ctr, int* flag, int64_t const* roff)
 {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     int64_t v = (int64_t)src_global[i];
+    if (v == -1) atomicAdd(&ctr->bad, 1ull);
     if (v >= lo && v < hi) {
       int64_t l = v - lo;
       if (atomicCAS(flag + l, 0, 1) == 0) {
-        dist[l]                      = 0;
-        queue[atomicAdd(nq, 1ull)]   = (uint32_t)l;
+        dist[l]                                 = 0;
+        queue[atomicAdd(&ctr->next_n, 1ull)]    = (uint32_t)l;
+        atomicAdd(&ctr->next_m, (unsigned long long)(roff[l + 1] - roff[l]));
       }
     }
   }
@@ -302,13 +327,22 @@ __global__ void k_init_sources(V const* src_global, size_t n, int64_t lo, int64_
 // 2D top-down: frontier = row-local source ids gathered from the row (pads
 // UINT32_MAX); candidate v << gb | parent for every block edge; v is filtered only
 // when it is this rank's own vertex and already visited
+//
+// m: the candidate buffer's length, at least the real count *total (positions past
+// it get the sentinel ~0, which sorts last)
 template <typename V>
 __global__ void k_block_candidates(uint32_t const* frontier, int64_t nf, unsigned long long const* pre, int64_t m,
-                                   int64_t const* off, uint32_t const* idx, int64_t row_lo, int64_t lo, int64_t hi,
-                                   V const* dist, int gb, unsigned long long* out)
+                                   unsigned long long const* total, int64_t const* off, uint32_t const* idx,
+                                   int64_t row_lo, int64_t lo, int64_t hi, V const* dist, int gb,
+                                   unsigned long long* out)
 {
-  V const INF = std::numeric_limits<V>::max();
+  V const INF       = std::numeric_limits<V>::max();
+  int64_t const mr  = (int64_t)*total;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < m; t += (int64_t)gridDim.x * blockDim.x) {
+    if (t >= mr) {
+      out[t] = ~0ull;
+      continue;
+    }
     int64_t a = 0, b = nf - 1;  // last frontier slot with pre <= t
     while (a < b) {
       int64_t mid = (a + b + 1) >> 1;
@@ -384,10 +418,11 @@ __global__ void k_td_claim(unsigned long long const* cand, int64_t n, int64_t lo
 {
   V const INF = std::numeric_limits<V>::max();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t v = (int64_t)(cand[i] >> 32) - lo;
-    long long u = (long long)(uint32_t)cand[i];
-    bool take = false;
-    if (dist[v] == INF) {
+    unsigned long long const x = cand[i];  // ~0: a padded segment's filler
+    int64_t v   = (int64_t)(x >> 32) - lo;
+    long long u = (long long)(uint32_t)x;
+    bool take   = false;
+    if (x != ~0ull && dist[v] == INF) {
       atomicMin(best + v, u);
       take = atomicCAS(flag + v, 0, 1) == 0;
     }
@@ -419,8 +454,9 @@ __global__ void k_scan_total(unsigned long long const* pre, unsigned long long c
   if (threadIdx.x == 0) *out = pre[n - 1] + dg[n - 1];
 }
 
-// a level's (vertices, edges) folded on the device: red[0..1] are then summed over the
-// ranks, red[2] keeps this rank's vertex count (one read-back per level)
+// a level's (vertices, edges) of this rank folded on the device, with the unknown
+// source count: allgathered over the ranks, one read-back per level gives every
+// rank's counts (the totals, and the row's frontier sizes for a top-down level)
 __global__ void k_level_fold(level_ctr const* c, double* red)
 {
   if (threadIdx.x) return;
@@ -431,7 +467,26 @@ __global__ void k_level_fold(level_ctr const* c, double* red)
   }
   red[0] = (double)n;
   red[1] = (double)m;
-  red[2] = (double)n;
+  red[2] = (double)c->bad;
+}
+
+// padded send: destination q's segment [q * m, (q + 1) * m) holds its split range of
+// the expanded candidates, then the filler ~0
+__global__ void k_pad_send(unsigned long long const* cu, int64_t const* pos, int R, int64_t m,
+                           unsigned long long* out)
+{
+  int64_t const n = (int64_t)R * m;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const q = t / m, i = t - q * m;
+    out[t]          = i < pos[q + 1] - pos[q] ? cu[pos[q] + i] : ~0ull;
+  }
+}
+
+// send counts per column owner from the split points (and zero when there are none)
+__global__ void k_pos_counts(int64_t const* pos, int R, int have, int64_t* cnt)
+{
+  int const q = threadIdx.x;
+  if (q < R) cnt[q] = have ? pos[q + 1] - pos[q] : 0;
 }
 
 __global__ void k_mark_bits(uint32_t const* q, int64_t n, uint32_t* bits)
@@ -464,6 +519,13 @@ __device__ __forceinline__ void flush_parts(level_ctr* ctr, unsigned long long n
 }
 
 constexpr int kProbe = 8;  // first neighbours tested per vertex in the probe (bfs.hip: 8 measured best)
+// top-down candidate counts up to this are not read back: the buffer takes the row
+// frontier's degree sum (a bound) and is sorted at that length
+constexpr int64_t kCandRead = int64_t(1) << 17;
+// every column peer's candidate buffer at most this: the column exchange sends padded
+// segments of the buffer's length, known to every rank from the level counts (no
+// count read; at most R * kPadSend * 8 bytes a rank)
+constexpr int64_t kPadSend = 8192;
 
 // the global id of bitmap position x
 __device__ __forceinline__ int64_t pos_to_global(uint32_t x, int64_t const* voff, int64_t W)
@@ -473,15 +535,18 @@ __device__ __forceinline__ int64_t pos_to_global(uint32_t x, int64_t const* voff
 }
 
 // Bottom-up probe: one lane per owned vertex, 64 consecutive vertices per wave.  An
-// unvisited vertex loads its first kProbe neighbour positions and their frontier
-// words back to back and takes the lowest hit (the smallest-global-id frontier
-// neighbour: positions keep the id order).  The wave's next-frontier bits are two
-// whole words of seg_next that no other wave writes (no atomics, no memset); misses
-// of lists longer than kProbe go to residual sub-queue (chunk % kParts).
+// unvisited vertex tests its first kHeadN neighbours from the head table (one
+// 16-byte load), then, on a miss, the next kProbe from the adjacency (three aligned
+// 16-byte loads of the padded position array), every frontier word loaded back to
+// back, and takes the lowest hit (the smallest-global-id frontier neighbour:
+// positions keep the id order).  The wave's next-frontier bits are two whole words
+// of seg_next that no other wave writes (no atomics, no memset); misses of longer
+// lists go to residual sub-queue (chunk % kParts).
 template <typename V>
-__global__ __launch_bounds__(256) void k_mg_bu_probe(int64_t n_own, int64_t const* off, uint32_t const* pos, V* dist,
-                                                      V* pred, uint32_t const* bitmap, int64_t const* voff, int64_t W,
-                                                      V depth1, uint32_t* seg_next, uint32_t* res, level_ctr* ctr)
+__global__ __launch_bounds__(256) void k_mg_bu_probe(int64_t n_own, int64_t const* off, uint32_t const* pos,
+                                                      v4u_t const* head, V* dist, V* pred, uint32_t const* bitmap,
+                                                      int64_t const* voff, int64_t W, V depth1, uint32_t* seg_next,
+                                                      uint32_t* res, level_ctr* ctr)
 {
   V const INF    = std::numeric_limits<V>::max();
   int const lane = threadIdx.x & 63;
@@ -492,29 +557,51 @@ __global__ __launch_bounds__(256) void k_mg_bu_probe(int64_t n_own, int64_t cons
   for (int64_t c = blockIdx.x * (int64_t)(kBlock / 64) + (threadIdx.x >> 6); c < nchunks; c += stride) {
     int64_t const v = (c << 6) + lane;
     bool const un   = v < n_own && dist[v] == INF;
-    int64_t beg = 0, end = 0;
-    if (un) {
-      beg = off[v];
-      end = off[v + 1];
-    }
-    int64_t const deg = end - beg;
+    v4u_t hv        = {0u, 0u, 0u, 0u};
+    if (un) hv = head[v];
+    int64_t const deg = (int64_t)hv.w;
     bool hit = false, more = false;
     uint32_t par = 0;
     if (deg > 0) {
-      uint32_t u[kProbe];
+      uint32_t const u[kHeadN] = {hv.x, hv.y, hv.z};
+      uint32_t fw[kHeadN];
 #pragma unroll
-      for (int t = 0; t < kProbe; ++t) u[t] = pos[beg + (t < deg ? t : 0)];
-      uint32_t fw[kProbe];  // every frontier word first: the loads issue back to back
-#pragma unroll
-      for (int t = 0; t < kProbe; ++t) fw[t] = bitmap[u[t] >> 5];
+      for (int t = 0; t < kHeadN; ++t) fw[t] = bitmap[u[t] >> 5];
       uint32_t hm = 0;
 #pragma unroll
-      for (int t = 0; t < kProbe; ++t) hm |= (t < deg ? (fw[t] >> (u[t] & 31u)) & 1u : 0u) << t;
+      for (int t = 0; t < kHeadN; ++t) hm |= (t < deg ? (fw[t] >> (u[t] & 31u)) & 1u : 0u) << t;
 #pragma unroll
-      for (int t = kProbe - 1; t >= 0; --t)
+      for (int t = kHeadN - 1; t >= 0; --t)
         if ((hm >> t) & 1u) par = u[t];
       hit  = hm != 0;
-      more = !hit && deg > kProbe;
+      more = !hit && deg > kHeadN;
+      if (more) {
+        // the next kProbe positions: the aligned 12-entry span around them (the
+        // position array has kPosPad entries of padding past its end)
+        int64_t const b2  = off[v] + kHeadN;
+        int64_t const a0  = b2 & ~int64_t(3);
+        int const sh      = (int)(b2 - a0);
+        int64_t const rem = deg - kHeadN;
+        v4u_t const* p    = reinterpret_cast<v4u_t const*>(pos + a0);
+        v4u_t const c0 = p[0], c1 = p[1], c2 = p[2];
+        uint32_t const wv[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+        uint32_t w2[kProbe];
+#pragma unroll
+        for (int t = 0; t < kProbe; ++t) w2[t] = sh == 0 ? wv[t] : sh == 1 ? wv[t + 1] : sh == 2 ? wv[t + 2] : wv[t + 3];
+#pragma unroll
+        for (int t = 1; t < kProbe; ++t) w2[t] = t < rem ? w2[t] : w2[0];
+        uint32_t f2[kProbe];
+#pragma unroll
+        for (int t = 0; t < kProbe; ++t) f2[t] = bitmap[w2[t] >> 5];
+        uint32_t h2 = 0;
+#pragma unroll
+        for (int t = 0; t < kProbe; ++t) h2 |= (t < rem ? (f2[t] >> (w2[t] & 31u)) & 1u : 0u) << t;
+#pragma unroll
+        for (int t = kProbe - 1; t >= 0; --t)
+          if ((h2 >> t) & 1u) par = w2[t];
+        hit  = h2 != 0;
+        more = !hit && rem > kProbe;
+      }
     }
     if (hit) {
       dist[v] = depth1;
@@ -537,7 +624,7 @@ __global__ __launch_bounds__(256) void k_mg_bu_probe(int64_t n_own, int64_t cons
   flush_parts(ctr, my_n, my_m);
 }
 
-// Bottom-up residual: 16-lane groups scan the probe's misses from neighbour kProbe on
+// Bottom-up residual: 16-lane groups scan the probe's misses from neighbour kHeadN + kProbe on
 template <typename V>
 __global__ __launch_bounds__(256) void k_mg_bu_residual(int64_t n_own, int64_t const* off, uint32_t const* pos,
                                                          V* dist, V* pred, uint32_t const* bitmap, int64_t const* voff,
@@ -563,7 +650,7 @@ __global__ __launch_bounds__(256) void k_mg_bu_residual(int64_t n_own, int64_t c
     while ((unsigned long long)i >= s_pre[p + 1]) ++p;
     int64_t const v   = res[p * rcap + (i - (int64_t)s_pre[p])];
     int64_t const beg = off[v], end = off[v + 1];
-    for (int64_t base = beg + kProbe; base < end; base += w) {
+    for (int64_t base = beg + kHeadN + kProbe; base < end; base += w) {
       int64_t const e = base + lane;
       bool hit        = false;
       uint32_t u      = 0;
@@ -587,23 +674,43 @@ __global__ __launch_bounds__(256) void k_mg_bu_residual(int64_t n_own, int64_t c
   flush_parts(ctr, my_n, my_m);
 }
 
-// the own frontier bitmap segment -> a list of local ids (bottom-up -> top-down)
-__global__ void k_seg_to_queue(uint32_t const* seg, int64_t nwords, uint32_t* q, unsigned long long* tail)
+// the own frontier bitmap segment -> a list of local ids (bottom-up -> top-down):
+// a lane per word, the block's bit counts scanned in LDS, one tail atomic per block
+// (a wave-serial append per set bit made it 73 us at RMAT-24's largest frontier)
+__global__ __launch_bounds__(256) void k_seg_to_queue(uint32_t const* seg, int64_t nwords, uint32_t* q,
+                                                      unsigned long long* tail)
 {
+  __shared__ unsigned s_w[kBlock / 64];
+  __shared__ unsigned long long s_base;
+  int const lane = threadIdx.x & 63;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += (int64_t)gridDim.x * blockDim.x) {
     int64_t const wi = base + threadIdx.x;
     uint32_t word    = wi < nwords ? seg[wi] : 0u;
-    for (int r = 0; r < 32; ++r) {
-      bool const take = word != 0;
-      if (!__any(take)) break;
-      uint32_t v = 0;
-      if (take) {
-        v = (uint32_t)(wi * 32 + (__ffs(word) - 1));
-        word &= word - 1;
-      }
-      long long const slot = wave_reserve(tail, take);
-      if (take) q[slot] = v;
+    unsigned const c = (unsigned)__popc(word);
+    unsigned x       = c;  // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      unsigned const y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
     }
+    if (lane == 63) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned t = 0;
+      for (int w = 0; w < kBlock / 64; ++w) {
+        unsigned const v = s_w[w];
+        s_w[w]           = t;
+        t += v;
+      }
+      s_base = t ? atomicAdd(tail, (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long o = s_base + s_w[threadIdx.x >> 6] + (x - c);
+    while (word) {
+      q[o++] = (uint32_t)(wi * 32 + (__ffs(word) - 1));
+      word &= word - 1;
+    }
+    __syncthreads();
   }
 }
 
@@ -630,9 +737,19 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   int const P     = mg.P;
   CGX_INPUT(!dir_opt || g.symmetric,
             "Invalid input argument: input graph should be symmetric for direction optimizing BFS.");
-  int64_t nsrc_total = comm.host_allreduce<int64_t>((int64_t)sources->size, CGX_COMM_SUM, s);
+  // every rank's source count (one host read), then every rank sees every source
+  auto const src_counts = comm.host_allgather<int64_t>((int64_t)sources->size, s);
+  int64_t nsrc_total = 0, src_mx = 0;
+  for (auto c : src_counts) nsrc_total += c, src_mx = std::max(src_mx, c);
   CGX_INPUT(nsrc_total > 0, "Invalid input argument: input should have at least one source");
   bfs_rows_t& rows = mg_rows<V>(h, g);
+  if (dir_opt && rows.n_own && rows.head.empty()) {
+    rows.head.set_stream(s);
+    rows.head.resize(rows.n_own * sizeof(v4u_t));
+    hipLaunchKernelGGL(k_mg_head, dim3(blocks(rows.n_own)), dim3(kBlock), 0, s, rows.off.data<int64_t>(),
+                       rows.pos.data<uint32_t>(), rows.n_own, rows.head.data<v4u_t>());
+    CGX_LAUNCH_CHECK();
+  }
   int64_t const n_own = mg.n_own(), lo = mg.voff[mg.p], hi = mg.voff[mg.p + 1];
   V const INF = std::numeric_limits<V>::max();
 
@@ -649,24 +766,23 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   h.last_bfs_levels    = 0;
   h.last_bfs_bottom_up = 0;
 
-  // sources: external -> global ids (collective), then claimed by their owners
-  dbuf<V> srcg(std::max<size_t>(sources->size, 1), s);
-  if (sources->size)
-    HIP_CHECK(hipMemcpyAsync(srcg.data(), sources->data, sources->size * sizeof(V), hipMemcpyDeviceToDevice, s));
-  mg_ext_to_global(h, g, srcg.data(), sources->size, true);
-  std::vector<size_t> rc;
+  // sources: external -> global ids through the replicated id maps (no exchange;
+  // unknown ids become -1, counted by k_init_sources), gathered to every rank (pads
+  // -2), claimed by their owners
   dbuf<V> all_src;
-  {  // every rank sees every source (small)
-    auto counts  = comm.host_allgather<int64_t>((int64_t)sources->size, s);
-    int64_t tot  = 0, mx = 0;
-    for (auto c : counts) tot += c, mx = std::max(mx, c);
-    dbuf<V> pad(std::max<int64_t>(mx, 1), s), gath(std::max<int64_t>(mx * P, 1), s);
-    fill<V>(pad.data(), std::max<int64_t>(mx, 1), (V)-1, s);
-    if (sources->size)
-      HIP_CHECK(hipMemcpyAsync(pad.data(), srcg.data(), sources->size * sizeof(V), hipMemcpyDeviceToDevice, s));
-    comm.allgather<V>(pad.data(), gath.data(), (size_t)std::max<int64_t>(mx, 1), s);
-    all_src = std::move(gath);
-    all_src.n = (size_t)std::max<int64_t>(mx, 1) * P;
+  {
+    int64_t const mx = std::max<int64_t>(src_mx, 1);
+    dbuf<V> pad(mx, s), gath(mx * P, s);
+    fill<V>(pad.data(), mx, (V)-2, s);
+    if (sources->size) {
+      HIP_CHECK(hipMemcpyAsync(pad.data(), sources->data, sources->size * sizeof(V), hipMemcpyDeviceToDevice, s));
+      mg_ext_to_global_local(h, g, pad.data(), sources->size);
+    } else {
+      mg_ensure_replicated_ids(h, g);
+    }
+    comm.allgather<V>(pad.data(), gath.data(), (size_t)mx, s);
+    all_src   = std::move(gath);
+    all_src.n = (size_t)mx * P;
   }
   dbuf<uint32_t> qa(std::max<int64_t>(n_own, 1), s), qb(std::max<int64_t>(n_own, 1), s);
   dbuf<int> flag(std::max<int64_t>(n_own, 1), s);
@@ -676,9 +792,8 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   dbuf<level_ctr> ctr(1, s);
   HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
   hipLaunchKernelGGL(k_init_sources<V>, dim3(blocks(all_src.n)), dim3(kBlock), 0, s, all_src.data(), all_src.n, lo, hi,
-                     dist, qa.data(), &ctr.data()->next_n, flag.data());
+                     dist, qa.data(), ctr.data(), flag.data(), rows.off.data<int64_t>());
   CGX_LAUNCH_CHECK();
-  int64_t nf_own = (int64_t)level_counts(to_host(ctr.data(), 1, s)[0]).first;
 
   dbuf<int64_t> voff_d(P + 1, s);
   HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
@@ -689,29 +804,30 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   dbuf<uint32_t> resq(dir_opt ? std::max<int64_t>(kParts * mg_residual_cap(n_own), 1) : 1, s);
   int64_t const W  = rows.words * 32;
   bool have_queue  = true;   // the own frontier is in qa (else in seg)
-  dbuf<double> scratch(1024, s), dsum(1, s);
-  // m_u: degrees of unvisited vertices (global)
-  double deg_own = 0;
-  if (n_own) {
-    device_sum(deg_sum_f{rows.off.data<int64_t>()}, (size_t)n_own, dsum.data(), scratch.data(), s);
-    deg_own = to_host_scalar(dsum.data(), s);
-  }
-  double m_u = comm.host_allreduce<double>(deg_own, CGX_COMM_SUM, s);
-  double m_f = 0;
-  {
-    // degrees of the initial frontier
-    dbuf<unsigned long long> dg(std::max<int64_t>(nf_own, 1), s);
-    double mf_own = 0;
-    if (nf_own) {
-      hipLaunchKernelGGL(k_frontier_degrees<V>, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own,
-                         rows.off.data<int64_t>(), dg.data());
-      CGX_LAUNCH_CHECK();
-      for (auto x : to_host(dg.data(), nf_own, s)) mf_own += (double)x;
+  // a level's counts: every rank's (vertices, edges, unknown sources) allgathered,
+  // one read: the totals, this rank's and its row's frontier sizes
+  dbuf<double> red(3, s), red_all(3 * (size_t)P, s);
+  std::vector<int64_t> n_of(P, 0), m_of(P, 0);
+  auto fold = [&]() {
+    hipLaunchKernelGGL(k_level_fold, dim3(1), dim3(64), 0, s, ctr.data(), red.data());
+    CGX_LAUNCH_CHECK();
+    comm.allgather<double>(red.data(), red_all.data(), 3, s);
+    auto const gr = to_host(red_all.data(), 3 * (size_t)P, s);
+    int64_t nf_ = 0;
+    double mf_  = 0;
+    for (int q = 0; q < P; ++q) {
+      n_of[q] = (int64_t)gr[3 * q];
+      m_of[q] = (int64_t)gr[3 * q + 1];
+      nf_ += n_of[q];
+      mf_ += gr[3 * q + 1];
     }
-    m_f = comm.host_allreduce<double>(mf_own, CGX_COMM_SUM, s);
-    m_u -= m_f;
-  }
-  int64_t nf = comm.host_allreduce<int64_t>(nf_own, CGX_COMM_SUM, s);
+    return std::make_tuple(nf_, mf_, (int64_t)gr[2]);
+  };
+  auto [nf, m_f, bad_src] = fold();
+  CGX_INPUT(bad_src == 0, "Invalid input argument: vertex id not in the graph");
+  int64_t nf_own = n_of[mg.p];
+  // m_u: degrees of the unvisited vertices (every stored edge once, less the sources')
+  double m_u = (double)g.num_edges - m_f;
   V limit    = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
                                                (unsigned long long)std::numeric_limits<V>::max());
   V depth    = 0;
@@ -746,8 +862,8 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       comm.allgather<uint32_t>(seg.data(), bitmap.data(), (size_t)rows.words, s);
       if (n_own) {
         hipLaunchKernelGGL(k_mg_bu_probe<V>, dim3(grid_for((n_own + 63) / 64, kBlock / 64, 4096)), dim3(kBlock), 0, s,
-                           n_own, rows.off.data<int64_t>(), rows.pos.data<uint32_t>(), dist, pred, bitmap.data(),
-                           voff_d.data(), W, depth1, seg_next.data(), resq.data(), ctr.data());
+                           n_own, rows.off.data<int64_t>(), rows.pos.data<uint32_t>(), rows.head.data<v4u_t>(), dist,
+                           pred, bitmap.data(), voff_d.data(), W, depth1, seg_next.data(), resq.data(), ctr.data());
         CGX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_mg_bu_residual<V>, dim3(1024), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
                            rows.pos.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), W, depth1,
@@ -765,13 +881,17 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
         CGX_LAUNCH_CHECK();
         have_queue = true;
       }
-      // 2D: the row's own frontiers to every rank of the row (row-local source ids)
-      auto row_counts = rowc.host_allgather<int64_t>(nf_own, s);
-      int64_t mx      = 0;
-      for (auto x : row_counts) mx = std::max(mx, x);
+      // 2D: the row's own frontiers to every rank of the row (row-local source ids);
+      // the row's frontier sizes and degree sums are the last level's counts
+      int const row0 = (mg.p / mg.C) * mg.C;
+      int64_t mx = 0, cap = 0;
+      for (int q = row0; q < row0 + mg.C; ++q) {
+        mx = std::max(mx, n_of[q]);
+        cap += m_of[q];  // every candidate edge of the block leaves a row frontier vertex
+      }
       int64_t const nfg = mx * (int64_t)rowc.size;
-      int64_t mcand     = 0;
       dbuf<unsigned long long> tot(1, s);
+      HIP_CHECK(hipMemsetAsync(tot.data(), 0, sizeof(unsigned long long), s));
       dbuf<uint32_t> fsend(std::max<int64_t>(mx, 1), s), fgath(std::max<int64_t>(nfg, 1), s);
       dbuf<unsigned long long> dg(std::max<int64_t>(nfg, 1), s), pre(std::max<int64_t>(nfg, 1), s);
       if (mx) {
@@ -785,16 +905,21 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
         exclusive_scan<unsigned long long, unsigned long long>(dg.data(), pre.data(), nfg, s);
         hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(64), 0, s, pre.data(), dg.data(), nfg, tot.data());
         CGX_LAUNCH_CHECK();
-        mcand = (int64_t)to_host_scalar(tot.data(), s);
       }
+      // the candidate count: below kCandRead the row's degree sum bounds it and the
+      // buffer is sorted at that length (sentinels past the real count) with no host
+      // read; above, the exact count is read (the sort's length then matters more)
+      int64_t mcand = cap;
+      if (mx && cap > kCandRead) mcand = (int64_t)to_host_scalar(tot.data(), s);
+      if (!mx) mcand = 0;
       // candidates over the block, smallest parent per destination
       dbuf<unsigned long long> cand(std::max<int64_t>(mcand, 1), s), cs(std::max<int64_t>(mcand, 1), s),
         cu(std::max<int64_t>(mcand, 1), s);
       dbuf<size_t> cnt(1, s);
       if (mcand) {
         hipLaunchKernelGGL(k_block_candidates<V>, dim3(blocks(mcand)), dim3(kBlock), 0, s, fgath.data(), nfg,
-                           pre.data(), mcand, blk.off.data<int64_t>(), blk.idx.data<uint32_t>(), blk.row_lo, lo, hi,
-                           dist, gb, cand.data());
+                           pre.data(), mcand, tot.data(), blk.off.data<int64_t>(), blk.idx.data<uint32_t>(), blk.row_lo,
+                           lo, hi, dist, gb, cand.data());
         CGX_LAUNCH_CHECK();
         radix_sort_keys<unsigned long long>(cand.data(), cs.data(), mcand, 0, 2 * gb, s);
         size_t tmp = 0;
@@ -806,18 +931,53 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
         CGX_LAUNCH_CHECK();
       }
       // to the destinations' owners: the R ranks of column c (the sentinel run, if
-      // any, sorts last and is dropped)
-      std::vector<size_t> counts(colc.size, 0);
-      if (mcand) {
-        dbuf<int64_t> pos(colc.size + 1, s);
-        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), cnt.data(), colvoff_d.data(), colc.size,
+      // any, sorts last and is dropped).
+      int const Rn = colc.size;
+      dbuf<int64_t> pos(Rn + 1, s);
+      if (mcand)
+        hipLaunchKernelGGL(k_split_points, dim3(1), dim3(64), 0, s, cu.data(), cnt.data(), colvoff_d.data(), Rn,
                            pos.data());
-        CGX_LAUNCH_CHECK();
-        auto hp = to_host(pos.data(), colc.size + 1, s);
-        for (int q = 0; q < colc.size; ++q) counts[q] = (size_t)(hp[q + 1] - hp[q]);
+      // every column peer's buffer length (peer q of the column is in grid row q):
+      // all small -> padded segments, no count read
+      std::vector<int64_t> peer_m(Rn, 0);
+      bool padded = true;
+      for (int q = 0; q < Rn && padded; ++q) {
+        int64_t pmx = 0, pcap = 0;
+        for (int j = 0; j < mg.C; ++j) {
+          pmx = std::max(pmx, n_of[q * mg.C + j]);
+          pcap += m_of[q * mg.C + j];
+        }
+        peer_m[q] = pmx ? pcap : 0;
+        padded    = peer_m[q] <= kPadSend;
       }
-      std::vector<size_t> rcnt;
-      auto got = exchange<int64_t>(colc, reinterpret_cast<int64_t const*>(cu.data()), counts, rcnt, s);
+      std::vector<size_t> counts(Rn), rcnt(Rn);
+      dbuf<unsigned long long> sendp(padded ? std::max<int64_t>((int64_t)Rn * mcand, 1) : 1, s);
+      unsigned long long const* sendv = cu.data();
+      if (padded) {
+        if (mcand) {
+          hipLaunchKernelGGL(k_pad_send, dim3(blocks((int64_t)Rn * mcand)), dim3(kBlock), 0, s, cu.data(), pos.data(),
+                             Rn, mcand, sendp.data());
+          CGX_LAUNCH_CHECK();
+        }
+        sendv = sendp.data();
+        for (int q = 0; q < Rn; ++q) {
+          counts[q] = (size_t)mcand;
+          rcnt[q]   = (size_t)peer_m[q];
+        }
+      } else {
+        // send counts from the split points, their allgather inside the column, one
+        // read for both directions' counts
+        dbuf<int64_t> cnts((size_t)Rn * (Rn + 1), s);
+        hipLaunchKernelGGL(k_pos_counts, dim3(1), dim3(64), 0, s, pos.data(), Rn, mcand ? 1 : 0, cnts.data());
+        CGX_LAUNCH_CHECK();
+        colc.allgather<int64_t>(cnts.data(), cnts.data() + Rn, (size_t)Rn, s);
+        auto const hc = to_host(cnts.data(), (size_t)Rn * (Rn + 1), s);
+        for (int q = 0; q < Rn; ++q) {
+          counts[q] = (size_t)hc[q];
+          rcnt[q]   = (size_t)hc[Rn + (size_t)q * Rn + colc.rank];
+        }
+      }
+      auto got = exchange_known<int64_t>(colc, reinterpret_cast<int64_t const*>(sendv), counts, rcnt, s);
       if (got.n)
         hipLaunchKernelGGL(k_td_claim<V>, dim3(capped(got.n)), dim3(kBlock), 0, s,
                            reinterpret_cast<unsigned long long const*>(got.data()), (int64_t)got.n, lo, dist,
@@ -830,15 +990,9 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       CGX_LAUNCH_CHECK();
       std::swap(qa, qb);
     }
-    dbuf<double> red(3, s);
-    hipLaunchKernelGGL(k_level_fold, dim3(1), dim3(64), 0, s, ctr.data(), red.data());
-    CGX_LAUNCH_CHECK();
-    comm.allreduce<double>(red.data(), red.data(), 2, CGX_COMM_SUM, s);
-    auto gr = to_host(red.data(), 3, s);
-    nf      = (int64_t)gr[0];
-    m_f     = gr[1];
-    nf_own  = (int64_t)gr[2];
-    m_u     = m_u > m_f ? m_u - m_f : 0;
+    std::tie(nf, m_f, std::ignore) = fold();
+    nf_own = n_of[mg.p];
+    m_u    = m_u > m_f ? m_u - m_f : 0;
     ++depth;
     ++levels;
   }
@@ -847,7 +1001,7 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   if (pred) {
     if (n_own) hipLaunchKernelGGL(k_fill_pred_none<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, pred, n_own);
     CGX_LAUNCH_CHECK();
-    mg_global_to_ext(h, g, pred, (size_t)n_own);
+    mg_global_to_ext_local(h, g, pred, (size_t)n_own);
   }
   HIP_CHECK(hipStreamSynchronize(s));
 }

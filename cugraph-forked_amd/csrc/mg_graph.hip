@@ -470,6 +470,96 @@ void mg_global_to_ext(handle_t& h, graph_t& g, void* ids, size_t n)
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
+namespace {
+
+// rank q's slice of the padded allgather (stride mx) -> its global range
+template <typename V>
+__global__ void k_compact_slices(V const* gath, int64_t mx, int64_t const* voff, int P, int64_t V_total, V* out)
+{
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < V_total; g += (int64_t)gridDim.x * blockDim.x) {
+    int const q = mg_owner_of_global(g, voff, P);
+    out[g]      = gath[q * mx + (g - voff[q])];
+  }
+}
+
+template <typename V>
+__global__ void k_global_to_ext_rep(V* x, size_t n, V const* nmap, int64_t V_total)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    int64_t const v = (int64_t)x[i];
+    if (v >= 0 && v < V_total) x[i] = nmap[v];
+  }
+}
+
+template <typename V>
+void ensure_rep_impl(handle_t& h, graph_t& g)
+{
+  mg_graph_t& mg = *g.mg;
+  hipStream_t s  = h.stream;
+  comm_t& comm   = *h.mg->world;
+  int64_t const Vt = g.num_vertices;
+  int64_t mx       = 1;
+  for (int q = 0; q < mg.P; ++q) mx = std::max<int64_t>(mx, mg.voff[q + 1] - mg.voff[q]);
+  dbuf<V> pad(mx, s), gath(mx * mg.P, s);
+  if (mg.n_own())
+    HIP_CHECK(hipMemcpyAsync(pad.data(), g.number_map.data(), mg.n_own() * sizeof(V), hipMemcpyDeviceToDevice, s));
+  comm.allgather<V>(pad.data(), gath.data(), (size_t)mx, s);
+  dbuf<int64_t> voff_d(mg.P + 1, s);
+  HIP_CHECK(hipMemcpyAsync(voff_d.data(), mg.voff.data(), (mg.P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  for (buffer* b : {&mg.rep_nmap, &mg.rep_ext_sorted, &mg.rep_gid}) {
+    b->set_stream(s);
+    b->resize(std::max<int64_t>(Vt, 1) * sizeof(V));
+  }
+  if (Vt) {
+    hipLaunchKernelGGL(k_compact_slices<V>, dim3(blocks(Vt)), dim3(kBlock), 0, s, gath.data(), mx, voff_d.data(),
+                       mg.P, Vt, mg.rep_nmap.data<V>());
+    CGX_LAUNCH_CHECK();
+    dbuf<V> iv(Vt, s);
+    iota<V>(iv.data(), Vt, V(0), s);
+    radix_sort_pairs<V, V>(mg.rep_nmap.data<V>(), mg.rep_ext_sorted.data<V>(), iv.data(), mg.rep_gid.data<V>(), Vt, 0,
+                           8 * sizeof(V), s);
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  mg.rep_valid = true;
+}
+
+}  // namespace
+
+void mg_ensure_replicated_ids(handle_t& h, graph_t& g)
+{
+  if (g.mg->rep_valid) return;
+  if (g.vertex_type == INT32) ensure_rep_impl<int32_t>(h, g);
+  else ensure_rep_impl<int64_t>(h, g);
+}
+
+void mg_global_to_ext_local(handle_t& h, graph_t& g, void* ids, size_t n)
+{
+  mg_ensure_replicated_ids(h, g);
+  if (!n) return;
+  auto run = [&](auto tag) {
+    using V = decltype(tag);
+    hipLaunchKernelGGL(k_global_to_ext_rep<V>, dim3(blocks(n)), dim3(kBlock), 0, h.stream, static_cast<V*>(ids), n,
+                       g.mg->rep_nmap.data<V>(), g.num_vertices);
+    CGX_LAUNCH_CHECK();
+  };
+  if (g.vertex_type == INT32) run(int32_t{});
+  else run(int64_t{});
+}
+
+void mg_ext_to_global_local(handle_t& h, graph_t& g, void* ids, size_t n)
+{
+  mg_ensure_replicated_ids(h, g);
+  if (!n) return;
+  auto run = [&](auto tag) {
+    using V = decltype(tag);
+    hipLaunchKernelGGL(k_answer_ext<V>, dim3(blocks(n)), dim3(kBlock), 0, h.stream, static_cast<V const*>(ids), n,
+                       g.mg->rep_ext_sorted.data<V>(), g.mg->rep_gid.data<V>(), g.num_vertices, static_cast<V*>(ids));
+    CGX_LAUNCH_CHECK();
+  };
+  if (g.vertex_type == INT32) run(int32_t{});
+  else run(int64_t{});
+}
+
 }  // namespace cgx
 
 using namespace cgx;
