@@ -79,6 +79,20 @@ void device_alloc_stats(double* out);  // [5]: driver allocations, their bytes a
 // cached or reused) and the stream is synchronised; the caller frees it with hipFree.
 void* device_forget(void* p, hipStream_t s);
 
+// compute units of the current device (persistent grids: resident blocks per CU x
+// this), queried once per device
+inline int device_cu_count()
+{
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0) d = 0;
+  static int cache[64] = {};
+  if (d < 64 && cache[d] > 0) return cache[d];
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
+  if (d < 64) cache[d] = n;
+  return n;
+}
+
 class buffer {
  public:
   buffer() = default;

@@ -312,7 +312,6 @@ __global__ void k_to_vertex(uint32_t const* x, int64_t n, V* out)
 constexpr int kHashEdges   = 1024;
 constexpr int kHashRows    = 128;  // row arrays 5 KB: 5 blocks per CU
 constexpr int kHashResident = 5;    // resident blocks per CU (the persistent grid)
-constexpr int kCUs          = 256;  // MI355X
 constexpr int kHashSlots   = 2048;
 constexpr int kHashThreads = 256;
 
@@ -1808,8 +1807,9 @@ void sweep(louvain_state& S, level_graph const& g, sweep_plan& P, uint32_t const
                        self, a, P.ag.data(), k, S.m, S.gamma, P.scale, P.inv_scale, next, up_down, own};
     // persistent blocks: the resident count (5 per CU at 30 KB of LDS with fp32 weights,
     // 4 with fp64 weights (registers) or 64-bit keys (38 KB of LDS))
-    unsigned const hg  = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(g.wf ? kHashResident : kHashResident - 1) * kCUs);
-    unsigned const hgw = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(kHashResident - 1) * kCUs);  // 38 KB
+    int64_t const cus  = device_cu_count();
+    unsigned const hg  = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(g.wf ? kHashResident : kHashResident - 1) * cus);
+    unsigned const hgw = (unsigned)std::min<int64_t>(P.nchunks, (int64_t)(kHashResident - 1) * cus);  // 38 KB
     bool const wide = S.tune.louvain_wide_keys;  // tests of the 64-bit keys
     if (g.nv < (1 << 24) - 1 && !wide) {
       if (g.wf) hipLaunchKernelGGL((k_sweep_hash<uint32_t, float>), dim3(hg), dim3(kHashThreads), 0, s, ha);

@@ -519,6 +519,8 @@ __device__ __forceinline__ void flush_parts(level_ctr* ctr, unsigned long long n
 }
 
 constexpr int kProbe = 8;  // first neighbours tested per vertex in the probe (bfs.hip: 8 measured best)
+// bottom-up -> top-down only while more than V / kTdBack vertices are unvisited
+constexpr double kTdBack = 64.0;
 // top-down candidate counts up to this are not read back: the buffer takes the row
 // frontier's degree sum (a bound) and is sorted at that length
 constexpr int64_t kCandRead = int64_t(1) << 17;
@@ -825,7 +827,8 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   };
   auto [nf, m_f, bad_src] = fold();
   CGX_INPUT(bad_src == 0, "Invalid input argument: vertex id not in the graph");
-  int64_t nf_own = n_of[mg.p];
+  int64_t nf_own  = n_of[mg.p];
+  int64_t reached = nf;  // vertices with a distance (global)
   // m_u: degrees of the unvisited vertices (every stored edge once, less the sources')
   double m_u = (double)g.num_edges - m_f;
   V limit    = (V)std::min<unsigned long long>((unsigned long long)depth_limit,
@@ -848,7 +851,14 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   while (nf > 0 && depth < limit) {
     if (dir_opt) {
       if (!bottom_up && m_f > m_u / h.tune.mg_bfs_alpha) bottom_up = true;
-      else if (bottom_up && (double)nf < (double)g.num_vertices / h.tune.mg_bfs_beta) bottom_up = false;
+      // back to top-down (Beamer's beta) only while many vertices are unvisited: a
+      // multi-GPU top-down level costs ~0.1-0.3 ms of small launches and exchanges,
+      // a bottom-up level over the few vertices left of a small-diameter graph
+      // ~20 us (RMAT-24 one rank: 1.45 -> 1.30 ms per traversal); a long-diameter
+      // graph's tail (many levels, most vertices unvisited) still goes top-down
+      else if (bottom_up && (double)nf < (double)g.num_vertices / h.tune.mg_bfs_beta &&
+               (double)(g.num_vertices - reached) > (double)g.num_vertices / kTdBack)
+        bottom_up = false;
     }
     HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
     V const depth1 = depth + 1;
@@ -991,6 +1001,7 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       std::swap(qa, qb);
     }
     std::tie(nf, m_f, std::ignore) = fold();
+    reached += nf;
     nf_own = n_of[mg.p];
     m_u    = m_u > m_f ? m_u - m_f : 0;
     ++depth;
