@@ -54,7 +54,9 @@ out = [
     f"Sources:",
     f"- `profiles/{tag}_bench_n1.json`: the bench line from `python bench.py` (default legs).",
     f"- `profiles/{tag}_bench_kernel_stats.csv`: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-traffic",
-    "  --no-cpu-baseline` (`scripts/gpu_profile_round.sh`). Graph construction is in the trace but in no timed region.",
+    "  --no-cpu-baseline` (`scripts/gpu_round.sh`). Graph construction is in the trace but in no timed region.",
+    f"- `profiles/{tag}_louvain_launches.md`, `profiles/{tag}_sssp_kernels.md`, `profiles/{tag}_pr_launches.csv`: per-launch",
+    "  extracts of the same run's kernel trace (`scripts/round_extracts.py`), where present.",
     "",
     "## PageRank iteration (the roofline kernel pair)",
     "",
