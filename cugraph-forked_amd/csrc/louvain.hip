@@ -2460,12 +2460,14 @@ __global__ void k_mark_used_list(uint32_t const* lab, int64_t n, uint32_t lo, ui
 
 // (l(u), l(v)) -> (new(l(u)) - new_lo, new(l(v))): l(u) is owned (nl_own), l(v)
 // through the looked-up table (keys sorted, values new ids)
+// dense: the new id of every wanted label, indexed by label (k_scatter_table; a
+// binary search over the wanted labels per pair was 7 ms a level at RMAT-24)
 __global__ void k_relabel_pairs_mg(u64 const* keys, int64_t n, uint32_t const* nl_own, uint32_t lo,
-                                   uint32_t const* tk, uint32_t const* tv, int64_t nt, uint32_t new_lo, u64* out)
+                                   uint32_t const* dense, uint32_t new_lo, u64* out)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t const lu = (uint32_t)(keys[i] >> 32), lv = (uint32_t)keys[i];
-    uint32_t const nv = tv[lower_bound_u32(tk, nt, lv)];
+    uint32_t const nv = dense[lv];
     out[i]            = ((u64)(nl_own[lu - lo] - new_lo) << 32) | (u64)nv;
   }
 }
@@ -2474,6 +2476,18 @@ __global__ void k_key_lo(u64 const* keys, int64_t n, uint32_t* out)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (uint32_t)keys[i];
+}
+
+__global__ void k_scatter_table(uint32_t const* tk, uint32_t const* tv, int64_t nt, uint32_t* dense)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nt; i += (int64_t)gridDim.x * blockDim.x)
+    dense[tk[i]] = tv[i];
+}
+
+__global__ void k_lookup_dense(uint32_t* x, int64_t n, uint32_t const* dense)
+{
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = dense[x[i]];
 }
 
 // x[i] -> the value of x[i] in the table (keys sorted, every x present)
@@ -2501,16 +2515,36 @@ int64_t sort_unique_u32(uint32_t const* in, int64_t n, dbuf<uint32_t>& out, int 
 }
 
 // distinct ids through a bitmap of the id range (ids < nv): nv / 8 bytes, where a sort
-// of n keys reads and writes them once per radix pass
-__global__ void k_set_bits(uint32_t const* in, int64_t n, uint32_t* bm)
+// of n keys reads and writes them once per radix pass.  The ids repeat (cluster ids of
+// many vertices), so they are marked as bytes with plain stores (idempotent, no
+// read-modify-write) and packed into the bitmap by a pass over the nv flag bytes: an
+// atomicOr per id serialised on the shared words (0.72 ms a call at RMAT-24; 0.47
+// with a load before each atomic)
+__global__ void k_set_flags(uint32_t const* in, int64_t n, uint8_t* fl)
 {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    atomicOr(bm + (in[i] >> 5), 1u << (in[i] & 31u));
+    fl[in[i]] = 1;
 }
-__global__ void k_word_popc(uint32_t const* bm, int64_t nw, uint32_t* wc)
+// word i of the bitmap from flag bytes [32 i, 32 i + 32) (the flag array is padded to
+// whole words), and its popcount (wc[nw] = 0)
+__global__ void k_flags_to_bits(uint8_t const* fl, int64_t nw, uint32_t* bm, uint32_t* wc)
 {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= nw; i += (int64_t)gridDim.x * blockDim.x)
-    wc[i] = i < nw ? (uint32_t)__popc(bm[i]) : 0u;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= nw; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i == nw) {
+      wc[i] = 0u;
+      continue;
+    }
+    uint4 const* p = reinterpret_cast<uint4 const*>(fl + i * 32);
+    uint4 const a = p[0], b = p[1];
+    uint32_t const w8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t bits        = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bits |= ((w8[k] >> (8 * j)) & 1u) << (4 * k + j);
+    bm[i] = bits;
+    wc[i] = (uint32_t)__popc(bits);
+  }
 }
 __global__ void k_emit_bits(uint32_t const* bm, uint32_t const* wp, int64_t nw, uint32_t* out)
 {
@@ -2538,10 +2572,11 @@ int64_t unique_ranks_bitmap(uint32_t const* in, int64_t n, int64_t nv, dbuf<uint
 {
   int64_t const nw = (nv + 31) / 32;
   dbuf<uint32_t> bm(std::max<int64_t>(nw, 1), s), wc(nw + 1, s), wp(nw + 1, s);
-  fill<uint32_t>(bm.data(), nw, 0u, s);
-  if (n) hipLaunchKernelGGL(k_set_bits, dim3(blocks(n)), dim3(kBlock), 0, s, in, n, bm.data());
+  dbuf<uint8_t> fl(std::max<int64_t>(nw, 1) * 32, s);
+  HIP_CHECK(hipMemsetAsync(fl.data(), 0, (size_t)std::max<int64_t>(nw, 1) * 32, s));
+  if (n) hipLaunchKernelGGL(k_set_flags, dim3(blocks(n)), dim3(kBlock), 0, s, in, n, fl.data());
   CGX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_word_popc, dim3(blocks(nw + 1)), dim3(kBlock), 0, s, bm.data(), nw, wc.data());
+  hipLaunchKernelGGL(k_flags_to_bits, dim3(blocks(nw + 1)), dim3(kBlock), 0, s, fl.data(), nw, bm.data(), wc.data());
   CGX_LAUNCH_CHECK();
   exclusive_scan<uint32_t, uint32_t>(wc.data(), wp.data(), (size_t)(nw + 1), s);
   int64_t const ncl = (int64_t)to_host_scalar(wp.data() + nw, s);
@@ -2904,6 +2939,11 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
   if (nr) HIP_CHECK(hipMemcpyAsync(want.data() + nm, lab_own, nr * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   int64_t const nw = sort_unique_u32(want.data(), nq, wk, lb, s);
   auto wv = collect_by_key<uint32_t>(S, wk.data(), nw, L.voff_d, lo, nl_own.data());
+  // the wanted labels' new ids as a dense table over the level's ids (only wanted
+  // entries are written and read)
+  dbuf<uint32_t> dense(std::max<int64_t>(L.nv, 1), s);
+  if (nw) hipLaunchKernelGGL(k_scatter_table, dim3(blocks(nw)), dim3(kBlock), 0, s, wk.data(), wv.data(), nw, dense.data());
+  CGX_LAUNCH_CHECK();
   level_graph out;
   out.nv    = nvoff[P];
   out.base  = nvoff[p];
@@ -2914,7 +2954,7 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
   out.w.resize(std::max<int64_t>(nm, 1), s);
   if (nm) {
     hipLaunchKernelGGL(k_relabel_pairs_mg, dim3(blocks(nm)), dim3(kBlock), 0, s, mk.data(), nm, nl_own.data(),
-                       (uint32_t)lo, wk.data(), wv.data(), nw, new_lo, mk2.data());
+                       (uint32_t)lo, dense.data(), new_lo, mk2.data());
     CGX_LAUNCH_CHECK();
     if (!radix_sort_pairs_db<u64, double>(mk2.data(), mk.data(), mw.data(), out.w.data(), (size_t)nm, 0,
                                           32 + bits_for(std::max<int64_t>(nu - 1, 0)), s)) {
@@ -2925,7 +2965,7 @@ level_graph mg_contract(louvain_state& S, level_graph const& g, mg_level& L, uin
                        out.dst.data(), /*cb=*/32);
     CGX_LAUNCH_CHECK();
   }
-  if (nr) hipLaunchKernelGGL(k_lookup_u32, dim3(blocks(nr)), dim3(kBlock), 0, s, lab_own, nr, wk.data(), wv.data(), nw);
+  if (nr) hipLaunchKernelGGL(k_lookup_dense, dim3(blocks(nr)), dim3(kBlock), 0, s, lab_own, nr, dense.data());
   CGX_LAUNCH_CHECK();
   voff = nvoff;
   return out;

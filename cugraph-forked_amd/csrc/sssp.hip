@@ -44,7 +44,9 @@
 //  * k_far_split: a dense pass over the distances -- [old, thr) to the near list, the
 //    far set's minimum -- instead of a pile of ids (the reference's far bucket: each
 //    split re-reads every far entry in arbitrary order, 0.3-0.5 ms a split at
-//    RMAT-24); k_sssp_fin: the termination flag and push or pull.
+//    RMAT-24).  Termination is k_sssp_ctl's (nothing left: the round after the last
+//    far split), push or pull each relax kernel's own reading of the list's size
+//    (a one-thread finishing kernel per round was 4-5 us of each ~100 rounds).
 // The state lives in one device block; the host enqueues kChunkRounds rounds and
 // reads the state once per chunk (rounds after termination return at once).  Every
 // grid is fixed and grid-strides over device-side counts.  The light-first copy of
@@ -101,7 +103,7 @@ struct sssp_state {
   W thr, old, delta;
   int fs;     // this round splits the far set
   int phase;  // the next relax: kLight (near list nq[P]) or kHeavy (bucket list nr[hl])
-  int pull;   // the next relax is a pull over the part (dense list)
+  int pad0;
   int rp;     // bucket list receiving this bucket's vertices
   int hl;     // bucket list a heavy round relaxes
   int epoch;  // a vertex joins bucket list rp once per epoch (stamp)
@@ -283,6 +285,19 @@ __device__ __forceinline__ void route_flush(sssp_args<V, E, W> const& a, split_s
   sg.bst.flush(a.bucket[rp], &st->nr[rp][0], a.eb);
 }
 
+// Whether round P's list is relaxed by a pull: its edges above the part's / pull_div
+// (a dense round: a pull reads the part in order and gathers only the frontier
+// sources' distances; a push gathers every destination's).  k_relax and k_pull
+// decide it alike from the same state words (neither changes them before reading).
+template <typename V, typename E, typename W>
+__device__ __forceinline__ bool round_pulls(sssp_args<V, E, W> const& a, sssp_state<W> const* st, int P)
+{
+  bool const hvy               = st->phase == kHeavy;
+  unsigned long long const c0  = hvy ? st->nr[st->hl][0] : st->nq[P][0];
+  unsigned long long const tot = c0 & ((1ull << a.eb) - 1ull);
+  return a.pull_div > 0 && tot * (unsigned long long)a.pull_div > (unsigned long long)a.pt[hvy ? kHeavy : kLight].ne;
+}
+
 // One relax round over a list's edge space, chunk by chunk: the near list's light
 // edges (kLight) or the bucket list's heavy edges (kHeavy).  Block 0 clears the
 // next near counter.
@@ -296,8 +311,9 @@ __global__ __launch_bounds__(256) void k_relax(sssp_args<V, E, W> a, int round)
   int const tid   = threadIdx.x;
   bool const hvy  = st->phase == kHeavy;
   int const hl    = st->hl;
+  bool const pulls = round_pulls(a, st, P);
   if (blockIdx.x == 0 && tid == 0) st->nq[Q][0] = 0;
-  if (st->pull) return;  // (k_pull relaxes this round)
+  if (pulls) return;  // (k_pull relaxes this round)
   part_t<V, E, W> const pt    = a.pt[hvy ? kHeavy : kLight];
   flist<V> const L            = hvy ? a.bucket[hl] : a.near[P];
   unsigned long long const c0 = hvy ? st->nr[hl][0] : st->nq[P][0];
@@ -473,6 +489,11 @@ __global__ void k_sssp_ctl(sssp_state<W>* st, int round, int eb)
       st->fs     = 1;
       st->minfar = inf;  // k_far_split notes the far set's exact minimum past the new thr
       st->epoch += 1;
+    } else {
+      // no near list, no bucket waiting for its heavy round, no far set: done (seen one
+      // round after the far split that emptied the far set: that round's launches
+      // found nothing to do)
+      st->done = 1;
     }
   }
 }
@@ -508,27 +529,6 @@ __global__ __launch_bounds__(256) void k_far_split(sssp_args<V, E, W> a, int rou
   block_min_far(st, fmin);
 }
 
-// One thread, after the far split: termination (no near list, no bucket list waiting for its heavy
-// round, no far set), and whether the next round pulls: its list's edges above the
-// part's / pull_div (a dense round: a pull reads the part in order and gathers only
-// the frontier sources' distances; a push gathers every destination's).
-template <typename V, typename E, typename W>
-__global__ void k_sssp_fin(sssp_args<V, E, W> a, int round)
-{
-  sssp_state<W>* st = a.st;
-  if (st->done) return;
-  using U     = typename bits_of<W>::utype;
-  int const Q = (round & 1) ^ 1;
-  int const eb = a.eb;
-  if (st->phase == kLight && (st->nq[Q][0] >> eb) == 0 && (st->nr[st->rp][0] >> eb) == 0 &&
-      st->minfar == (~U(0) >> 1))
-    st->done = 1;
-  bool const hvy               = st->phase == kHeavy;
-  unsigned long long const c0  = hvy ? st->nr[st->hl][0] : st->nq[Q][0];
-  unsigned long long const tot = c0 & ((1ull << eb) - 1ull);
-  st->pull = a.pull_div > 0 && tot * (unsigned long long)a.pull_div > (unsigned long long)a.pt[hvy ? kHeavy : kLight].ne;
-}
-
 // A dense round as a pull over the part (the light edges of every row in a light
 // round, the heavy edges in a heavy one), 2048 edges per chunk in order: a row
 // whose distance is above the round's floor (bucket start, or thr for heavy edges:
@@ -542,8 +542,8 @@ __global__ __launch_bounds__(256) void k_pull(sssp_args<V, E, W> a, int round)
 {
   using B           = typename bits_of<W>::type;
   sssp_state<W>* st = a.st;
-  if (st->done || !st->pull) return;
   int const P = round & 1;
+  if (st->done || !round_pulls(a, st, P)) return;
   int const tid    = threadIdx.x;
   bool const hvy   = st->phase == kHeavy;
   part_t<V, E, W> const pt = a.pt[hvy ? kHeavy : kLight];
@@ -1004,7 +1004,6 @@ void sssp_impl(handle_t& h, graph_t& g, size_t source, double cutoff, bool want_
       hipLaunchKernelGGL((k_split<V, E, W>), dim3(kSplitGrid), dim3(256), 0, s, a, round);
       hipLaunchKernelGGL(k_sssp_ctl<W>, dim3(1), dim3(1), 0, s, a.st, round, eb);
       hipLaunchKernelGGL((k_far_split<V, E, W>), dim3(kSplitGrid), dim3(256), 0, s, a, round);
-      hipLaunchKernelGGL((k_sssp_fin<V, E, W>), dim3(1), dim3(1), 0, s, a, round);
       CGX_LAUNCH_CHECK();
     }
     HIP_CHECK(hipMemcpyAsync(hs_st, st.data(), sizeof(sssp_state<W>), hipMemcpyDeviceToHost, s));
