@@ -391,6 +391,11 @@ extern "C" cugraph_error_code_t cugraph_sg_graph_create(const cugraph_resource_h
     g->symmetric        = properties ? properties->is_symmetric == TRUE : false;
     g->multigraph       = properties ? properties->is_multigraph == TRUE : false;
     build_sg_graph(*H(handle), *g, *ps, *pd, pw, renumber == TRUE);
+    // check: the reference forwards it to create_graph_from_edgelist
+    // (graph_sg.cpp:161-162), whose expensive_check_edgelist tests only a vertex list
+    // (create_graph_from_edgelist_impl.cuh:71-84, :169-190) -- and the SG C API passes
+    // none (graph_sg.cpp:155: std::nullopt), so on this path it checks nothing there
+    // either; the size and type checks above run regardless
     (void)check;
     *graph = reinterpret_cast<cugraph_graph_t*>(g.release());
   });
