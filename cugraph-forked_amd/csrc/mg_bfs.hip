@@ -457,17 +457,24 @@ __global__ void k_scan_total(unsigned long long const* pre, unsigned long long c
 // a level's (vertices, edges) of this rank folded on the device, with the unknown
 // source count: allgathered over the ranks, one read-back per level gives every
 // rank's counts (the totals, and the row's frontier sizes for a top-down level)
-__global__ void k_level_fold(level_ctr const* c, double* red)
+//
+// The fold is the level's last reader of the counters: it clears them for the next
+// level (one memset launch fewer per level)
+__global__ void k_level_fold(level_ctr* c, double* red)
 {
-  if (threadIdx.x) return;
-  unsigned long long n = c->next_n, m = c->next_m;
-  for (int p = 0; p < kParts; ++p) {
-    n += c->part[p][0];
-    m += c->part[p][1];
+  if (threadIdx.x == 0) {
+    unsigned long long n = c->next_n, m = c->next_m;
+    for (int p = 0; p < kParts; ++p) {
+      n += c->part[p][0];
+      m += c->part[p][1];
+    }
+    red[0] = (double)n;
+    red[1] = (double)m;
+    red[2] = (double)c->bad;
   }
-  red[0] = (double)n;
-  red[1] = (double)m;
-  red[2] = (double)c->bad;
+  __syncthreads();
+  unsigned long long* w = reinterpret_cast<unsigned long long*>(c);
+  for (size_t i = threadIdx.x; i < sizeof(level_ctr) / 8; i += blockDim.x) w[i] = 0ull;
 }
 
 // padded send: destination q's segment [q * m, (q + 1) * m) holds its split range of
@@ -860,8 +867,7 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
                (double)(g.num_vertices - reached) > (double)g.num_vertices / kTdBack)
         bottom_up = false;
     }
-    HIP_CHECK(hipMemsetAsync(ctr.data(), 0, sizeof(level_ctr), s));
-    V const depth1 = depth + 1;
+    V const depth1 = depth + 1;  // (the counters were cleared by the last fold)
     if (bottom_up) {
       if (have_queue) {  // queue -> own bitmap segment
         HIP_CHECK(hipMemsetAsync(seg.data(), 0, rows.words * 4, s));
