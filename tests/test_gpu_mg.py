@@ -90,8 +90,19 @@ def _spawn(fn, args, nprocs, deadline=150.0):
 
 
 def _graph(scale, weighted, seed=5):
+    """RMAT(scale, 16) symmetrised; scale = -k: RMAT(k) with a path of 300 new
+    vertices hung from vertex 1 (a long tail of one-vertex frontiers while most of the
+    path is unvisited: the MG BFS returns to top-down, mg_bfs.hip kTdBack)."""
     from oracle import graph as og
     from oracle import rmat
+    if scale < 0:
+        s, d = rmat.rmat(-scale, 16 << -scale, seed=seed)
+        n0 = 1 << -scale
+        chain = np.arange(n0, n0 + 300, dtype=s.dtype)
+        s = np.concatenate([s, np.array([1], s.dtype), chain[:-1]])
+        d = np.concatenate([d, chain[:1], chain[1:]])
+        w = rmat.rmat_weights(s.size, seed=seed + 1).astype(np.float64) if weighted else None
+        return og.symmetrize_dedup(s, d, w)
     s, d = rmat.rmat(scale, 16 << scale, seed=seed)
     w = rmat.rmat_weights(s.size, seed=seed + 1).astype(np.float64) if weighted else None
     return og.symmetrize_dedup(s, d, w)
@@ -140,6 +151,9 @@ def _worker(rank, world, port, C, scale, weighted, algo, comm="torch"):
         srct = torch.as_tensor(src.astype(np.int32), device="cuda")
         dist_, pred, v = plc.bfs(h, G, srct, algo == "bfs_do", 0, True, False)
         mine = (v.cpu().numpy(), dist_.cpu().numpy(), pred.cpu().numpy())
+        if scale < 0:  # the long tail: bottom-up levels in the core, then top-down ones again
+            lv, bu = h.last_bfs_levels(), h.last_bfs_bottom_up_steps()
+            assert bu > 0 and lv - bu > 250, (lv, bu)
     allr = [None] * world
     dist.all_gather_object(allr, mine)
     if rank == 0:
@@ -185,6 +199,14 @@ def test_mg_pagerank_vs_oracle(world, C, weighted):
                                           (4, 1, "bfs_do")])
 def test_mg_bfs_vs_oracle(world, C, algo):
     _spawn(_worker, (world, _free_port(), C, 12, False, algo), world)
+
+
+@pytest.mark.parametrize("world,C", [(2, 2), (4, 2)])
+def test_mg_bfs_long_tail_returns_to_top_down(world, C):
+    """Direction-optimising MG BFS on RMAT-10 plus a 300-vertex path: bottom-up in the
+    core, then back to top-down for the path (most of it unvisited), distances exact
+    and predecessors valid (mg_bfs_test.cpp rule)."""
+    _spawn(_worker, (world, _free_port(), C, -10, False, "bfs_do"), world)
 
 
 @pytest.mark.parametrize("algo", ["pagerank", "bfs_do"])
