@@ -47,6 +47,7 @@ struct tuning_t {
   double bfs_beta      = 64.0;
   double mg_bfs_alpha  = 40.0;  // multi-GPU BFS direction switch (mg_bfs.hip; one-rank RMAT-24: 40 / 64
   double mg_bfs_beta   = 64.0;  // 2.92 vs Beamer's 14 / 24 3.20 ms per traversal)
+  int mg_bfs_pipelined = 1;     // MG BFS: bottom-up levels enqueued a level ahead, counts read late (mg_bfs.hip bu_state)
   bool bfs_probe_vec   = true;  // bottom-up probe by 16-byte loads
   bool bfs_head        = true;  // bottom-up probe's head table
   int bfs_res_grid     = 1024;  // residual scan blocks

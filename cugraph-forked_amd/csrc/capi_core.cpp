@@ -545,6 +545,7 @@ extern "C" cugraph_error_code_t cugraph_amd_set_option(cugraph_resource_handle_t
     else if (n == "bfs_beta") t.bfs_beta = value;
     else if (n == "mg_bfs_alpha") t.mg_bfs_alpha = value;
     else if (n == "mg_bfs_beta") t.mg_bfs_beta = value;
+    else if (n == "mg_bfs_pipelined") i32(t.mg_bfs_pipelined);
     else if (n == "bfs_probe_vec") b(t.bfs_probe_vec);
     else if (n == "bfs_head") b(t.bfs_head);
     else if (n == "bfs_res_grid") i32(t.bfs_res_grid);

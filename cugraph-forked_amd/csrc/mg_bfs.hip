@@ -551,12 +551,22 @@ __device__ __forceinline__ int64_t pos_to_global(uint32_t x, int64_t const* voff
 // positions keep the id order).  The wave's next-frontier bits are two whole words
 // of seg_next that no other wave writes (no atomics, no memset); misses of longer
 // lists go to residual sub-queue (chunk % kParts).
+//
+// mode (pipelined bottom-up levels, bu_state::mode; null: run): not 1 -> this level
+// was enqueued ahead and is not to run: the own frontier segment (own, the
+// allgathered copy) is copied to seg_next unchanged, so the host's swap keeps it
 template <typename V>
 __global__ __launch_bounds__(256) void k_mg_bu_probe(int64_t n_own, int64_t const* off, uint32_t const* pos,
                                                       v4u_t const* head, V* dist, V* pred, uint32_t const* bitmap,
                                                       int64_t const* voff, int64_t W, V depth1, uint32_t* seg_next,
-                                                      uint32_t* res, level_ctr* ctr)
+                                                      uint32_t* res, level_ctr* ctr, int const* mode,
+                                                      uint32_t const* own, int64_t words)
 {
+  if (mode && *mode != 1) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+      seg_next[i] = own[i];
+    return;
+  }
   V const INF    = std::numeric_limits<V>::max();
   int const lane = threadIdx.x & 63;
   unsigned long long my_n = 0, my_m = 0;
@@ -638,8 +648,9 @@ template <typename V>
 __global__ __launch_bounds__(256) void k_mg_bu_residual(int64_t n_own, int64_t const* off, uint32_t const* pos,
                                                          V* dist, V* pred, uint32_t const* bitmap, int64_t const* voff,
                                                          int64_t W, V depth1, uint32_t* seg_next, uint32_t const* res,
-                                                         level_ctr* ctr)
+                                                         level_ctr* ctr, int const* mode)
 {
+  if (mode && *mode != 1) return;
   constexpr int w = 16;
   int const tid   = threadIdx.x;
   int const lane  = tid & (w - 1);
@@ -721,6 +732,75 @@ __global__ __launch_bounds__(256) void k_seg_to_queue(uint32_t const* seg, int64
     }
     __syncthreads();
   }
+}
+
+// ---------------------------------------------- pipelined bottom-up levels
+// Every bottom-up level has the same fixed-size exchange (the frontier bitmap
+// segments), so once a traversal is bottom-up the host enqueues the next level before
+// it has read the last one's counts: the direction rule runs on the device
+// (k_bu_ctl) and a level enqueued past a switch or the end runs as a no-op (mode !=
+// 1).  The host reads every level's counts one level late.
+struct bu_state {
+  double m_u;      // degree sum of the unvisited vertices (global)
+  double reached;  // vertices with a distance (global)
+  int mode;        // the next level: 1 bottom-up, 0 top-down (the host takes over), 2 done
+  int pad;
+};
+
+constexpr int kPipeMaxP = 64;  // ranks whose counts fit the report (the host path beyond)
+
+struct bu_report {
+  double nf, mf, mu, reached;
+  int mode, skipped, pad[2];
+  double red[3 * kPipeMaxP];  // every rank's (vertices, edges, unknown sources) of the level
+};
+struct bu_reports {
+  bu_report r[2];
+};
+
+__global__ void k_bu_init(bu_state* st, double m_u, double reached)
+{
+  st->m_u     = m_u;
+  st->reached = reached;
+  st->mode    = 1;
+}
+
+// a pipelined level's counts (every rank's, allgathered) -> the next level's mode by the
+// host loop's rule (mg_bfs_impl: back to top-down only below V / beta frontier vertices
+// with more than V / tdback unvisited), reported with the counts; a no-op level
+// reports itself skipped and changes nothing
+__global__ void k_bu_ctl(double const* red_all, int P, bu_state* st, bu_report* rep, double nv, double beta,
+                         double tdback)
+{
+  int const t = threadIdx.x;
+  if (st->mode != 1) {
+    if (t == 0) {
+      rep->skipped = 1;
+      rep->mode    = st->mode;
+    }
+    return;
+  }
+  for (int i = t; i < 3 * P; i += blockDim.x) rep->red[i] = red_all[i];
+  if (t) return;
+  double nf = 0, mf = 0;
+  for (int q = 0; q < P; ++q) {
+    nf += red_all[3 * q];
+    mf += red_all[3 * q + 1];
+  }
+  double const reached = st->reached + nf;
+  double const mu      = st->m_u > mf ? st->m_u - mf : 0.0;
+  int md               = 1;
+  if (nf == 0) md = 2;
+  else if (nf < nv / beta && nv - reached > nv / tdback) md = 0;
+  st->reached  = reached;
+  st->m_u      = mu;
+  st->mode     = md;
+  rep->nf      = nf;
+  rep->mf      = mf;
+  rep->mu      = mu;
+  rep->reached = reached;
+  rep->mode    = md;
+  rep->skipped = 0;
 }
 
 template <typename V>
@@ -855,8 +935,13 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   colvoff[mg.R] = g.num_vertices;
   dbuf<int64_t> colvoff_d(mg.R + 1, s);
   to_device(colvoff_d.data(), colvoff.data(), colvoff.size(), s);
+  bool const pipe_bu = dir_opt && h.tune.mg_bfs_pipelined && P <= kPipeMaxP;
+  dbuf<bu_state> bst(1, s);
+  dbuf<bu_report> brep(2, s);
+  hipEvent_t bev[2] = {nullptr, nullptr};
+  bool decided = false;  // the direction of the next level was set by a pipelined segment's end
   while (nf > 0 && depth < limit) {
-    if (dir_opt) {
+    if (dir_opt && !decided) {
       if (!bottom_up && m_f > m_u / h.tune.mg_bfs_alpha) bottom_up = true;
       // back to top-down (Beamer's beta) only while many vertices are unvisited: a
       // multi-GPU top-down level costs ~0.1-0.3 ms of small launches and exchanges,
@@ -867,7 +952,75 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
                (double)(g.num_vertices - reached) > (double)g.num_vertices / kTdBack)
         bottom_up = false;
     }
+    decided        = false;
     V const depth1 = depth + 1;  // (the counters were cleared by the last fold)
+    if (bottom_up && pipe_bu) {
+      // the rest of the bottom-up run, enqueued a level ahead (see bu_state)
+      if (!bev[0])
+        for (auto& e : bev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      bu_reports* hrep = h.pinned_as<bu_reports>();
+      hipLaunchKernelGGL(k_bu_init, dim3(1), dim3(1), 0, s, bst.data(), m_u, (double)reached);
+      CGX_LAUNCH_CHECK();
+      int const* mode = &bst.data()->mode;
+      auto enqueue = [&](V d1, int slot) {
+        if (have_queue) {  // queue -> own bitmap segment (the segment's first level: nf_own is known)
+          HIP_CHECK(hipMemsetAsync(seg.data(), 0, rows.words * 4, s));
+          if (nf_own)
+            hipLaunchKernelGGL(k_mark_bits, dim3(blocks(nf_own)), dim3(kBlock), 0, s, qa.data(), nf_own, seg.data());
+          CGX_LAUNCH_CHECK();
+          have_queue = false;
+        }
+        comm.allgather<uint32_t>(seg.data(), bitmap.data(), (size_t)rows.words, s);
+        if (n_own) {
+          hipLaunchKernelGGL(k_mg_bu_probe<V>, dim3(grid_for((n_own + 63) / 64, kBlock / 64, 4096)), dim3(kBlock), 0,
+                             s, n_own, rows.off.data<int64_t>(), rows.pos.data<uint32_t>(), rows.head.data<v4u_t>(),
+                             dist, pred, bitmap.data(), voff_d.data(), W, d1, seg_next.data(), resq.data(), ctr.data(),
+                             mode, bitmap.data() + (size_t)mg.p * rows.words, rows.words);
+          CGX_LAUNCH_CHECK();
+          hipLaunchKernelGGL(k_mg_bu_residual<V>, dim3(1024), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
+                             rows.pos.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), W, d1,
+                             seg_next.data(), resq.data(), ctr.data(), mode);
+          CGX_LAUNCH_CHECK();
+        }
+        std::swap(seg, seg_next);
+        hipLaunchKernelGGL(k_level_fold, dim3(1), dim3(64), 0, s, ctr.data(), red.data());
+        CGX_LAUNCH_CHECK();
+        comm.allgather<double>(red.data(), red_all.data(), 3, s);
+        hipLaunchKernelGGL(k_bu_ctl, dim3(1), dim3(64), 0, s, red_all.data(), P, bst.data(), brep.data() + slot,
+                           (double)g.num_vertices, h.tune.mg_bfs_beta, kTdBack);
+        CGX_LAUNCH_CHECK();
+        HIP_CHECK(hipMemcpyAsync(&hrep->r[slot], brep.data() + slot, sizeof(bu_report), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipEventRecord(bev[slot], s));
+      };
+      int slot = 0;
+      enqueue(depth1, slot);
+      while (true) {
+        bool const more = (V)(depth + 1) < limit;  // the level after this one may run
+        if (more) enqueue((V)(depth + 2), slot ^ 1);
+        HIP_CHECK(hipEventSynchronize(bev[slot]));
+        bu_report const& r = hrep->r[slot];  // the level at depth: it ran bottom-up
+        ++levels;
+        ++bu_steps;
+        ++depth;
+        nf      = (int64_t)r.nf;
+        m_f     = r.mf;
+        m_u     = r.mu;
+        reached = (int64_t)r.reached;
+        for (int q = 0; q < P; ++q) {
+          n_of[q] = (int64_t)r.red[3 * q];
+          m_of[q] = (int64_t)r.red[3 * q + 1];
+        }
+        nf_own = n_of[mg.p];
+        if (r.mode != 1 || !more) {
+          if (more) HIP_CHECK(hipEventSynchronize(bev[slot ^ 1]));  // the level enqueued ahead: a no-op
+          bottom_up = r.mode == 1;
+          decided   = true;
+          break;
+        }
+        slot ^= 1;
+      }
+      continue;
+    }
     if (bottom_up) {
       if (have_queue) {  // queue -> own bitmap segment
         HIP_CHECK(hipMemsetAsync(seg.data(), 0, rows.words * 4, s));
@@ -879,11 +1032,12 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
       if (n_own) {
         hipLaunchKernelGGL(k_mg_bu_probe<V>, dim3(grid_for((n_own + 63) / 64, kBlock / 64, 4096)), dim3(kBlock), 0, s,
                            n_own, rows.off.data<int64_t>(), rows.pos.data<uint32_t>(), rows.head.data<v4u_t>(), dist,
-                           pred, bitmap.data(), voff_d.data(), W, depth1, seg_next.data(), resq.data(), ctr.data());
+                           pred, bitmap.data(), voff_d.data(), W, depth1, seg_next.data(), resq.data(), ctr.data(),
+                           nullptr, nullptr, 0);
         CGX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_mg_bu_residual<V>, dim3(1024), dim3(kBlock), 0, s, n_own, rows.off.data<int64_t>(),
                            rows.pos.data<uint32_t>(), dist, pred, bitmap.data(), voff_d.data(), W, depth1,
-                           seg_next.data(), resq.data(), ctr.data());
+                           seg_next.data(), resq.data(), ctr.data(), nullptr);
         CGX_LAUNCH_CHECK();
       }
       std::swap(seg, seg_next);
@@ -1013,6 +1167,8 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
     ++depth;
     ++levels;
   }
+  for (auto& e : bev)
+    if (e) HIP_CHECK(hipEventDestroy(e));
   h.last_bfs_levels    = levels;
   h.last_bfs_bottom_up = bu_steps;
   if (pred) {

@@ -112,7 +112,7 @@ size_t cugraph_amd_last_iterations(const cugraph_resource_handle_t* handle);
  * constexpr; these select the alternatives DESIGN.md measured, for A/B scripts and
  * the bitwise-equality tests).  Names: pr_win_bits (0 | 12 | 13 | 14 | 15), pr_packed,
  * pr_whole, pr_calib, pr_deal_global, pr_unit_w, pr_fuse, pr_enc, pr_hub, pr_band_cut (-1 | 0 | cut),
- * mg_bfs_alpha, mg_bfs_beta, pr_fast_build, pr_share_div (0 | n),
+ * mg_bfs_alpha, mg_bfs_beta, mg_bfs_pipelined (1 | 0), pr_fast_build, pr_share_div (0 | n),
  * mg_chunks, bfs_alpha, bfs_beta, bfs_probe_vec, bfs_head, bfs_res_grid,
  * bfs_probe_grid, bfs_td_cap, louvain_hash, louvain_big_hash, louvain_big_cap,
  * louvain_big_maxdeg, louvain_wide_keys, sssp_delta (0 | scale: delta = scale * average weight /

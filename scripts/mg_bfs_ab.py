@@ -1,6 +1,6 @@
 """Multi-GPU BFS direction thresholds on one rank (measurement aid, not product).
 
-usage: mg_bfs_ab.py SCALE ALPHA,BETA [ALPHA,BETA ...]
+usage: mg_bfs_ab.py SCALE ALPHA,BETA[,PIPELINED] [...]
 The MG BFS code path (2D top-down, 1D bottom-up, csrc/mg_bfs.hip) through a one-rank
 RCCL communicator on the bench's R-MAT graph: ms per traversal (median of 5) from the
 bench's 8 roots for each (mg_bfs_alpha, mg_bfs_beta), with the single-GPU BFS beside it.
@@ -58,11 +58,14 @@ def main():
     try:
         hm = p.ResourceHandle(ctx.ptr)
         gm, _, _ = bench.build_rmat_graph(p, hm, scale, transposed=False, mg=(0, 1))
-        for a, b in settings:
+        for st in settings:
+            a, b = st[0], st[1]
+            pipe = int(st[2]) if len(st) > 2 else 1
             hm.set_option("mg_bfs_alpha", a)
             hm.set_option("mg_bfs_beta", b)
+            hm.set_option("mg_bfs_pipelined", pipe)
             t = time_roots(p, hm, gm, roots)
-            print(f"MG one rank alpha {a:g} beta {b:g}: mean {statistics.mean(t):.3f} ms/traversal, "
+            print(f"MG one rank alpha {a:g} beta {b:g} pipelined {pipe}: mean {statistics.mean(t):.3f} ms/traversal, "
                   f"per root {[round(x, 3) for x in t]}", flush=True)
         gm = None
         hm = None
