@@ -1,0 +1,10 @@
+# SSSP leg (RMAT-24, uniform weights, 4 roots) under handle options, one bench child each
+# usage: TAG=x bash scripts/sssp_opts_ab.sh "opt1=v" "opt2=v,opt3=v" ...
+set -o pipefail
+OUT=gpurun_out/${TAG:-ssspopt}; mkdir -p $OUT
+i=0
+for o in "" "$@"; do
+  i=$((i+1))
+  timeout -k 10 240 python -u bench.py --sssp-only --no-traffic --no-cpu-baseline --options "$o" > $OUT/r$i.json 2> $OUT/r$i.err || exit 1
+  python -c "import json; d=json.load(open('$OUT/r$i.json')); print('[$o]', round(d['ms_mean'],3), d['rounds'])"
+done
