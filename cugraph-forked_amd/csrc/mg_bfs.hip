@@ -804,10 +804,12 @@ __global__ void k_bu_ctl(double const* red_all, int P, bu_state* st, bu_report* 
 }
 
 template <typename V>
-__global__ void k_fill_pred_none(V* pred, int64_t n)
+__global__ void k_pred_to_ext(V* pred, int64_t n, V const* nmap, int64_t nv)
 {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    if (pred[i] == std::numeric_limits<V>::max()) pred[i] = (V)-1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t const p = (int64_t)pred[i];
+    pred[i]         = p >= 0 && p < nv ? nmap[p] : (V)-1;
+  }
 }
 
 struct deg_sum_f {
@@ -1172,9 +1174,12 @@ void mg_bfs_impl(handle_t& h, graph_t& g, array_view_t* sources, bool dir_opt, s
   h.last_bfs_levels    = levels;
   h.last_bfs_bottom_up = bu_steps;
   if (pred) {
-    if (n_own) hipLaunchKernelGGL(k_fill_pred_none<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, pred, n_own);
+    // global parent ids -> external ids through the replicated number map (built for the
+    // sources at the start), unreached -> -1, in one pass
+    if (n_own)
+      hipLaunchKernelGGL(k_pred_to_ext<V>, dim3(blocks(n_own)), dim3(kBlock), 0, s, pred, n_own,
+                         mg.rep_nmap.data<V>(), g.num_vertices);
     CGX_LAUNCH_CHECK();
-    mg_global_to_ext_local(h, g, pred, (size_t)n_own);
   }
   HIP_CHECK(hipStreamSynchronize(s));
 }
